@@ -1,0 +1,230 @@
+/*
+ * gpuagg.h -- C ABI of the MI355X flow-aggregation engine for Retina.
+ *
+ * This is the drop-in boundary that replaces the per-event Go loops of
+ * matmerr/retina's enricher and advanced-metrics module (reference @ 2025-03-28):
+ *
+ *   Enricher.Write / Run / enrich        pkg/enricher/enricher.go:68-140,185-187
+ *   Cache.GetObjByIP (snapshot)          pkg/controllers/cache/cache.go:110-169
+ *   Module.Reconcile / updateMetricsContexts  pkg/module/metrics/metrics_module.go:205-264
+ *   Module.run -> metric.ProcessFlow     pkg/module/metrics/metrics_module.go:276-305
+ *   {Forward,DropCount,TCP,TCPRetrans,DNS}Metrics.ProcessFlow
+ *                                        pkg/module/metrics/{forward,drops,tcpflags,
+ *                                        tcpretrans,dns}.go
+ *   GaugeVec/CounterVec.WithLabelValues  pkg/metrics/interfaces.go:12-20 (the sink)
+ *
+ * The caller is the Go cgo plugin in go/pkg/gpuagg, which keeps
+ * the registry.Plugin interface (pkg/plugin/registry/registry.go:16-34) and feeds the
+ * decoded records of packetparser / dropreason / dns / tcpretrans as column batches.
+ *
+ * Conventions: plain C types only; every entry returns 0 (GPUAGG_OK) or a negative
+ * GPUAGG_E* code and never aborts; gpuagg_last_error() gives the message.  One ctx is
+ * used by one thread at a time; every entry re-binds the ctx's HIP device, so cgo's
+ * OS-thread migration is harmless.
+ */
+#ifndef GPUAGG_H
+#define GPUAGG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPUAGG_ABI_VERSION 1u
+
+/* error codes */
+#define GPUAGG_OK 0
+#define GPUAGG_EINVAL (-1)     /* bad argument / spec                           */
+#define GPUAGG_ENOMEM (-2)     /* host or device allocation failed               */
+#define GPUAGG_EDEVICE (-3)    /* HIP runtime error or no usable gfx950 device   */
+#define GPUAGG_ECAPACITY (-4)  /* a fixed-capacity table overflowed              */
+#define GPUAGG_ESTATE (-5)     /* call not valid in the ctx's current state      */
+#define GPUAGG_EDUPLICATE (-6) /* two metrics would register the same family     */
+#define GPUAGG_ERANGE (-7)     /* value outside the encodable range              */
+
+typedef struct gpuagg_ctx gpuagg_ctx;
+
+/* ------------------------------------------------------------------------------
+ * Configuration
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_config {
+  uint32_t abi_version;          /* = GPUAGG_ABI_VERSION                             */
+  int32_t device;                /* HIP device ordinal                               */
+  int32_t remote_context;        /* cfg.RemoteContext (pkg/config/config.go:72):
+                                    0 = local context, 1 = remote context            */
+  uint32_t max_slots;            /* endpoint identity slots (pods), <= 2^21-2        */
+  uint32_t max_ips;              /* pod IPs in the IP table                          */
+  uint32_t sparse_capacity_log2; /* group-by hash table entries = 2^this (0: 22)     */
+  uint32_t cms_depth;            /* count-min rows (0 = sketches off)                */
+  uint32_t cms_width_log2;       /* count-min columns = 2^this                       */
+  uint32_t hll_precision;        /* HyperLogLog p (registers 2^p per source pod; 0=off) */
+} gpuagg_config;
+
+int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out);
+void gpuagg_destroy(gpuagg_ctx *ctx);
+const char *gpuagg_last_error(const gpuagg_ctx *ctx);
+
+/* ------------------------------------------------------------------------------
+ * Module.Reconcile: one entry per crd MetricsContextOptions
+ * (crd/api/v1alpha1/metricsconfiguration_types.go:27-58).  A *_set flag of 0 means
+ * the Go slice was nil (which changes behaviour, basemetricsobject.go:31-49).
+ * Resets all accumulated state, like Clean() + ResetAdvancedMetricsRegistry()
+ * (metrics_module.go:208-213).
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_metric_options {
+  const char *metric_name;
+  const char *const *source_labels;
+  uint32_t n_source_labels;
+  int32_t source_labels_set;
+  const char *const *destination_labels;
+  uint32_t n_destination_labels;
+  int32_t destination_labels_set;
+} gpuagg_metric_options;
+
+int gpuagg_reconcile(gpuagg_ctx *ctx, const gpuagg_metric_options *opts, size_t n);
+
+/* ------------------------------------------------------------------------------
+ * Endpoint identity (the enricher's view of the IP cache).
+ *
+ * gpuagg_slot_intern returns a stable slot id for the label identity of a pod
+ * (namespace, pod name, first owner reference) -- the fields getEndpoint /
+ * getWorkloads copy into flow.Endpoint (enricher.go:142-183).  workload_kind ==
+ * NULL means the pod has no owner references.  Slot ids are never reused within a
+ * reconcile epoch, so counters keyed by slot stay valid across table swaps.
+ *
+ * gpuagg_set_endpoints replaces the IP -> slot map (a versioned snapshot of
+ * Cache.ipToEpKey/epMap, cache.go:17-46,204-233; services and nodes resolve to no
+ * endpoint, enricher.go:157-160, so they are simply absent).  It takes effect for
+ * batches submitted after the call.  ipv4 values use the record encoding below.
+ * ---------------------------------------------------------------------------- */
+int gpuagg_slot_intern(gpuagg_ctx *ctx, const char *namespace_, const char *pod_name,
+                       const char *workload_kind, const char *workload_name, int32_t *slot);
+int gpuagg_set_endpoints(gpuagg_ctx *ctx, const uint32_t *ipv4, const int32_t *slot, size_t n,
+                         uint64_t version);
+
+/* DNS label payload dictionary (utils.AddDNSInfo, flow_utils.go:186-220): interns
+ * (rcode, qtypes joined with ",", query, ips joined with ",", num_answers) and
+ * returns the id the producer writes into the dns_id column. */
+int gpuagg_dns_intern(gpuagg_ctx *ctx, uint32_t rcode, const char *qtypes_joined,
+                      const char *query, const char *ips_joined, uint32_t num_answers,
+                      uint32_t *dns_id);
+
+/* ------------------------------------------------------------------------------
+ * Records: one decoded flow per row, struct-of-arrays, all uint32.
+ *
+ *  src_ip, dst_ip  IPv4 as the u32 read little-endian from the 4 network-order
+ *                  address bytes (struct packet.src_ip, conntrack.c:37-38; the value
+ *                  utils.Int2ip turns into "a.b.c.d", utils_linux.go:51-55)
+ *  bytes           RetinaMetadata.Bytes (utils.PacketSize, flow_utils.go:267-274)
+ *  meta            bits  0-7  L4 protocol (6 TCP, 17 UDP, other: no L4)
+ *                  bits  8-15 flow.Verdict (1 FORWARDED, 2 DROPPED, 15 RETRANSMISSION,
+ *                             16 DNS; flow_utils.go:19-21)
+ *                  bits 16-17 flow.TrafficDirection (0 UNKNOWN, 1 INGRESS, 2 EGRESS)
+ *                  bits 18-20 RetinaMetadata.DropReason (metadata_linux.pb.go:76-84)
+ *                  bits 21-26 TCP flags FIN,SYN,RST,PSH,ACK,URG (types_linux.go:22-31)
+ *                  bit  27    IsReply
+ *                  bits 28-29 RetinaMetadata.DnsType (0 UNKNOWN, 1 QUERY, 2 RESPONSE)
+ *  ports           source port | destination port << 16 (host order, as in flow.L4)
+ *  dns_id          gpuagg_dns_intern id (DNS verdict rows only; 0xFFFFFFFF reserved)
+ * ports / dns_id may be NULL when no enabled metric reads them.
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_columns {
+  uint32_t *src_ip;
+  uint32_t *dst_ip;
+  uint32_t *bytes;
+  uint32_t *meta;
+  uint32_t *ports;
+  uint32_t *dns_id;
+} gpuagg_columns;
+
+/* Library-owned pinned host batch (the enricher's input ring, enricher.go:45). */
+typedef struct gpuagg_batch {
+  gpuagg_columns cols;
+  size_t capacity;
+} gpuagg_batch;
+
+int gpuagg_alloc_batch(gpuagg_ctx *ctx, size_t capacity, gpuagg_batch **out);
+void gpuagg_free_batch(gpuagg_ctx *ctx, gpuagg_batch *batch);
+
+/* Host-fed submit: copies n rows to HBM and enqueues the aggregation.  Returns once
+ * the batch's host buffers may be refilled; the aggregation itself runs async. */
+int gpuagg_submit(gpuagg_ctx *ctx, gpuagg_batch *batch, size_t n);
+
+/* Device-resident submit: the columns already live in this ctx's device memory. */
+int gpuagg_submit_device(gpuagg_ctx *ctx, const gpuagg_columns *dev_cols, size_t n);
+
+/* Wait for every submitted batch. */
+int gpuagg_sync(gpuagg_ctx *ctx);
+
+/* ------------------------------------------------------------------------------
+ * Output: the Prometheus series the reference's GaugeVec/CounterVec would hold
+ * (names under namespace "networkobservability", prometheusexporter.go:11,46-66).
+ * Values are exact uint64 (the reference's float64 is exact below 2^53).
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_result gpuagg_result;
+
+int gpuagg_snapshot(gpuagg_ctx *ctx, gpuagg_result **out);
+size_t gpuagg_result_count(const gpuagg_result *r);
+int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric,
+                         uint32_t *n_labels, const char *const **label_names,
+                         const char *const **label_values, uint64_t *value);
+void gpuagg_result_free(gpuagg_result *r);
+
+/* ------------------------------------------------------------------------------
+ * Sketches (new; no reference code): count-min over the 5-tuple and HyperLogLog
+ * of distinct destination IPs per source pod.  Estimates read the state of the
+ * last gpuagg_snapshot / gpuagg_sketch_refresh.
+ * ---------------------------------------------------------------------------- */
+int gpuagg_sketch_refresh(gpuagg_ctx *ctx);
+int gpuagg_cms_estimate(gpuagg_ctx *ctx, uint32_t src_ip, uint32_t dst_ip, uint32_t ports,
+                        uint32_t proto, uint64_t *estimate);
+int gpuagg_hll_estimate(gpuagg_ctx *ctx, int32_t slot, double *estimate);
+int gpuagg_cms_copy(gpuagg_ctx *ctx, uint32_t *host_out, size_t n_words);
+int gpuagg_hll_copy(gpuagg_ctx *ctx, uint8_t *host_out, size_t n_bytes);
+
+/* ------------------------------------------------------------------------------
+ * Multi-GPU merge (one process per GPU).  Mergeable device state is exposed so the
+ * caller's collective (RCCL through torch.distributed) can reduce it in place:
+ *   dense counters: sum u64      count-min: sum u32      HLL registers: max u8
+ * The sparse group-by table is exported as a compact entry list, all-gathered by
+ * the caller and imported (insert-or-add) on the merging rank.
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_state_desc {
+  uint64_t *dense_count;   size_t dense_len;    /* u64[dense_len], two arrays */
+  uint64_t *dense_bytes;
+  uint32_t *cms;           size_t cms_len;      /* u32[cms_len]                */
+  uint8_t *hll;            size_t hll_len;      /* u8[hll_len]                 */
+  size_t sparse_entry_words;                    /* u64 words per exported entry */
+} gpuagg_state_desc;
+
+int gpuagg_state(gpuagg_ctx *ctx, gpuagg_state_desc *out);
+/* Compacts the sparse table into dev_out (device u64[cap * sparse_entry_words]);
+ * *n_out = entries written.  GPUAGG_ECAPACITY if cap is too small. */
+int gpuagg_sparse_export(gpuagg_ctx *ctx, uint64_t *dev_out, size_t cap, size_t *n_out);
+/* Inserts-and-adds n exported entries (device pointer) into this ctx's table. */
+int gpuagg_sparse_import(gpuagg_ctx *ctx, const uint64_t *dev_in, size_t n);
+
+/* ------------------------------------------------------------------------------
+ * Introspection
+ * ---------------------------------------------------------------------------- */
+typedef struct gpuagg_stats {
+  uint64_t records;          /* rows submitted                                   */
+  uint64_t batches;          /* batches submitted                                */
+  uint64_t sparse_entries;   /* occupied group-by table entries (at last sync)   */
+  uint64_t sparse_dropped;   /* updates lost to a full group-by table            */
+  uint64_t kernel_launches;  /* timed aggregation launches                       */
+  double kernel_ms;          /* summed device time of timed launches (HIP events) */
+} gpuagg_stats;
+
+int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
+/* Enables HIP-event timing of the aggregation kernel on the ctx's stream. */
+int gpuagg_set_timing(gpuagg_ctx *ctx, int enabled);
+/* Returns the ctx's HIP stream (hipStream_t) as an opaque pointer. */
+void *gpuagg_stream(gpuagg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUAGG_H */

@@ -1,0 +1,115 @@
+"""ctypes declarations of ``include/gpuagg.h`` (the C-ABI boundary).
+
+This is the binding a maintainer would add on the Python side; the Go side's cgo
+binding is in ``go/pkg/gpuagg``.  Loading fails loudly when the
+in-tree library is missing: there is no CPU fallback behind this ABI.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpuagg.so")
+
+ABI_VERSION = 1
+OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE = 0, -1, -2, -3, -4, -5, -6, -7
+ERR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", ECAPACITY: "ECAPACITY",
+             ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE"}
+
+u32p = C.POINTER(C.c_uint32)
+
+
+class Config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("remote_context", C.c_int32),
+                ("max_slots", C.c_uint32), ("max_ips", C.c_uint32),
+                ("sparse_capacity_log2", C.c_uint32), ("cms_depth", C.c_uint32),
+                ("cms_width_log2", C.c_uint32), ("hll_precision", C.c_uint32)]
+
+
+class MetricOptions(C.Structure):
+    _fields_ = [("metric_name", C.c_char_p),
+                ("source_labels", C.POINTER(C.c_char_p)), ("n_source_labels", C.c_uint32),
+                ("source_labels_set", C.c_int32),
+                ("destination_labels", C.POINTER(C.c_char_p)), ("n_destination_labels", C.c_uint32),
+                ("destination_labels_set", C.c_int32)]
+
+
+class Columns(C.Structure):
+    _fields_ = [("src_ip", u32p), ("dst_ip", u32p), ("bytes", u32p), ("meta", u32p),
+                ("ports", u32p), ("dns_id", u32p)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("cols", Columns), ("capacity", C.c_size_t)]
+
+
+class StateDesc(C.Structure):
+    _fields_ = [("dense_count", C.c_void_p), ("dense_len", C.c_size_t),
+                ("dense_bytes", C.c_void_p),
+                ("cms", C.c_void_p), ("cms_len", C.c_size_t),
+                ("hll", C.c_void_p), ("hll_len", C.c_size_t),
+                ("sparse_entry_words", C.c_size_t)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("batches", C.c_uint64), ("sparse_entries", C.c_uint64),
+                ("sparse_dropped", C.c_uint64), ("kernel_launches", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+
+# (name, restype, argtypes) for every entry point declared in include/gpuagg.h
+SIGNATURES = [
+    ("gpuagg_create", C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    ("gpuagg_destroy", None, [C.c_void_p]),
+    ("gpuagg_last_error", C.c_char_p, [C.c_void_p]),
+    ("gpuagg_reconcile", C.c_int, [C.c_void_p, C.POINTER(MetricOptions), C.c_size_t]),
+    ("gpuagg_slot_intern", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                     C.POINTER(C.c_int32)]),
+    ("gpuagg_set_endpoints", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int32), C.c_size_t, C.c_uint64]),
+    ("gpuagg_dns_intern", C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_char_p,
+                                    C.c_uint32, u32p]),
+    ("gpuagg_alloc_batch", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.POINTER(Batch))]),
+    ("gpuagg_free_batch", None, [C.c_void_p, C.POINTER(Batch)]),
+    ("gpuagg_submit", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_size_t]),
+    ("gpuagg_submit_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t]),
+    ("gpuagg_sync", C.c_int, [C.c_void_p]),
+    ("gpuagg_snapshot", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("gpuagg_result_count", C.c_size_t, [C.c_void_p]),
+    ("gpuagg_result_series", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.POINTER(C.c_char_p)),
+                                       C.POINTER(C.POINTER(C.c_char_p)), C.POINTER(C.c_uint64)]),
+    ("gpuagg_result_free", None, [C.c_void_p]),
+    ("gpuagg_sketch_refresh", C.c_int, [C.c_void_p]),
+    ("gpuagg_cms_estimate", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_uint64)]),
+    ("gpuagg_hll_estimate", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double)]),
+    ("gpuagg_cms_copy", C.c_int, [C.c_void_p, u32p, C.c_size_t]),
+    ("gpuagg_hll_copy", C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t]),
+    ("gpuagg_state", C.c_int, [C.c_void_p, C.POINTER(StateDesc)]),
+    ("gpuagg_sparse_export", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("gpuagg_sparse_import", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("gpuagg_get_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    ("gpuagg_set_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("gpuagg_stream", C.c_void_p, [C.c_void_p]),
+]
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load the in-tree engine library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError("retina_amd: %s is missing; run __graft_entry__.build() "
+                          "(there is no CPU fallback)" % path)
+    lib = C.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,151 @@
+// Internal definitions shared by the HIP kernels and the host runtime.
+//
+// Key design (DESIGN.md sections 3-5):
+//  * A metric "group" is one (family, context-options) pair. forward_count and
+//    forward_bytes with the same options share a group: every group accumulates a
+//    count and a byte sum per key, so Inc() and Add(PacketSize) both come out of it
+//    (forward.go:217-224, drops.go:388-395).
+//  * Local-context groups whose label values depend only on the endpoint slot
+//    (options among namespace/podname/workload/service) are DENSE: counters indexed by
+//    (slot, side, sub).  Everything else (remote context, ip/port options, DNS) is
+//    SPARSE: a 192-bit key in an HBM open-addressed table.
+//  * The device groups on a key at least as fine as the label tuple; the host turns
+//    keys into label values and sums equal tuples, so the result is exact.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define GA_HD __host__ __device__ __forceinline__
+#else
+#define GA_HD inline
+#endif
+
+namespace gpuagg {
+
+// ---- record meta word (include/gpuagg.h) -----------------------------------------
+GA_HD uint32_t meta_proto(uint32_t m) { return m & 0xFFu; }
+GA_HD uint32_t meta_verdict(uint32_t m) { return (m >> 8) & 0xFFu; }
+GA_HD uint32_t meta_tdir(uint32_t m) { return (m >> 16) & 3u; }
+GA_HD uint32_t meta_reason(uint32_t m) { return (m >> 18) & 7u; }
+GA_HD uint32_t meta_flags(uint32_t m) { return (m >> 21) & 0x3Fu; }
+GA_HD uint32_t meta_dnstype(uint32_t m) { return (m >> 28) & 3u; }
+
+constexpr uint32_t kVerdictForwarded = 1, kVerdictDropped = 2, kVerdictRetrans = 15,
+                   kVerdictDns = 16;
+constexpr uint32_t kDnsQuery = 1, kDnsResponse = 2;
+// kernel flag bits (pkg/plugin/packetparser/types_linux.go:22-31)
+constexpr uint32_t kFin = 1, kSyn = 2, kRst = 4, kPsh = 8, kAck = 16, kUrg = 32;
+
+// TCP flag label indices, in getFlagValues order (tcpflags.go:134-175).
+enum FlagIdx : uint32_t { F_FIN = 0, F_SYNACK, F_SYN, F_ACK, F_RST, F_PSH, F_URG, F_COUNT };
+
+// Bit set of FlagIdx that getFlagValues returns for a kernel flag byte.
+GA_HD uint32_t flag_label_mask(uint32_t f) {
+  uint32_t m = 0;
+  if (f & kFin) m |= 1u << F_FIN;
+  if ((f & kSyn) && (f & kAck)) {
+    m |= 1u << F_SYNACK;
+  } else {
+    if (f & kSyn) m |= 1u << F_SYN;
+    if (f & kAck) m |= 1u << F_ACK;
+  }
+  if (f & kRst) m |= 1u << F_RST;
+  if (f & kPsh) m |= 1u << F_PSH;
+  if (f & kUrg) m |= 1u << F_URG;
+  return m;
+}
+
+// ---- metric plan -------------------------------------------------------------------
+enum Family : uint8_t {
+  FAM_FWD = 0, FAM_DROP, FAM_TCPFLAGS, FAM_RETRANS, FAM_DNS_REQ, FAM_DNS_RESP, FAM_COUNT
+};
+// Context option bits (types.go:300-327).
+enum Opt : uint8_t {
+  OPT_IP = 1, OPT_NS = 2, OPT_POD = 4, OPT_WL = 8, OPT_SVC = 16, OPT_PORT = 32
+};
+constexpr uint8_t OPT_EP = OPT_NS | OPT_POD | OPT_WL;  // options read from the endpoint
+
+constexpr int kMaxGroups = 16;
+
+struct GroupPlan {
+  uint8_t family;
+  uint8_t sparse;    // 0 dense, 1 sparse
+  uint8_t src_opts;  // local: the single local ctx; remote: source ctx
+  uint8_t dst_opts;  // remote: destination ctx
+  uint32_t nsub;     // dense: sub-bins per (key, side): 1 or 8
+  uint64_t dense_base;
+  uint32_t key_mode;  // dense: 0 constant key, 1 slot key
+  uint32_t pad;
+};
+
+struct Plan {
+  int32_t local;
+  int32_t ngroups;
+  uint32_t need_ports;
+  uint32_t need_dns;
+  GroupPlan g[kMaxGroups];
+};
+
+// ---- hashing -----------------------------------------------------------------------
+GA_HD uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+// IP table: open addressing, linear probing. Entry = ip | slot << 32 | apiserver << 53.
+constexpr uint64_t kIpEmpty = ~0ULL;
+constexpr uint32_t kSlotBits = 21;
+constexpr uint32_t kMaxSlot = (1u << kSlotBits) - 2;  // slot ids 0..kMaxSlot
+GA_HD uint32_t ip_hash(uint32_t ip) { return (uint32_t)fmix64((uint64_t)ip ^ 0x9E3779B97F4A7C15ULL); }
+GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
+  return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
+}
+
+// Sparse group-by key: k0 = occ | group<<59 | sub<<53 | s_slot1<<32 | s_ip
+//                      k1 = s_port17<<47 | d_port17<<30 | d_slot1<<9
+//                      k2 = d_ip<<32 | dns_id
+// sub: bits 5..3 reason or flag index, bits 2..1 traffic direction, bit 0 side (local).
+constexpr uint64_t kKeyOcc = 1ULL << 63;
+constexpr uint64_t kKeyPending = ~0ULL;  // k2 before publication
+GA_HD uint64_t key0(uint32_t group, uint32_t sub, uint32_t s_slot1, uint32_t s_ip) {
+  return kKeyOcc | ((uint64_t)group << 59) | ((uint64_t)sub << 53) | ((uint64_t)s_slot1 << 32) |
+         (uint64_t)s_ip;
+}
+GA_HD uint64_t key1(uint32_t s_port17, uint32_t d_port17, uint32_t d_slot1) {
+  return ((uint64_t)s_port17 << 47) | ((uint64_t)d_port17 << 30) | ((uint64_t)d_slot1 << 9);
+}
+GA_HD uint64_t key2(uint32_t d_ip, uint32_t dns_id) { return ((uint64_t)d_ip << 32) | dns_id; }
+GA_HD uint32_t key_group(uint64_t k0) { return (uint32_t)(k0 >> 59) & 15u; }
+GA_HD uint32_t key_sub(uint64_t k0) { return (uint32_t)(k0 >> 53) & 63u; }
+GA_HD uint32_t key_s_slot1(uint64_t k0) { return (uint32_t)(k0 >> 32) & ((1u << 21) - 1); }
+GA_HD uint32_t key_s_ip(uint64_t k0) { return (uint32_t)k0; }
+GA_HD uint32_t key_s_port17(uint64_t k1) { return (uint32_t)(k1 >> 47) & 0x1FFFFu; }
+GA_HD uint32_t key_d_port17(uint64_t k1) { return (uint32_t)(k1 >> 30) & 0x1FFFFu; }
+GA_HD uint32_t key_d_slot1(uint64_t k1) { return (uint32_t)(k1 >> 9) & ((1u << 21) - 1); }
+GA_HD uint32_t key_d_ip(uint64_t k2) { return (uint32_t)(k2 >> 32); }
+GA_HD uint32_t key_dns(uint64_t k2) { return (uint32_t)k2; }
+GA_HD uint64_t key_hash(uint64_t k0, uint64_t k1, uint64_t k2) {
+  return fmix64(k0 ^ fmix64(k1 ^ fmix64(k2 ^ 0x243F6A8885A308D3ULL)));
+}
+constexpr uint32_t kSparseMaxProbe = 1u << 16;
+constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
+
+// ---- sketches ---------------------------------------------
+constexpr uint64_t kCmsSeed = 0x5EED5EED5EED5EEDULL;
+constexpr uint64_t kCmsRowStep = 0x9E3779B97F4A7C15ULL;
+constexpr uint64_t kHllSeed = 0xA5A5A5A5DEADBEEFULL;
+GA_HD uint64_t cms_base(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
+  const uint64_t lo = (uint64_t)src | ((uint64_t)dst << 32);
+  const uint64_t hi = (uint64_t)ports | ((uint64_t)proto << 32);
+  return fmix64(lo ^ fmix64(hi ^ kCmsSeed));
+}
+GA_HD uint32_t cms_col(uint64_t base, uint32_t row, uint32_t wmask) {
+  return (uint32_t)fmix64(base + (uint64_t)(row + 1) * kCmsRowStep) & wmask;
+}
+GA_HD uint64_t hll_hash(uint32_t dst) { return fmix64((uint64_t)dst ^ kHllSeed); }
+
+}  // namespace gpuagg

@@ -1,0 +1,42 @@
+// Host <-> kernel launch interface (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gpuagg_internal.h"
+
+namespace gpuagg {
+
+struct ColsView {
+  const uint32_t *src_ip, *dst_ip, *bytes, *meta, *ports, *dns_id;
+};
+
+struct SparseView {
+  uint64_t *k0, *k1, *k2, *cnt, *byt;
+  uint32_t mask;
+  uint64_t *dropped;
+};
+
+struct LaunchArgs {
+  ColsView cols;
+  size_t n;
+  const uint64_t *ip_slots;
+  uint32_t ip_mask;
+  Plan plan;
+  uint64_t *dense_cnt, *dense_byt;
+  SparseView sparse;
+  uint32_t *cms;
+  uint32_t cms_depth, cms_wlog2;
+  uint8_t *hll;
+  uint32_t hll_p;
+  uint32_t max_blocks;
+};
+
+hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st);
+hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);
+hipError_t launch_sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t out_cap,
+                                uint64_t *counter, hipStream_t st);
+hipError_t launch_sparse_import(const SparseView &v, const uint64_t *in, size_t n, hipStream_t st);
+
+}  // namespace gpuagg

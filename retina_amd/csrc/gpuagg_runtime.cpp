@@ -1,0 +1,1005 @@
+// Host runtime of the flow-aggregation engine: the C ABI of include/gpuagg.h.
+//
+// Restates, on the host side of the boundary, the parts of the reference that are
+// not per-record work:
+//  * metric registry resolution  -- Module.updateMetricsContexts (metrics_module.go:205-264)
+//    and the constructors / Init of every metric (forward.go:88-118, drops.go:256-286,
+//    tcpflags.go:31-51, tcpretrans.go:210-230, dns.go:340-372)
+//  * label schemas               -- getLabels (types.go:329-365, forward.go:120-142,
+//    drops.go:288-307, tcpflags.go:53-66, tcpretrans.go:232-245, dns.go:374-402)
+//  * label values                -- getByDirectionValues (types.go:418-505), enum names
+//    (metadata_linux.pb.go:87-95), DNSRcodeToString (flow_utils.go:237-257)
+//  * the IP cache snapshot       -- an open-addressed IP -> slot table in HBM
+// Per-record work runs in gpuagg_kernels.hip.
+#include "../../include/gpuagg.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gpuagg_internal.h"
+#include "gpuagg_launch.h"
+
+using namespace gpuagg;
+
+namespace {
+
+const char *kDropReasonNames[7] = {"IPTABLE_RULE_DROP", "IPTABLE_NAT_DROP", "TCP_CONNECT_BASIC",
+                                   "TCP_ACCEPT_BASIC",  "TCP_CLOSE_BASIC",  "CONNTRACK_ADD_DROP",
+                                   "UNKNOWN_DROP"};
+const char *kFlagNames[F_COUNT] = {"FIN", "SYNACK", "SYN", "ACK", "RST", "PSH", "URG"};
+const char *kRcodeNames[6] = {"NOERROR", "FORMERR", "SERVFAIL", "NXDOMAIN", "NOTIMP", "REFUSED"};
+const char *kApiServer = "kubernetes-apiserver";  // pkg/common/types.go:15
+
+std::string drop_reason_name(uint32_t r) { return r < 7 ? kDropReasonNames[r] : std::to_string(r); }
+// cilium flow.TrafficDirection names (parity unpinned: cilium proto not in the reference tree)
+std::string traffic_direction_name(uint32_t t) {
+  switch (t) {
+    case 0: return "TRAFFIC_DIRECTION_UNKNOWN";
+    case 1: return "INGRESS";
+    case 2: return "EGRESS";
+  }
+  return std::to_string(t);
+}
+std::string ip_string(uint32_t ip) {  // utils.Int2ip + net.IP.String()
+  char b[20];
+  snprintf(b, sizeof b, "%u.%u.%u.%u", ip & 255u, (ip >> 8) & 255u, (ip >> 16) & 255u, ip >> 24);
+  return b;
+}
+
+std::string lower(const char *s) {
+  std::string o(s ? s : "");
+  for (auto &c : o) c = (char)tolower((unsigned char)c);
+  return o;
+}
+
+struct SlotAttr {
+  std::string ns, pod, wk_kind, wk_name;
+  bool has_owner = false;
+  bool api = false;
+};
+
+struct DnsAttr {
+  uint32_t rcode, nresp;
+  std::string qtypes, query, ips;
+};
+
+enum ValueKind { VK_COUNT, VK_BYTES };
+
+// One registered metric object (the value type of Module.registry).
+struct Instance {
+  std::string registry_name;  // MetricsContextOptions.MetricName
+  uint8_t family;
+  ValueKind vk;
+  std::string vec_name;  // "networkobservability_adv_..."
+  std::vector<std::string> label_names;
+  bool active;      // emits series (Init created a vector and update() matches)
+  bool adv_enable;  // forward remote: ctx values only when advanced
+  bool has_src, has_dst;
+  uint8_t src_opts, dst_opts;
+  int group;
+};
+
+struct Group {
+  uint8_t family, src_opts, dst_opts;
+  bool sparse;
+  uint32_t nsub, key_mode;
+  uint64_t dense_base, nkeys;
+};
+
+struct Series {
+  std::string metric;
+  std::vector<std::string> names, values;
+  uint64_t value;
+};
+
+}  // namespace
+
+struct gpuagg_result {
+  std::vector<Series> series;
+  std::vector<std::vector<const char *>> name_ptrs, value_ptrs;
+};
+
+struct gpuagg_ctx {
+  gpuagg_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // registry / plan
+  bool remote = false;
+  std::vector<Instance> inst;
+  std::vector<Group> groups;
+  Plan plan{};
+
+  // identity dictionaries
+  std::map<std::tuple<std::string, std::string, std::string, std::string, int>, int32_t> slot_ids;
+  std::vector<SlotAttr> slots;
+  std::unordered_map<std::string, uint32_t> dns_ids;
+  std::vector<DnsAttr> dns;
+
+  // IP table
+  uint64_t *d_ip = nullptr;
+  size_t ip_cap = 0;  // slots
+  uint64_t ip_version = 0;
+
+  // dense counters
+  uint64_t *d_dense_cnt = nullptr, *d_dense_byt = nullptr;
+  size_t dense_len = 0;
+
+  // sparse table
+  SparseView sv{};
+  size_t sparse_slots = 0;
+  uint64_t *d_counter = nullptr;  // export counter
+  uint64_t *d_export = nullptr;
+  size_t export_cap = 0;
+
+  // sketches
+  uint32_t *d_cms = nullptr;
+  size_t cms_len = 0;
+  uint8_t *d_hll = nullptr;
+  size_t hll_len = 0;
+  std::vector<uint32_t> h_cms;
+  std::vector<uint8_t> h_hll;
+
+  // device staging for host-fed batches
+  uint32_t *d_cols[6] = {};
+  size_t staging_cap = 0;
+  std::vector<gpuagg_batch *> batches;
+
+  // stats / timing
+  gpuagg_stats stats{};
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+  uint32_t max_blocks = 2048;
+};
+
+// ------------------------------------------------------------------------------------
+namespace {
+
+int fail(gpuagg_ctx *c, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return fail((c), GPUAGG_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(_e));   \
+  } while (0)
+
+int bind(gpuagg_ctx *c) {
+  HIPCHK(c, hipSetDevice(c->device));
+  return GPUAGG_OK;
+}
+
+template <class T>
+int dev_alloc(gpuagg_ctx *c, T **p, size_t count) {
+  *p = nullptr;
+  if (!count) return GPUAGG_OK;
+  hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+  if (e != hipSuccess)
+    return fail(c, GPUAGG_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+  return GPUAGG_OK;
+}
+template <class T>
+void dev_free(T *&p) {
+  if (p) hipFree((void *)p);
+  p = nullptr;
+}
+
+uint8_t parse_opts(const char *const *labels, uint32_t n) {  // NewCtxOption (types.go:300-327)
+  uint8_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const std::string s = lower(labels[i]);
+    if (s == "ip") o |= OPT_IP;
+    else if (s == "namespace") o |= OPT_NS;
+    else if (s == "podname") o |= OPT_POD;
+    else if (s == "workload") o |= OPT_WL;
+    else if (s == "service") o |= OPT_SVC;
+    else if (s == "port") o |= OPT_PORT;
+  }
+  return o;
+}
+
+void ctx_label_names(uint8_t opts, const char *prefix, std::vector<std::string> &out) {
+  std::string p(prefix);
+  if (opts & OPT_IP) out.push_back(p + "ip");
+  if (opts & OPT_NS) out.push_back(p + "namespace");
+  if (opts & OPT_POD) out.push_back(p + "podname");
+  if (opts & OPT_WL) {
+    out.push_back(p + "workload_kind");
+    out.push_back(p + "workload_name");
+  }
+  if (opts & OPT_SVC) out.push_back(p + "service");
+  if (opts & OPT_PORT) out.push_back(p + "port");
+}
+
+// getByDirectionValues for one side tuple (types.go:418-505).
+void ctx_values(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, uint32_t port17,
+                std::vector<std::string> &out) {
+  const SlotAttr *a = (slot1 && slot1 - 1 < c->slots.size()) ? &c->slots[slot1 - 1] : nullptr;
+  if (opts & OPT_IP) out.push_back(ip_string(ip));
+  if (opts & OPT_NS) out.push_back(a ? a->ns : "unknown");
+  if (opts & OPT_POD) out.push_back(a ? a->pod : "unknown");
+  if (opts & OPT_WL) {
+    if (a && a->has_owner) {
+      out.push_back(a->wk_kind);
+      out.push_back(a->wk_name);
+    } else {
+      out.push_back("unknown");
+      out.push_back("unknown");
+    }
+  }
+  if (opts & OPT_SVC) out.push_back("unknown");
+  if (opts & OPT_PORT) out.push_back((port17 & 0x10000u) ? std::to_string(port17 & 0xFFFFu) : "unknown");
+}
+
+int ensure_staging(gpuagg_ctx *c, size_t cap) {
+  if (cap <= c->staging_cap) return GPUAGG_OK;
+  for (auto &p : c->d_cols) dev_free(p);
+  for (auto &p : c->d_cols) {
+    int rc = dev_alloc(c, &p, cap);
+    if (rc) return rc;
+  }
+  c->staging_cap = cap;
+  return GPUAGG_OK;
+}
+
+int reset_state(gpuagg_ctx *c) {
+  if (c->dense_len) {
+    HIPCHK(c, hipMemsetAsync(c->d_dense_cnt, 0, c->dense_len * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_dense_byt, 0, c->dense_len * 8, c->stream));
+  }
+  if (c->sparse_slots) {
+    HIPCHK(c, hipMemsetAsync(c->sv.k0, 0, c->sparse_slots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sv.k1, 0, c->sparse_slots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sv.cnt, 0, c->sparse_slots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sv.byt, 0, c->sparse_slots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sv.dropped, 0, 8, c->stream));
+    HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+  }
+  if (c->cms_len) HIPCHK(c, hipMemsetAsync(c->d_cms, 0, c->cms_len * 4, c->stream));
+  if (c->hll_len) HIPCHK(c, hipMemsetAsync(c->d_hll, 0, c->hll_len, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPUAGG_OK;
+}
+
+int ensure_sparse(gpuagg_ctx *c) {
+  if (c->sparse_slots) return GPUAGG_OK;
+  const uint32_t lg = c->cfg.sparse_capacity_log2 ? c->cfg.sparse_capacity_log2 : 22;
+  if (lg < 4 || lg > 30) return fail(c, GPUAGG_EINVAL, "sparse_capacity_log2 %u out of [4,30]", lg);
+  const size_t n = (size_t)1 << lg;
+  int rc;
+  if ((rc = dev_alloc(c, &c->sv.k0, n)) || (rc = dev_alloc(c, &c->sv.k1, n)) ||
+      (rc = dev_alloc(c, &c->sv.k2, n)) || (rc = dev_alloc(c, &c->sv.cnt, n)) ||
+      (rc = dev_alloc(c, &c->sv.byt, n)) || (rc = dev_alloc(c, &c->sv.dropped, 1)) ||
+      (rc = dev_alloc(c, &c->d_counter, 1)))
+    return rc;
+  c->sv.mask = (uint32_t)(n - 1);
+  c->sparse_slots = n;
+  return GPUAGG_OK;
+}
+
+void drain_timing(gpuagg_ctx *c) {
+  for (auto &ev : c->pending_events) {
+    float ms = 0.f;
+    if (hipEventSynchronize(ev.second) == hipSuccess && hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) {
+      c->stats.kernel_ms += ms;
+      c->stats.kernel_launches += 1;
+    }
+    hipEventDestroy(ev.first);
+    hipEventDestroy(ev.second);
+  }
+  c->pending_events.clear();
+}
+
+int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
+  if (n == 0) return GPUAGG_OK;
+  if (n > 0xFFFFFFFFull) return fail(c, GPUAGG_ERANGE, "batch of %zu rows exceeds 2^32-1", n);
+  if (!c->ip_cap) return fail(c, GPUAGG_ESTATE, "gpuagg_set_endpoints was never called");
+  if (c->plan.need_ports && !cv.ports) return fail(c, GPUAGG_EINVAL, "enabled metrics read the ports column");
+  if ((c->cms_len) && !cv.ports) return fail(c, GPUAGG_EINVAL, "count-min reads the ports column");
+  if (c->plan.need_dns && !cv.dns_id) return fail(c, GPUAGG_EINVAL, "enabled DNS metrics read the dns_id column");
+  LaunchArgs a{};
+  a.cols = cv;
+  a.n = n;
+  a.ip_slots = c->d_ip;
+  a.ip_mask = (uint32_t)(c->ip_cap - 1);
+  a.plan = c->plan;
+  a.dense_cnt = c->d_dense_cnt;
+  a.dense_byt = c->d_dense_byt;
+  a.sparse = c->sv;
+  a.cms = c->d_cms;
+  a.cms_depth = c->cms_len ? c->cfg.cms_depth : 0;
+  a.cms_wlog2 = c->cfg.cms_width_log2;
+  a.hll = c->d_hll;
+  a.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
+  a.max_blocks = c->max_blocks;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+  }
+  HIPCHK(c, launch_aggregate(a, c->stream));
+  if (c->timing) {
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    c->pending_events.emplace_back(e0, e1);
+  }
+  c->stats.records += n;
+  c->stats.batches += 1;
+  return GPUAGG_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+extern "C" {
+
+int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
+  if (!cfg || !out) return GPUAGG_EINVAL;
+  *out = nullptr;
+  if (cfg->abi_version != GPUAGG_ABI_VERSION) return GPUAGG_EINVAL;
+  std::unique_ptr<gpuagg_ctx> c(new gpuagg_ctx());
+  c->cfg = *cfg;
+  c->device = cfg->device;
+  c->remote = cfg->remote_context != 0;
+  if (cfg->max_slots == 0 || cfg->max_slots > kMaxSlot + 1) return GPUAGG_EINVAL;
+  if (cfg->cms_depth && (cfg->cms_width_log2 < 4 || cfg->cms_width_log2 > 28 || cfg->cms_depth > 16))
+    return GPUAGG_EINVAL;
+  if (cfg->hll_precision && (cfg->hll_precision < 4 || cfg->hll_precision > 18)) return GPUAGG_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c->device || c->device < 0)
+    return GPUAGG_EDEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return GPUAGG_EDEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GPUAGG_EDEVICE;  // built for gfx950 only
+  if (hipSetDevice(c->device) != hipSuccess) return GPUAGG_EDEVICE;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return GPUAGG_EDEVICE;
+  c->max_blocks = (uint32_t)prop.multiProcessorCount * 8u;
+  if (cfg->cms_depth) {
+    c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
+    if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) return GPUAGG_ENOMEM;
+  }
+  if (cfg->hll_precision) {
+    c->hll_len = (size_t)cfg->max_slots << cfg->hll_precision;
+    if (dev_alloc(c.get(), &c->d_hll, c->hll_len)) return GPUAGG_ENOMEM;
+  }
+  if (reset_state(c.get())) return GPUAGG_EDEVICE;
+  *out = c.release();
+  return GPUAGG_OK;
+}
+
+void gpuagg_destroy(gpuagg_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  drain_timing(c);
+  for (auto *b : c->batches) {
+    for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
+                         &b->cols.ports, &b->cols.dns_id})
+      if (*p) hipHostFree(*p);
+    delete b;
+  }
+  dev_free(c->d_ip);
+  dev_free(c->d_dense_cnt);
+  dev_free(c->d_dense_byt);
+  dev_free(c->sv.k0);
+  dev_free(c->sv.k1);
+  dev_free(c->sv.k2);
+  dev_free(c->sv.cnt);
+  dev_free(c->sv.byt);
+  dev_free(c->sv.dropped);
+  dev_free(c->d_counter);
+  dev_free(c->d_export);
+  dev_free(c->d_cms);
+  dev_free(c->d_hll);
+  for (auto &p : c->d_cols) dev_free(p);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *gpuagg_last_error(const gpuagg_ctx *c) { return c ? c->err.c_str() : "null ctx"; }
+
+int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n) {
+  if (!c || (n && !opts)) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const bool local = !c->remote;
+
+  // Module.updateMetricsContexts: registry keyed by MetricName, last writer wins.
+  std::map<std::string, Instance> registry;
+  for (size_t i = 0; i < n; ++i) {
+    const gpuagg_metric_options &o = opts[i];
+    const std::string name = o.metric_name ? o.metric_name : "";
+    const std::string lname = lower(name.c_str());
+    Instance in{};
+    in.registry_name = name;
+    in.has_src = local ? o.source_labels_set != 0 : o.source_labels_set != 0;
+    in.has_dst = local ? false : o.destination_labels_set != 0;
+    in.src_opts = in.has_src ? parse_opts(o.source_labels, o.n_source_labels) : 0;
+    in.dst_opts = in.has_dst ? parse_opts(o.destination_labels, o.n_destination_labels) : 0;
+    in.adv_enable = name != "" && (o.n_source_labels > 0 || o.n_destination_labels > 0);
+    bool make = false;
+    if (name.find("forward") != std::string::npos) {
+      make = lname.find("forward") != std::string::npos;
+      in.family = FAM_FWD;
+      in.active = name == "forward_count" || name == "forward_bytes";
+      in.vk = name == "forward_bytes" ? VK_BYTES : VK_COUNT;
+      in.vec_name = name == "forward_bytes" ? "adv_forward_bytes" : "adv_forward_count";
+    } else if (name.find("drop") != std::string::npos) {
+      make = true;
+      in.family = FAM_DROP;
+      in.active = name == "drop_count" || name == "drop_bytes";
+      in.vk = name == "drop_bytes" ? VK_BYTES : VK_COUNT;
+      in.vec_name = name == "drop_bytes" ? "adv_drop_bytes" : "adv_drop_count";
+    } else if (name.find("tcp") != std::string::npos) {
+      if (lname.find("retrans") != std::string::npos) {  // NewTCPRetransMetrics overwrites
+        make = true;
+        in.family = FAM_RETRANS;
+        in.vec_name = "adv_tcpretrans_count";
+        in.active = true;
+      } else if (lname.find("flag") != std::string::npos) {
+        make = true;
+        in.family = FAM_TCPFLAGS;
+        in.vec_name = "adv_tcpflags_count";
+        in.active = true;
+      }
+      in.vk = VK_COUNT;
+    } else if (name.find("node_apiserver") != std::string::npos) {
+      make = false;  // latency metrics: next, not part of this path yet
+    } else if (name.find("dns") != std::string::npos || name.find("pktmon") != std::string::npos) {
+      if (lname.find("dns") != std::string::npos) {
+        make = true;
+        in.vk = VK_COUNT;
+        if (name == "dns_request_count") {
+          in.family = FAM_DNS_REQ;
+          in.vec_name = "adv_dns_request_count";
+        } else if (name == "dns_response_count") {
+          in.family = FAM_DNS_RESP;
+          in.vec_name = "adv_dns_response_count";
+        } else {
+          return fail(c, GPUAGG_EINVAL,
+                      "metric %s: DNS metric with no vector (dns.go:352-372 leaves it nil and the "
+                      "first DNS flow would panic)", name.c_str());
+        }
+        in.active = true;
+      }
+    }
+    if (!make) continue;
+    if (local && in.active && !in.has_src)
+      return fail(c, GPUAGG_EINVAL,
+                  "metric %s: local context needs sourceLabels (srcCtx is nil, basemetricsobject.go:32-39)",
+                  name.c_str());
+    registry[name] = in;
+  }
+
+  // label schemas
+  std::map<std::string, int> fam_seen;
+  std::vector<Instance> inst;
+  for (auto &kv : registry) {
+    Instance in = kv.second;
+    std::vector<std::string> ln;
+    switch (in.family) {
+      case FAM_FWD: ln = {"direction"}; break;
+      case FAM_DROP: ln = {"reason", "direction"}; break;
+      case FAM_TCPFLAGS: ln = {"flag"}; break;
+      case FAM_RETRANS: ln = {"direction"}; break;
+      case FAM_DNS_REQ: ln = {"query_type", "query"}; break;
+      case FAM_DNS_RESP: ln = {"return_code", "query_type", "query", "response", "num_response"}; break;
+    }
+    const bool ctx_labels = in.family != FAM_FWD || in.adv_enable;
+    if (ctx_labels) {
+      if (local) {
+        if (in.has_src) ctx_label_names(in.src_opts, "", ln);
+      } else {
+        if (in.has_src) ctx_label_names(in.src_opts, "source_", ln);
+        if (in.has_dst) ctx_label_names(in.dst_opts, "destination_", ln);
+      }
+    }
+    in.label_names = ln;
+    in.vec_name = std::string("networkobservability_") + in.vec_name;
+    if (in.active) {
+      if (fam_seen.count(in.vec_name))
+        return fail(c, GPUAGG_EDUPLICATE, "metrics %s and %s both register %s",
+                    registry.count(in.registry_name) ? in.registry_name.c_str() : "?",
+                    inst[fam_seen[in.vec_name]].registry_name.c_str(), in.vec_name.c_str());
+      fam_seen[in.vec_name] = (int)inst.size();
+    }
+    inst.push_back(in);
+  }
+
+  // groups: one per (family, effective options)
+  std::vector<Group> groups;
+  uint64_t dense_total = 0;
+  for (auto &in : inst) {
+    in.group = -1;
+    if (!in.active) continue;
+    uint8_t so = in.has_src ? in.src_opts : 0, dopt = in.has_dst ? in.dst_opts : 0;
+    if (in.family == FAM_FWD && !in.adv_enable) so = dopt = 0;
+    if (local && so == 0) continue;  // getLocalCtxValues yields no values: no updates
+    int gi = -1;
+    for (size_t g = 0; g < groups.size(); ++g)
+      if (groups[g].family == in.family && groups[g].src_opts == so && groups[g].dst_opts == dopt) gi = (int)g;
+    if (gi < 0) {
+      if (groups.size() >= (size_t)kMaxGroups)
+        return fail(c, GPUAGG_ECAPACITY, "more than %d metric groups", kMaxGroups);
+      Group g{};
+      g.family = in.family;
+      g.src_opts = so;
+      g.dst_opts = dopt;
+      const bool dns = in.family == FAM_DNS_REQ || in.family == FAM_DNS_RESP;
+      g.sparse = !local || dns || (so & (OPT_IP | OPT_PORT));
+      if (!g.sparse) {
+        g.key_mode = (so & OPT_EP) ? 1 : 0;
+        g.nkeys = g.key_mode ? c->cfg.max_slots : 1;
+        g.nsub = (in.family == FAM_DROP || in.family == FAM_TCPFLAGS) ? 8 : 1;
+        g.dense_base = dense_total;
+        dense_total += g.nkeys * 2 * g.nsub;
+      }
+      groups.push_back(g);
+      gi = (int)groups.size() - 1;
+    }
+    in.group = gi;
+  }
+
+  Plan p{};
+  p.local = local ? 1 : 0;
+  p.ngroups = (int32_t)groups.size();
+  bool any_sparse = false;
+  for (size_t g = 0; g < groups.size(); ++g) {
+    GroupPlan &gp = p.g[g];
+    gp.family = groups[g].family;
+    gp.sparse = groups[g].sparse;
+    gp.src_opts = groups[g].src_opts;
+    gp.dst_opts = groups[g].dst_opts;
+    gp.nsub = groups[g].nsub;
+    gp.dense_base = groups[g].dense_base;
+    gp.key_mode = groups[g].key_mode;
+    if ((gp.src_opts | gp.dst_opts) & OPT_PORT) p.need_ports = 1;
+    if (gp.family == FAM_DNS_REQ || gp.family == FAM_DNS_RESP) p.need_dns = 1;
+    any_sparse |= groups[g].sparse;
+  }
+
+  // (re)allocate state
+  if (dense_total != c->dense_len) {
+    dev_free(c->d_dense_cnt);
+    dev_free(c->d_dense_byt);
+    c->dense_len = 0;
+    if ((rc = dev_alloc(c, &c->d_dense_cnt, dense_total)) || (rc = dev_alloc(c, &c->d_dense_byt, dense_total)))
+      return rc;
+    c->dense_len = dense_total;
+  }
+  if (any_sparse && (rc = ensure_sparse(c))) return rc;
+  c->inst = inst;
+  c->groups = groups;
+  c->plan = p;
+  return reset_state(c);
+}
+
+int gpuagg_slot_intern(gpuagg_ctx *c, const char *ns, const char *pod, const char *wk_kind,
+                       const char *wk_name, int32_t *slot) {
+  if (!c || !ns || !pod || !slot) return GPUAGG_EINVAL;
+  const int has_owner = wk_kind != nullptr;
+  auto key = std::make_tuple(std::string(ns), std::string(pod), std::string(has_owner ? wk_kind : ""),
+                             std::string(has_owner && wk_name ? wk_name : ""), has_owner);
+  auto it = c->slot_ids.find(key);
+  if (it != c->slot_ids.end()) {
+    *slot = it->second;
+    return GPUAGG_OK;
+  }
+  if (c->slots.size() >= c->cfg.max_slots)
+    return fail(c, GPUAGG_ECAPACITY, "more than max_slots=%u endpoint identities", c->cfg.max_slots);
+  SlotAttr a;
+  a.ns = ns;
+  a.pod = pod;
+  a.has_owner = has_owner;
+  if (has_owner) {
+    a.wk_kind = wk_kind;
+    a.wk_name = wk_name ? wk_name : "";
+  }
+  a.api = a.ns == kApiServer && a.pod == kApiServer;
+  const int32_t id = (int32_t)c->slots.size();
+  c->slots.push_back(a);
+  c->slot_ids.emplace(key, id);
+  *slot = id;
+  return GPUAGG_OK;
+}
+
+int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slot, size_t n,
+                         uint64_t version) {
+  if (!c || (n && (!ipv4 || !slot))) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n > c->cfg.max_ips) return fail(c, GPUAGG_ECAPACITY, "%zu IPs exceed max_ips=%u", n, c->cfg.max_ips);
+  size_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  std::vector<uint64_t> tab(cap, kIpEmpty);
+  for (size_t i = 0; i < n; ++i) {
+    if (slot[i] < 0 || (size_t)slot[i] >= c->slots.size())
+      return fail(c, GPUAGG_EINVAL, "entry %zu: slot %d was not interned", i, slot[i]);
+    if (ipv4[i] == 0xFFFFFFFFu) return fail(c, GPUAGG_ERANGE, "255.255.255.255 cannot be a pod IP");
+    uint32_t h = ip_hash(ipv4[i]) & (uint32_t)(cap - 1);
+    for (;;) {
+      if (tab[h] == kIpEmpty) {
+        tab[h] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
+        break;
+      }
+      if ((uint32_t)tab[h] == ipv4[i]) {  // duplicate IP: last writer wins (cache.go:227-230)
+        tab[h] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
+        break;
+      }
+      h = (h + 1) & (uint32_t)(cap - 1);
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches use the old table
+  if (cap != c->ip_cap) {
+    dev_free(c->d_ip);
+    c->ip_cap = 0;
+    if ((rc = dev_alloc(c, &c->d_ip, cap))) return rc;
+  }
+  HIPCHK(c, hipMemcpy(c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
+  c->ip_cap = cap;
+  c->ip_version = version;
+  return GPUAGG_OK;
+}
+
+int gpuagg_dns_intern(gpuagg_ctx *c, uint32_t rcode, const char *qtypes, const char *query,
+                      const char *ips, uint32_t nresp, uint32_t *id) {
+  if (!c || !qtypes || !query || !ips || !id) return GPUAGG_EINVAL;
+  std::string key = std::to_string(rcode) + '\x1f' + qtypes + '\x1f' + query + '\x1f' + ips +
+                    '\x1f' + std::to_string(nresp);
+  auto it = c->dns_ids.find(key);
+  if (it != c->dns_ids.end()) {
+    *id = it->second;
+    return GPUAGG_OK;
+  }
+  if (c->dns.size() >= 0xFFFFFFFEull) return fail(c, GPUAGG_ECAPACITY, "DNS dictionary full");
+  const uint32_t nid = (uint32_t)c->dns.size();
+  c->dns.push_back(DnsAttr{rcode, nresp, qtypes, query, ips});
+  c->dns_ids.emplace(std::move(key), nid);
+  *id = nid;
+  return GPUAGG_OK;
+}
+
+int gpuagg_alloc_batch(gpuagg_ctx *c, size_t cap, gpuagg_batch **out) {
+  if (!c || !out || !cap) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  auto *b = new gpuagg_batch();
+  b->capacity = cap;
+  for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
+                       &b->cols.ports, &b->cols.dns_id}) {
+    if (hipHostMalloc((void **)p, cap * 4, hipHostMallocDefault) != hipSuccess) {
+      delete b;
+      return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", cap * 4);
+    }
+    memset(*p, 0, cap * 4);
+  }
+  if ((rc = ensure_staging(c, cap))) return rc;
+  c->batches.push_back(b);
+  *out = b;
+  return GPUAGG_OK;
+}
+
+void gpuagg_free_batch(gpuagg_ctx *c, gpuagg_batch *b) {
+  if (!c || !b) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
+                       &b->cols.ports, &b->cols.dns_id})
+    if (*p) hipHostFree(*p);
+  c->batches.erase(std::remove(c->batches.begin(), c->batches.end(), b), c->batches.end());
+  delete b;
+}
+
+int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
+  if (!c || !b || n > b->capacity) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if ((rc = ensure_staging(c, b->capacity))) return rc;
+  uint32_t *src[6] = {b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports, b->cols.dns_id};
+  const bool need[6] = {true, true, true, true, c->plan.need_ports || c->cms_len > 0, (bool)c->plan.need_dns};
+  for (int i = 0; i < 6; ++i)
+    if (need[i] && n) HIPCHK(c, hipMemcpyAsync(c->d_cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->stream));
+  ColsView cv{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3], c->d_cols[4], c->d_cols[5]};
+  if ((rc = launch(c, cv, n))) return rc;
+  // The single staging area is reused by the next submit, which is stream-ordered
+  // behind this kernel; the pinned batch is free once its copies have completed.
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPUAGG_OK;
+}
+
+int gpuagg_submit_device(gpuagg_ctx *c, const gpuagg_columns *d, size_t n) {
+  if (!c || !d) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  ColsView cv{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id};
+  return launch(c, cv, n);
+}
+
+int gpuagg_sync(gpuagg_ctx *c) {
+  if (!c) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  drain_timing(c);
+  return GPUAGG_OK;
+}
+
+int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
+  if (!c || !out) return GPUAGG_EINVAL;
+  *out = nullptr;
+  int rc = gpuagg_sync(c);
+  if (rc) return rc;
+
+  // dense counters
+  std::vector<uint64_t> dc(c->dense_len), db(c->dense_len);
+  if (c->dense_len) {
+    HIPCHK(c, hipMemcpy(dc.data(), c->d_dense_cnt, c->dense_len * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(db.data(), c->d_dense_byt, c->dense_len * 8, hipMemcpyDeviceToHost));
+  }
+  // sparse entries
+  std::vector<uint64_t> ent;
+  size_t nent = 0;
+  if (c->sparse_slots) {
+    uint64_t dropped = 0;
+    HIPCHK(c, hipMemcpy(&dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+    c->stats.sparse_dropped = dropped;
+    if (dropped)
+      return fail(c, GPUAGG_ECAPACITY, "group-by table full: %llu updates lost (raise sparse_capacity_log2)",
+                  (unsigned long long)dropped);
+    if (c->export_cap < c->sparse_slots) {
+      dev_free(c->d_export);
+      if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
+      c->export_cap = c->sparse_slots;
+    }
+    rc = gpuagg_sparse_export(c, c->d_export, c->export_cap, &nent);
+    if (rc) return rc;
+    ent.resize(nent * kSparseEntryWords);
+    if (nent) HIPCHK(c, hipMemcpy(ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
+    c->stats.sparse_entries = nent;
+  }
+
+  // render: key -> label tuple, summing equal tuples
+  std::vector<std::map<std::vector<std::string>, uint64_t>> acc(c->inst.size());
+  std::vector<std::string> vals;
+  const bool local = !c->remote;
+  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
+    const Instance &in = c->inst[ii];
+    if (!in.active || in.group < 0) continue;
+    const Group &g = c->groups[in.group];
+    auto &dst = acc[ii];
+    if (!g.sparse) {
+      for (uint64_t key = 0; key < g.nkeys; ++key)
+        for (uint32_t side = 0; side < 2; ++side)
+          for (uint32_t sub = 0; sub < g.nsub; ++sub) {
+            const uint64_t idx = g.dense_base + (key * 2 + side) * g.nsub + sub;
+            if (!dc[idx]) continue;
+            vals.clear();
+            if (g.family == FAM_DROP) vals.push_back(drop_reason_name(sub));
+            if (g.family == FAM_TCPFLAGS) vals.push_back(kFlagNames[sub]);
+            if (g.family != FAM_TCPFLAGS) vals.push_back(side == 0 ? "ingress" : "egress");
+            ctx_values(c, g.src_opts, 0, g.key_mode ? (uint32_t)key + 1 : 0, 0, vals);
+            dst[vals] += in.vk == VK_BYTES ? db[idx] : dc[idx];
+          }
+      continue;
+    }
+    for (size_t e = 0; e < nent; ++e) {
+      const uint64_t *w = &ent[e * kSparseEntryWords];
+      if ((int)key_group(w[0]) != in.group) continue;
+      const uint32_t sub = key_sub(w[0]);
+      vals.clear();
+      const uint32_t hi = sub >> 3, tdir = (sub >> 1) & 3, side = sub & 1;
+      switch (g.family) {
+        case FAM_FWD:
+        case FAM_RETRANS:
+          vals.push_back(local ? (side == 0 ? "ingress" : "egress") : traffic_direction_name(tdir));
+          break;
+        case FAM_DROP:
+          vals.push_back(drop_reason_name(hi));
+          vals.push_back(local ? (side == 0 ? "ingress" : "egress") : traffic_direction_name(tdir));
+          break;
+        case FAM_TCPFLAGS: vals.push_back(kFlagNames[hi]); break;
+        case FAM_DNS_REQ:
+        case FAM_DNS_RESP: {
+          const uint32_t id = key_dns(w[2]);
+          if (id >= c->dns.size()) return fail(c, GPUAGG_EINVAL, "dns_id %u was not interned", id);
+          const DnsAttr &a = c->dns[id];
+          if (g.family == FAM_DNS_RESP) vals.push_back(a.rcode < 6 ? kRcodeNames[a.rcode] : "");
+          vals.push_back(a.qtypes);
+          vals.push_back(a.query);
+          if (g.family == FAM_DNS_RESP) {
+            vals.push_back(a.ips);
+            vals.push_back(std::to_string(a.nresp));
+          }
+          break;
+        }
+      }
+      if (local) {
+        ctx_values(c, g.src_opts, key_s_ip(w[0]), key_s_slot1(w[0]), key_s_port17(w[1]), vals);
+      } else {
+        if (in.has_src) ctx_values(c, g.src_opts, key_s_ip(w[0]), key_s_slot1(w[0]), key_s_port17(w[1]), vals);
+        if (in.has_dst) ctx_values(c, g.dst_opts, key_d_ip(w[2]), key_d_slot1(w[1]), key_d_port17(w[1]), vals);
+      }
+      dst[vals] += in.vk == VK_BYTES ? w[4] : w[3];
+    }
+  }
+
+  auto *r = new gpuagg_result();
+  for (size_t ii = 0; ii < c->inst.size(); ++ii)
+    for (auto &kv : acc[ii]) r->series.push_back(Series{c->inst[ii].vec_name, c->inst[ii].label_names, kv.first, kv.second});
+  r->name_ptrs.resize(r->series.size());
+  r->value_ptrs.resize(r->series.size());
+  for (size_t i = 0; i < r->series.size(); ++i) {
+    for (auto &s : r->series[i].names) r->name_ptrs[i].push_back(s.c_str());
+    for (auto &s : r->series[i].values) r->value_ptrs[i].push_back(s.c_str());
+  }
+  if (c->cms_len || c->hll_len) {
+    if ((rc = gpuagg_sketch_refresh(c))) {
+      gpuagg_result_free(r);
+      return rc;
+    }
+  }
+  *out = r;
+  return GPUAGG_OK;
+}
+
+size_t gpuagg_result_count(const gpuagg_result *r) { return r ? r->series.size() : 0; }
+
+int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, uint32_t *n_labels,
+                         const char *const **names, const char *const **values, uint64_t *value) {
+  if (!r || i >= r->series.size()) return GPUAGG_EINVAL;
+  const Series &s = r->series[i];
+  if (metric) *metric = s.metric.c_str();
+  if (n_labels) *n_labels = (uint32_t)s.names.size();
+  if (names) *names = r->name_ptrs[i].data();
+  if (values) *values = r->value_ptrs[i].data();
+  if (value) *value = s.value;
+  return GPUAGG_OK;
+}
+
+void gpuagg_result_free(gpuagg_result *r) { delete r; }
+
+// ---- sketches ---------------------------------------------------------------------
+int gpuagg_sketch_refresh(gpuagg_ctx *c) {
+  if (!c) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_cms.resize(c->cms_len);
+  c->h_hll.resize(c->hll_len);
+  if (c->cms_len) HIPCHK(c, hipMemcpy(c->h_cms.data(), c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
+  if (c->hll_len) HIPCHK(c, hipMemcpy(c->h_hll.data(), c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
+  return GPUAGG_OK;
+}
+
+int gpuagg_cms_estimate(gpuagg_ctx *c, uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto,
+                        uint64_t *est) {
+  if (!c || !est) return GPUAGG_EINVAL;
+  if (!c->cms_len || c->h_cms.size() != c->cms_len) return fail(c, GPUAGG_ESTATE, "no count-min snapshot");
+  const uint64_t base = cms_base(src, dst, ports, proto);
+  const uint32_t wmask = (1u << c->cfg.cms_width_log2) - 1u;
+  uint64_t m = ~0ull;
+  for (uint32_t r = 0; r < c->cfg.cms_depth; ++r)
+    m = std::min<uint64_t>(m, c->h_cms[((size_t)r << c->cfg.cms_width_log2) + cms_col(base, r, wmask)]);
+  *est = m;
+  return GPUAGG_OK;
+}
+
+int gpuagg_hll_estimate(gpuagg_ctx *c, int32_t slot, double *est) {
+  if (!c || !est) return GPUAGG_EINVAL;
+  if (!c->hll_len || c->h_hll.size() != c->hll_len) return fail(c, GPUAGG_ESTATE, "no HLL snapshot");
+  if (slot < 0 || (uint32_t)slot >= c->cfg.max_slots) return GPUAGG_EINVAL;
+  const uint32_t p = c->cfg.hll_precision;
+  const size_t m = (size_t)1 << p;
+  const uint8_t *reg = &c->h_hll[(size_t)slot << p];
+  double sum = 0;
+  size_t zeros = 0;
+  for (size_t i = 0; i < m; ++i) {
+    sum += std::ldexp(1.0, -(int)reg[i]);
+    zeros += reg[i] == 0;
+  }
+  const double md = (double)m;
+  const double alpha = 0.7213 / (1.0 + 1.079 / md);
+  double e = alpha * md * md / sum;
+  if (e <= 2.5 * md && zeros) e = md * std::log(md / (double)zeros);  // linear counting
+  *est = e;
+  return GPUAGG_OK;
+}
+
+int gpuagg_cms_copy(gpuagg_ctx *c, uint32_t *out, size_t n) {
+  if (!c || !out || n < c->cms_len) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->cms_len) HIPCHK(c, hipMemcpy(out, c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
+  return GPUAGG_OK;
+}
+
+int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
+  if (!c || !out || n < c->hll_len) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->hll_len) HIPCHK(c, hipMemcpy(out, c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
+  return GPUAGG_OK;
+}
+
+// ---- multi-GPU merge hooks -----------------------------------------------------------
+int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
+  if (!c || !o) return GPUAGG_EINVAL;
+  o->dense_count = c->d_dense_cnt;
+  o->dense_bytes = c->d_dense_byt;
+  o->dense_len = c->dense_len;
+  o->cms = c->d_cms;
+  o->cms_len = c->cms_len;
+  o->hll = c->d_hll;
+  o->hll_len = c->hll_len;
+  o->sparse_entry_words = kSparseEntryWords;
+  return GPUAGG_OK;
+}
+
+int gpuagg_sparse_export(gpuagg_ctx *c, uint64_t *dev_out, size_t cap, size_t *n_out) {
+  if (!c || !n_out) return GPUAGG_EINVAL;
+  *n_out = 0;
+  if (!c->sparse_slots) return GPUAGG_OK;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 8, c->stream));
+  HIPCHK(c, launch_sparse_export(c->sv, c->sparse_slots, dev_out, cap, c->d_counter, c->stream));
+  uint64_t n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *n_out = (size_t)std::min<uint64_t>(n, cap);
+  if (n > cap) return fail(c, GPUAGG_ECAPACITY, "export buffer holds %zu of %llu entries", cap, (unsigned long long)n);
+  return GPUAGG_OK;
+}
+
+int gpuagg_sparse_import(gpuagg_ctx *c, const uint64_t *dev_in, size_t n) {
+  if (!c || (n && !dev_in)) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if (!n) return GPUAGG_OK;
+  if ((rc = ensure_sparse(c))) return rc;
+  HIPCHK(c, launch_sparse_import(c->sv, dev_in, n, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPUAGG_OK;
+}
+
+int gpuagg_get_stats(gpuagg_ctx *c, gpuagg_stats *out) {
+  if (!c || !out) return GPUAGG_EINVAL;
+  *out = c->stats;
+  return GPUAGG_OK;
+}
+
+int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
+  if (!c) return GPUAGG_EINVAL;
+  c->timing = enabled != 0;
+  if (!enabled) {
+    c->stats.kernel_ms = 0;
+    c->stats.kernel_launches = 0;
+  }
+  return GPUAGG_OK;
+}
+
+void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+"""Python host of the flow-aggregation engine (over the C-ABI in include/gpuagg.h).
+
+Mirrors the reference's host-side vocabulary so tests read like Retina's own:
+
+* ``GpuAgg.reconcile(context_options)``  -- Module.Reconcile / updateMetricsContexts
+  (pkg/module/metrics/metrics_module.go:205-264)
+* ``GpuAgg.set_endpoints`` / ``load_endpoints`` -- the enricher's IP cache snapshot
+  (pkg/controllers/cache/cache.go:110-233)
+* ``GpuAgg.submit`` / ``submit_device``    -- Enricher.Write of a whole batch
+  (pkg/enricher/enricher.go:185-187)
+* ``GpuAgg.snapshot``                      -- what the AdvancedRegistry would expose
+  (pkg/exporter/prometheusexporter.go:17-66)
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _abi
+
+SeriesKey = Tuple[str, Tuple[Tuple[str, str], ...]]
+
+
+class GpuAggError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s (%d): %s" % (_abi.ERR_NAMES.get(code, "E?"), code, msg))
+        self.code = code
+
+
+@dataclass
+class ContextOptions:
+    """crd MetricsContextOptions (metricsconfiguration_types.go:27-58); None = nil slice."""
+    metric_name: str
+    source_labels: Optional[List[str]] = None
+    destination_labels: Optional[List[str]] = None
+
+
+def _opts(o) -> ContextOptions:
+    if isinstance(o, ContextOptions):
+        return o
+    if isinstance(o, dict):
+        return ContextOptions(o["metric_name"], o.get("source_labels"), o.get("destination_labels"))
+    return ContextOptions(o.metric_name, o.source_labels, o.destination_labels)
+
+
+@dataclass
+class Endpoint:
+    """A pod's identity as the enricher copies it into flow.Endpoint (enricher.go:142-183)."""
+    namespace: str
+    name: str
+    ips: Sequence[int]  # LE u32 IPv4, primary first (ipaddr.go:35-50)
+    owner_refs: Optional[Sequence[Tuple[str, str]]] = None  # (kind, name)
+
+
+class HostBatch:
+    """A library-owned pinned batch with numpy views of its columns."""
+
+    def __init__(self, ptr, capacity: int):
+        self.ptr = ptr
+        self.capacity = capacity
+        cols = ptr.contents.cols
+        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+            p = getattr(cols, name)
+            setattr(self, name, np.ctypeslib.as_array(p, shape=(capacity,)))
+
+    def fill(self, batch, start: int = 0, n: Optional[int] = None) -> int:
+        """Copy rows [start, start+n) of an object with numpy column attributes."""
+        total = len(batch.src_ip)
+        n = min(self.capacity, total - start) if n is None else n
+        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+            src = getattr(batch, name, None)
+            if src is not None:
+                getattr(self, name)[:n] = src[start:start + n]
+            else:
+                getattr(self, name)[:n] = 0
+        return n
+
+
+class GpuAgg:
+    """One engine context bound to one MI355X (gfx950) device."""
+
+    def __init__(self, device: int = 0, remote_context: bool = False, max_slots: int = 1 << 14,
+                 max_ips: int = 1 << 16, sparse_capacity_log2: int = 22, cms_depth: int = 0,
+                 cms_width_log2: int = 20, hll_precision: int = 0):
+        self.lib = _abi.load()
+        cfg = _abi.Config(_abi.ABI_VERSION, device, 1 if remote_context else 0, max_slots, max_ips,
+                          sparse_capacity_log2, cms_depth, cms_width_log2 if cms_depth else 0,
+                          hll_precision)
+        h = C.c_void_p()
+        rc = self.lib.gpuagg_create(C.byref(cfg), C.byref(h))
+        if rc != _abi.OK:
+            raise GpuAggError(rc, "gpuagg_create failed (device %d; a gfx950 GPU is required)" % device)
+        self.h = h
+        self.cfg = cfg
+        self.device = device
+        self.remote_context = remote_context
+        self._batches: List[HostBatch] = []
+
+    # -- plumbing --------------------------------------------------------------------
+    def _check(self, rc: int) -> None:
+        if rc != _abi.OK:
+            msg = self.lib.gpuagg_last_error(self.h)
+            raise GpuAggError(rc, msg.decode() if msg else "")
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.gpuagg_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- Module.Reconcile ------------------------------------------------------------
+    def reconcile(self, context_options: Iterable) -> None:
+        opts = [_opts(o) for o in context_options]
+        keep = []
+
+        def strarr(lst):
+            if lst is None:
+                return None, 0, 0
+            arr = (C.c_char_p * max(1, len(lst)))(*[s.encode() for s in lst])
+            keep.append(arr)
+            return arr, len(lst), 1
+
+        arr = (_abi.MetricOptions * max(1, len(opts)))()
+        for i, o in enumerate(opts):
+            s, ns, sset = strarr(o.source_labels)
+            d, nd, dset = strarr(o.destination_labels)
+            arr[i].metric_name = o.metric_name.encode()
+            arr[i].source_labels = C.cast(s, C.POINTER(C.c_char_p)) if s is not None else None
+            arr[i].n_source_labels = ns
+            arr[i].source_labels_set = sset
+            arr[i].destination_labels = C.cast(d, C.POINTER(C.c_char_p)) if d is not None else None
+            arr[i].n_destination_labels = nd
+            arr[i].destination_labels_set = dset
+        self._check(self.lib.gpuagg_reconcile(self.h, arr, len(opts)))
+
+    # -- endpoints / dictionaries ----------------------------------------------------
+    def slot_intern(self, namespace: str, pod: str, workload_kind: Optional[str] = None,
+                    workload_name: Optional[str] = None) -> int:
+        s = C.c_int32()
+        self._check(self.lib.gpuagg_slot_intern(
+            self.h, namespace.encode(), pod.encode(),
+            None if workload_kind is None else workload_kind.encode(),
+            None if workload_name is None else (workload_name or "").encode(), C.byref(s)))
+        return s.value
+
+    def set_endpoints(self, ips: np.ndarray, slots: np.ndarray, version: int = 0) -> None:
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(self.lib.gpuagg_set_endpoints(
+            self.h, ips.ctypes.data_as(_abi.u32p), slots.ctypes.data_as(C.POINTER(C.c_int32)),
+            len(ips), version))
+
+    def load_endpoints(self, endpoints: Sequence[Endpoint], version: int = 0) -> Dict[int, int]:
+        """Interns every endpoint identity and installs the IP -> slot table.
+
+        Later endpoints win an IP held by an earlier one (cache.go:204-233)."""
+        ip_to_slot: Dict[int, int] = {}
+        for ep in endpoints:
+            owner = ep.owner_refs[0] if ep.owner_refs else None
+            slot = self.slot_intern(ep.namespace, ep.name, owner[0] if owner else None,
+                                    owner[1] if owner else None)
+            for ip in ep.ips:
+                ip_to_slot[int(ip)] = slot
+        ips = np.fromiter(ip_to_slot.keys(), dtype=np.uint32, count=len(ip_to_slot))
+        sl = np.fromiter(ip_to_slot.values(), dtype=np.int32, count=len(ip_to_slot))
+        self.set_endpoints(ips, sl, version)
+        return ip_to_slot
+
+    def dns_intern(self, rcode: int, qtypes: Sequence[str], query: str, ips: Sequence[str],
+                   num_answers: int) -> int:
+        out = C.c_uint32()
+        self._check(self.lib.gpuagg_dns_intern(self.h, rcode, ",".join(qtypes).encode(),
+                                               query.encode(), ",".join(ips).encode(),
+                                               num_answers, C.byref(out)))
+        return out.value
+
+    # -- records -----------------------------------------------------------------------
+    def alloc_batch(self, capacity: int) -> HostBatch:
+        p = C.POINTER(_abi.Batch)()
+        self._check(self.lib.gpuagg_alloc_batch(self.h, capacity, C.byref(p)))
+        b = HostBatch(p, capacity)
+        self._batches.append(b)
+        return b
+
+    def submit(self, batch: HostBatch, n: int) -> None:
+        self._check(self.lib.gpuagg_submit(self.h, batch.ptr, n))
+
+    def submit_numpy(self, batch, chunk: int = 1 << 22) -> None:
+        """Host-fed path: streams a numpy column batch through pinned buffers."""
+        total = len(batch.src_ip)
+        hb = None
+        for b in self._batches:
+            if b.capacity >= min(chunk, max(total, 1)):
+                hb = b
+                break
+        if hb is None:
+            hb = self.alloc_batch(max(1, min(chunk, total)))
+        start = 0
+        while start < total:
+            n = hb.fill(batch, start)
+            self.submit(hb, n)
+            start += n
+
+    @staticmethod
+    def device_columns(src_ip, dst_ip, nbytes, meta, ports=None, dns_id=None) -> "_abi.Columns":
+        """Columns from device tensors (torch int32/uint32, contiguous, on this device)."""
+        def ptr(t):
+            if t is None:
+                return None
+            return C.cast(C.c_void_p(t.data_ptr()), _abi.u32p)
+        return _abi.Columns(ptr(src_ip), ptr(dst_ip), ptr(nbytes), ptr(meta), ptr(ports), ptr(dns_id))
+
+    def submit_device(self, cols: "_abi.Columns", n: int) -> None:
+        self._check(self.lib.gpuagg_submit_device(self.h, C.byref(cols), n))
+
+    def sync(self) -> None:
+        self._check(self.lib.gpuagg_sync(self.h))
+
+    # -- output ------------------------------------------------------------------------
+    def snapshot(self) -> Dict[SeriesKey, int]:
+        r = C.c_void_p()
+        self._check(self.lib.gpuagg_snapshot(self.h, C.byref(r)))
+        out: Dict[SeriesKey, int] = {}
+        try:
+            n = self.lib.gpuagg_result_count(r)
+            metric = C.c_char_p()
+            nl = C.c_uint32()
+            names = C.POINTER(C.c_char_p)()
+            vals = C.POINTER(C.c_char_p)()
+            v = C.c_uint64()
+            for i in range(n):
+                self._check(self.lib.gpuagg_result_series(r, i, C.byref(metric), C.byref(nl),
+                                                          C.byref(names), C.byref(vals), C.byref(v)))
+                labels = tuple((names[j].decode(), vals[j].decode()) for j in range(nl.value))
+                out[(metric.value.decode(), labels)] = v.value
+        finally:
+            self.lib.gpuagg_result_free(r)
+        return out
+
+    # -- sketches ----------------------------------------------------------------------
+    def sketch_refresh(self) -> None:
+        self._check(self.lib.gpuagg_sketch_refresh(self.h))
+
+    def cms_estimate(self, src_ip: int, dst_ip: int, ports: int, proto: int) -> int:
+        out = C.c_uint64()
+        self._check(self.lib.gpuagg_cms_estimate(self.h, src_ip, dst_ip, ports, proto, C.byref(out)))
+        return out.value
+
+    def hll_estimate(self, slot: int) -> float:
+        out = C.c_double()
+        self._check(self.lib.gpuagg_hll_estimate(self.h, slot, C.byref(out)))
+        return out.value
+
+    def cms_array(self) -> np.ndarray:
+        d = self.state()
+        a = np.zeros(d.cms_len, np.uint32)
+        self._check(self.lib.gpuagg_cms_copy(self.h, a.ctypes.data_as(_abi.u32p), a.size))
+        return a.reshape(self.cfg.cms_depth, -1) if a.size else a
+
+    def hll_array(self) -> np.ndarray:
+        d = self.state()
+        a = np.zeros(d.hll_len, np.uint8)
+        self._check(self.lib.gpuagg_hll_copy(self.h, a.ctypes.data_as(C.POINTER(C.c_uint8)), a.size))
+        return a.reshape(self.cfg.max_slots, -1) if a.size else a
+
+    # -- merge / introspection -----------------------------------------------------------
+    def state(self) -> "_abi.StateDesc":
+        d = _abi.StateDesc()
+        self._check(self.lib.gpuagg_state(self.h, C.byref(d)))
+        return d
+
+    def sparse_export(self, dev_ptr: int, cap: int) -> int:
+        n = C.c_size_t()
+        self._check(self.lib.gpuagg_sparse_export(self.h, C.c_void_p(dev_ptr), cap, C.byref(n)))
+        return n.value
+
+    def sparse_import(self, dev_ptr: int, n: int) -> None:
+        self._check(self.lib.gpuagg_sparse_import(self.h, C.c_void_p(dev_ptr), n))
+
+    def stats(self) -> Dict[str, float]:
+        s = _abi.Stats()
+        self._check(self.lib.gpuagg_get_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in _abi.Stats._fields_}
+
+    def set_timing(self, enabled: bool) -> None:
+        self._check(self.lib.gpuagg_set_timing(self.h, 1 if enabled else 0))

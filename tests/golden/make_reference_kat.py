@@ -1,0 +1,228 @@
+"""Writes reference_kat.json: the known-answer cases of the reference's own Go tests,
+transcribed as data (inputs + expected outputs), each citing the test it comes from.
+
+The reference cannot run here (no Go toolchain), so these vectors pin
+the oracle.  Run:  python tests/golden/make_reference_kat.py
+"""
+
+import json
+import os
+
+ALL = ["ip", "namespace", "podName", "Workload", "PORT", "serVICE"]
+SRC_ALL = ["source_ip", "source_namespace", "source_podname", "source_workload_kind",
+           "source_workload_name", "source_service", "source_port"]
+DST_ALL = [s.replace("source_", "destination_") for s in SRC_ALL]
+LOC_ALL = [s.replace("source_", "") for s in SRC_ALL]
+EMPTY_EP = {"namespace": "", "pod_name": ""}
+ALL_FLAGS = {"SYN": True, "FIN": True, "RST": True, "PSH": True, "URG": True, "ECE": True,
+             "CWR": True, "ACK": True}
+
+
+def fl(verdict=0, source=None, destination=None, ip=None, l4=None, tdir=0):
+    return {"verdict": verdict, "source": source, "destination": destination, "ip": ip, "l4": l4,
+            "traffic_direction": tdir}
+
+
+def tcp(flags):
+    return {"proto": "TCP", "flags": flags}
+
+
+F, D = 1, 2
+
+kat = {
+    # pkg/module/metrics/types_test.go:21-141 (TestNewCtxOps)
+    "ctx_options": [
+        {"name": "empty opts", "opts": [], "ctx": "source", "labels": [], "flow": fl(),
+         "values": []},
+        {"name": "source opts 1", "opts": ALL, "ctx": "source", "labels": SRC_ALL, "flow": fl(),
+         "values": ["unknown"] * 7},
+        {"name": "dest opts 1", "opts": ALL, "ctx": "destination", "labels": DST_ALL, "flow": fl(),
+         "values": ["unknown"] * 7},
+        {"name": "source opts with flow", "opts": ALL, "ctx": "source", "labels": SRC_ALL,
+         "flow": fl(source={"namespace": "ns", "pod_name": "test"}),
+         "values": ["unknown", "ns", "test", "unknown", "unknown", "unknown", "unknown"]},
+        {"name": "source opts with flow (destination)", "opts": ALL, "ctx": "destination",
+         "labels": DST_ALL, "flow": fl(destination={"namespace": "ns", "pod_name": "test"}),
+         "values": ["unknown", "ns", "test", "unknown", "unknown", "unknown", "unknown"]},
+        {"name": "source opts of ip", "opts": ["ip", "namespace", "podName"], "ctx": "source",
+         "labels": ["source_ip", "source_namespace", "source_podname"],
+         "flow": fl(source={"namespace": "ns", "pod_name": "test"},
+                    ip={"source": "10.0.0.1", "destination": ""}),
+         "values": ["10.0.0.1", "ns", "test"]},
+        {"name": "dest opts of ip", "opts": ["ip", "namespace", "podName"], "ctx": "destination",
+         "labels": ["destination_ip", "destination_namespace", "destination_podname"],
+         "flow": fl(destination={"namespace": "ns", "pod_name": "test"},
+                    ip={"source": "", "destination": "10.0.0.1"}),
+         "values": ["10.0.0.1", "ns", "test"]},
+        {"name": "dest opts of ip with no destination info", "opts": ["ip", "namespace", "podName"],
+         "ctx": "destination",
+         "labels": ["destination_ip", "destination_namespace", "destination_podname"],
+         "flow": fl(source={"namespace": "ns", "pod_name": "test"},
+                    ip={"source": "10.0.0.1", "destination": ""}),
+         "values": ["", "unknown", "unknown"]},
+    ],
+    # pkg/module/metrics/dns_test.go:165-234 (TestGetLabels)
+    "dns_labels": [
+        {"name": "basic context request labels", "local_opts": None, "kind": "request",
+         "want": ["query_type", "query"]},
+        {"name": "basic context response labels", "local_opts": None, "kind": "response",
+         "want": ["return_code", "query_type", "query", "response", "num_response"]},
+        {"name": "local context request labels",
+         "local_opts": ["ip", "namespace", "podname", "service", "port", "workload"],
+         "kind": "request",
+         "want": ["query_type", "query", "ip", "namespace", "podname", "workload_kind",
+                  "workload_name", "service", "port"]},
+    ],
+    # pkg/module/metrics/dns_test.go:236-335 (TestValues); flows built with AddDNSInfo
+    # (qtype, rcode 0, "bing.com", ["A"], num_answers, ips)
+    "dns_values": [
+        {"name": "basic context", "metric_name": "", "input": None, "call": "response", "want": None},
+        {"name": "Query", "metric_name": "dns_request_count", "input": ["Q", 0, []],
+         "call": "request", "want": ["A", "bing.com"]},
+        {"name": "Response", "metric_name": "dns_response_count", "input": ["R", 1, ["1.1.1.1"]],
+         "call": "response", "want": ["NOERROR", "A", "bing.com", "1.1.1.1", "1"]},
+        {"name": "UnknownType/DNSRequest", "metric_name": "dns_request_count",
+         "input": ["U", 0, []], "call": "response", "want": None},
+        {"name": "UnknownType/DNSResponse", "metric_name": "dns_response_count",
+         "input": ["U", 0, []], "call": "response", "want": None},
+        {"name": "Query/ResponseMetric", "metric_name": "dns_response_count", "input": ["Q", 0, []],
+         "call": "request", "want": None},
+        {"name": "Response/RequestMetric", "metric_name": "dns_request_count",
+         "input": ["R", 1, ["1.1.1.1"]], "call": "response", "want": None},
+    ],
+    # pkg/module/metrics/dns_test.go:337-456 (TestProcessLocalCtx): getLocalCtxValues mocked
+    "dns_local_ctx": [
+        {"name": "No context labels", "tdir": None, "local_values": None, "want": None},
+        {"name": "Only ingress labels", "tdir": 0,
+         "local_values": {"ingress": ["PodA", "NamespaceA"], "egress": None},
+         "want": ["NOERROR", "A", "bing.com", "1.1.1.1", "1", "PodA", "NamespaceA"]},
+        {"name": "Only egress labels", "tdir": 0,
+         "local_values": {"ingress": None, "egress": ["PodA", "NamespaceA"]},
+         "want": ["NOERROR", "A", "bing.com", "1.1.1.1", "1", "PodA", "NamespaceA"]},
+        {"name": "Both ingress and egress labels with ingress flow", "tdir": 1,
+         "local_values": {"ingress": ["PodA", "NamespaceA"], "egress": ["PodB", "NamespaceB"]},
+         "want": ["NOERROR", "A", "bing.com", "1.1.1.1", "1", "PodA", "NamespaceA"]},
+        {"name": "Both ingress and egress labels with egress flow", "tdir": 2,
+         "local_values": {"ingress": ["PodA", "NamespaceA"], "egress": ["PodB", "NamespaceB"]},
+         "want": ["NOERROR", "A", "bing.com", "1.1.1.1", "1", "PodB", "NamespaceB"]},
+    ],
+    # forward_test.go:31-310, drops_test.go:20-299, tcpflags_test.go:20-497:
+    # constructor nil-ness, advEnable, label schema and the WithLabelValues call count.
+    "metric_objects": [],
+    # pkg/enricher/enricher_test.go:41-157: secondary IPs resolve to their pods.
+    "enricher": {
+        "endpoints": [
+            {"name": "pod1", "namespace": "ns1", "ipv4": "1.1.1.1", "other_ipv4s": ["1.1.1.2"],
+             "owner_refs": [["Pod", "pod1-deployment"]]},
+            {"name": "pod2", "namespace": "ns2", "ipv4": "2.2.2.2", "other_ipv4s": ["2.2.2.3"],
+             "owner_refs": [["Pod", "pod2-deployment"]]},
+        ],
+        "flow": {"source": "1.1.1.2", "destination": "2.2.2.3"},
+        "want_source": ["ns1", "pod1"], "want_destination": ["ns2", "pod2"],
+    },
+    # pkg/utils/utils_linux_test.go:19-73 (TestToFlow) and :75-96 (TestAddPacketSize)
+    "to_flow": {
+        "args": ["1.1.1.1", "2.2.2.2", 443, 80, 6],
+        "want_ip": ["1.1.1.1", "2.2.2.2", 1], "want_ports": [443, 80],
+        "obs_points": [[0, "TO_STACK"], [1, "TO_ENDPOINT"], [2, "FROM_NETWORK"],
+                       [3, "TO_NETWORK"], [4, "UNKNOWN_POINT"]],
+        "packet_size": 100,
+    },
+    # pkg/utils/utils_linux_test.go:120-167 (TestAddDropReason): verdict DROPPED + reason names
+    "drop_reason": [[0, "IPTABLE_RULE_DROP"], [1, "IPTABLE_NAT_DROP"], [5, "CONNTRACK_ADD_DROP"],
+                    [6, "UNKNOWN_DROP"]],
+}
+
+
+def mo(family, name, opts, flow, labels, calls, nil=False, adv=False, local=False, src="forward_test.go"):
+    kat["metric_objects"].append({"family": family, "name": name, "opts": opts, "flow": flow,
+                                  "labels": labels, "metric_call": calls, "nil_obj": nil,
+                                  "adv": adv, "local": local, "source": src})
+
+
+def o(name="", src=None, dst=None):
+    return {"metric_name": name, "source_labels": src, "destination_labels": dst}
+
+
+# forward_test.go:35-278
+mo("forward", "empty opts", o(), fl(), ["direction"], 0, nil=True)
+mo("forward", "plain opts", o("forward"), fl(F), ["direction"], 1)
+mo("forward", "plain opts with nil flow", o("forward"), None, ["direction"], 0)
+mo("forward", "plain opts dropped verdict", o("forward"), fl(D), ["direction"], 0)
+mo("forward", "source opts 1 without metric name", o(src=ALL), fl(), ["direction"], 0, nil=True)
+mo("forward", "source opts 1", o("forward", src=ALL), fl(F), ["direction"] + SRC_ALL, 1, adv=True)
+mo("forward", "dest opts 1", o("FORWARD", dst=ALL), fl(F), ["direction"] + DST_ALL, 1, adv=True)
+mo("forward", "source opts with flow", o("forward", src=ALL), fl(F, source=EMPTY_EP),
+   ["direction"] + SRC_ALL, 1, adv=True)
+mo("forward", "drop source opts expect nil", o("drop", src=ALL), fl(F, source=EMPTY_EP),
+   ["direction"] + SRC_ALL, 1, nil=True, adv=True)
+mo("forward", "source opts with flow dropped verdict", o("forward", src=ALL),
+   fl(D, source=EMPTY_EP), ["direction"] + SRC_ALL, 0, adv=True)
+mo("forward", "source opts with flow in local context", o("forward", src=ALL),
+   fl(F, source=EMPTY_EP), ["direction"] + LOC_ALL, 1, adv=True, local=True)
+mo("forward", "dest opts 1 with flow in local context", o("FORWARD", src=ALL),
+   fl(F, destination=EMPTY_EP), ["direction"] + LOC_ALL, 1, adv=True, local=True)
+mo("forward", "src and dest opts 1 with flow in local context", o("FORWARD", src=ALL),
+   fl(F, source=EMPTY_EP, destination=EMPTY_EP), ["direction"] + LOC_ALL, 2, adv=True, local=True)
+# drops_test.go:23-265
+S = "drops_test.go"
+mo("drop", "empty opts", o(), fl(F), ["reason"], 0, nil=True, src=S)
+mo("drop", "empty opts dropped", o(), fl(D), ["reason"], 0, nil=True, src=S)
+mo("drop", "plain opts", o("drop"), fl(), ["reason", "direction"], 0, src=S)
+mo("drop", "plain opts dropped verdict", o("drop"), fl(D), ["reason", "direction"], 1, src=S)
+mo("drop", "plain opts dropped verdict nil flow", o("drop"), None, ["reason", "direction"], 0, src=S)
+mo("drop", "source opts 1 without metric name", o(src=ALL), fl(D), ["reason", "direction"], 1,
+   nil=True, src=S)
+mo("drop", "source opts 1", o("drop", src=ALL), fl(D), ["reason", "direction"] + SRC_ALL, 1,
+   adv=True, src=S)
+mo("drop", "dest opts 1", o("DROP", dst=ALL), fl(D), ["reason", "direction"] + DST_ALL, 1,
+   adv=True, src=S)
+mo("drop", "source opts with flow", o("drop", src=ALL), fl(D, source=EMPTY_EP),
+   ["reason", "direction"] + SRC_ALL, 1, adv=True, src=S)
+mo("drop", "forward source opts with flow", o("forward", src=ALL), fl(D, source=EMPTY_EP),
+   ["reason", "direction"] + SRC_ALL, 1, nil=True, adv=True, src=S)
+mo("drop", "drop source opts with flow in localcontext", o("drop", src=ALL),
+   fl(D, source=EMPTY_EP), ["reason", "direction"] + LOC_ALL, 1, adv=True, local=True, src=S)
+mo("drop", "drop source opts with destination flow in localcontext", o("drop", src=ALL),
+   fl(D, destination=EMPTY_EP), ["reason", "direction"] + LOC_ALL, 1, adv=True, local=True, src=S)
+mo("drop", "drop source opts with source and destination flow in localcontext", o("drop", src=ALL),
+   fl(D, source=EMPTY_EP, destination=EMPTY_EP), ["reason", "direction"] + LOC_ALL, 2, adv=True,
+   local=True, src=S)
+# tcpflags_test.go:24-467
+S = "tcpflags_test.go"
+EXCEPT_ACK = {k: v for k, v in ALL_FLAGS.items() if k != "ACK"}
+EXCEPT_SYN = {k: v for k, v in ALL_FLAGS.items() if k != "SYN"}
+mo("tcpflags", "empty opts", o(), fl(), [], 1, nil=True, src=S)
+mo("tcpflags", "empty opts nil flow", o("tcpflags"), None, ["flag"], 0, src=S)
+mo("tcpflags", "plain opts", o("tcpflags"), fl(), ["flag"], 0, src=S)
+mo("tcpflags", "source opts 1 without metric name", o(src=ALL), fl(F), ["flag"] + SRC_ALL, 0,
+   nil=True, adv=False, src=S)
+mo("tcpflags", "source opts 1", o("flag", src=ALL), fl(), ["flag"] + SRC_ALL, 0, adv=True, src=S)
+mo("tcpflags", "dest opts 1", o("flag", dst=ALL), fl(F), ["flag"] + DST_ALL, 0, adv=True, src=S)
+mo("tcpflags", "source opts with flow", o("flag", src=ALL), fl(F, source=EMPTY_EP),
+   ["flag"] + SRC_ALL, 0, adv=True, src=S)
+mo("tcpflags", "source opts with flow with flags", o("flag", src=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp({"SYN": True})), ["flag"] + SRC_ALL, 1, adv=True, src=S)
+mo("tcpflags", "source opts with nil flow", o("flag", src=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp(None)), ["flag"] + SRC_ALL, 0, adv=True, src=S)
+mo("tcpflags", "source opts with flow with all flags except ack", o("flag", src=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp(EXCEPT_ACK)), ["flag"] + SRC_ALL, 7, adv=True, src=S)
+mo("tcpflags", "dest opts with flow with all flags", o("flag", dst=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp(ALL_FLAGS)), ["flag"] + DST_ALL, 7, adv=True, src=S)
+mo("tcpflags", "dest opts with flow with all but syn flags", o("flag", dst=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp(EXCEPT_SYN)), ["flag"] + DST_ALL, 7, adv=True, src=S)
+mo("tcpflags", "dest opts with flow with all flags dropped verdict", o("flag", dst=ALL),
+   fl(D, source=EMPTY_EP, l4=tcp(ALL_FLAGS)), ["flag"] + DST_ALL, 0, adv=True, src=S)
+mo("tcpflags", "local ctx dest opts with flow with all flags", o("flag", src=ALL),
+   fl(F, source=EMPTY_EP, l4=tcp(ALL_FLAGS)), ["flag"] + LOC_ALL, 7, adv=True, local=True, src=S)
+mo("tcpflags", "local ctx no endpoints with all flags", o("flag", src=ALL),
+   fl(F, l4=tcp(ALL_FLAGS)), ["flag"] + LOC_ALL, 0, adv=True, local=True, src=S)
+mo("tcpflags", "local ctx src and dest opts with flow with all flags", o("flag", src=ALL),
+   fl(F, source=EMPTY_EP, destination=EMPTY_EP, l4=tcp(ALL_FLAGS)), ["flag"] + LOC_ALL, 14,
+   adv=True, local=True, src=S)
+
+if __name__ == "__main__":
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kat.json")
+    with open(out, "w") as f:
+        json.dump(kat, f, indent=1, sort_keys=True)
+    print("wrote", out, len(kat["metric_objects"]), "metric-object cases")
