@@ -64,22 +64,18 @@ def gen_device_records(n: int, pods, seed: int, device, gen_kw, chunk: int = 8_0
 
 
 def cpu_baseline(cfg_name: str, pods, spec, sample: int, seed: int, gen_kw):
-    """The oracle (a 1-thread port of the Go path) timed on a bounded sample."""
-    from oracle import oracle as O
-    from oracle import records as R
+    """The C port of the reference path (oracle/ref_cpu.c, go-shaped: dotted-string IPs,
+    string-keyed cache and label maps; enrich + every ProcessFlow per flow on one thread)
+    timed on a bounded sample of the same workload."""
+    from oracle.ref_cpu import RefCPU
     from retina_amd import workloads as W
     recs = W.gen_records(sample, pods, seed, **gen_kw)
-    eps = [R.EndpointSpec(e.namespace, e.name, list(e.ips), e.owner_refs) for e in pods.endpoints]
-    cache = R.build_cache(eps)
-    module = O.Module(remote_context=False)
-    module.reconcile(R.spec_from_json(spec))
-    b = R.Batch(recs.src_ip, recs.dst_ip, recs.bytes, recs.meta, recs.ports, recs.dns_id)
-    t0 = time.perf_counter()
-    R.replay(b, cache, module)
-    dt = time.perf_counter() - t0
+    r = RefCPU(spec, pods.endpoints, False, recs.dns)
+    dt = r.process(recs)
+    r.close()
     return {"value": sample / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "%d records of config %s through oracle/oracle.py (enrich + every metric's "
-                      "ProcessFlow, one flow at a time), %.1f s" % (sample, cfg_name, dt)}
+            "sample": "%d records of config %s through oracle/ref_cpu.c (C port of enricher.go + "
+                      "metrics module, 1 thread), %.1f s" % (sample, cfg_name, dt)}
 
 
 def main():
@@ -89,7 +85,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: config size)")
-    ap.add_argument("--cpu-sample", type=int, default=400_000)
+    ap.add_argument("--cpu-sample", type=int, default=12_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

@@ -119,8 +119,9 @@ int gpuagg_dns_intern(gpuagg_ctx *ctx, uint32_t rcode, const char *qtypes_joined
  *                  utils.Int2ip turns into "a.b.c.d", utils_linux.go:51-55)
  *  bytes           RetinaMetadata.Bytes (utils.PacketSize, flow_utils.go:267-274)
  *  meta            bits  0-7  L4 protocol (6 TCP, 17 UDP, other: no L4)
- *                  bits  8-15 flow.Verdict (1 FORWARDED, 2 DROPPED, 15 RETRANSMISSION,
- *                             16 DNS; flow_utils.go:19-21)
+ *                  bits  8-15 verdict passed to utils.ToFlow (1 FORWARDED, 2 DROPPED,
+ *                             15 RETRANSMISSION, 16 DNS; flow_utils.go:19-21); 0 means
+ *                             FORWARDED, as ToFlow maps it (flow_utils.go:94-96)
  *                  bits 16-17 flow.TrafficDirection (0 UNKNOWN, 1 INGRESS, 2 EGRESS)
  *                  bits 18-20 RetinaMetadata.DropReason (metadata_linux.pb.go:76-84)
  *                  bits 21-26 TCP flags FIN,SYN,RST,PSH,ACK,URG (types_linux.go:22-31)

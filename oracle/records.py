@@ -74,6 +74,7 @@ def flow_from_record(src_ip: int, dst_ip: int, nbytes: int, meta: int, ports: in
     f = O.to_flow(O.int2ip(src_ip), O.int2ip(dst_ip), sport, dport, proto, 0, verdict)
     f.traffic_direction = tdir
     meta_ext = O.RetinaMetadata(bytes=nbytes)
+    verdict = f.verdict  # after ToFlow's 0 -> FORWARDED (flow_utils.go:94-96)
     if verdict in (O.VERDICT_FORWARDED, O.VERDICT_RETRANSMISSION):
         O.add_tcp_flags(f, (flags & 2) >> 1, (flags & 16) >> 4, flags & 1, (flags & 4) >> 2,
                         (flags & 8) >> 3, (flags & 32) >> 5)

@@ -24,7 +24,12 @@ namespace gpuagg {
 
 // ---- record meta word (include/gpuagg.h) -----------------------------------------
 GA_HD uint32_t meta_proto(uint32_t m) { return m & 0xFFu; }
-GA_HD uint32_t meta_verdict(uint32_t m) { return (m >> 8) & 0xFFu; }
+// The column holds the verdict the producer passed to utils.ToFlow, which turns 0 into
+// FORWARDED (flow_utils.go:94-96).
+GA_HD uint32_t meta_verdict(uint32_t m) {
+  const uint32_t v = (m >> 8) & 0xFFu;
+  return v ? v : 1u;
+}
 GA_HD uint32_t meta_tdir(uint32_t m) { return (m >> 16) & 3u; }
 GA_HD uint32_t meta_reason(uint32_t m) { return (m >> 18) & 7u; }
 GA_HD uint32_t meta_flags(uint32_t m) { return (m >> 21) & 0x3Fu; }

@@ -160,8 +160,8 @@ def gen_records(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, drop_fr
                         for a in range(int(na[j]))]
                 key = (int(rc[j]), int(qt[j]), int(q[j]), int(na[j]))
                 p = (int(rc[j]), [qtypes[qt[j]]], "q%d.example.com" % q[j], ipsl, int(na[j]))
-            else:
-                key = (0, int(qt[j]), int(q[j]), -1)
+            else:  # same key as a rcode-0, no-answer response: identical label payload
+                key = (0, int(qt[j]), int(q[j]), 0)
                 p = (0, [qtypes[qt[j]]], "q%d.example.com" % q[j], [], 0)
             i = index.get(key)
             if i is None:

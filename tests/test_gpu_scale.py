@@ -1,0 +1,72 @@
+"""GPU parity at larger sizes: against the C port (millions of records) and, at the full
+BASELINE.json C2 size (100M records), against the numpy restatement -- exact, plus
+size-independent properties (determinism, host-fed == device-resident, chunking)."""
+
+import numpy as np
+import pytest
+
+from oracle.ref_cpu import RefCPU, values_only
+from oracle.vectorized import LocalDense
+from retina_amd import workloads as W
+
+from .helpers import diff_series, engine_series, make_engine
+
+pytestmark = pytest.mark.gpu
+
+MID = [
+    ("c1-local", W.C1_LOCAL, False, 10_000, {}),
+    ("c1-remote", W.C1_REMOTE, True, 10_000, {}),
+    ("c2-local", W.LOCAL_FWD_DROP, False, 10_000, {}),
+    ("c4-zipf", W.LOCAL_FWD_DROP, False, 10_000, {"zipf": 1.2}),
+    ("c5-local", W.C5_SPEC, False, 100_000, {"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
+]
+
+
+@pytest.mark.parametrize("cid,sp,remote,npods,gen", MID, ids=[m[0] for m in MID])
+def test_midsize_vs_c_port(gpu_device, cid, sp, remote, npods, gen):
+    pods = W.make_pods(npods, seed=2)
+    recs = W.gen_records(1_000_000, pods, seed=77, **gen)
+    r = RefCPU(sp, pods.endpoints, remote, recs.dns)
+    r.process(recs)
+    want = r.series()
+    r.close()
+    got = values_only(engine_series(recs, pods, sp, remote, gpu_device, host_fed=False, chunks=3,
+                                    sparse_capacity_log2=23))
+    assert got == want, diff_series(got, want)
+
+
+def test_full_c2_exact(gpu_device):
+    """BASELINE.json config 2 at full size: 100M records, 10k pods, 1 MI355X."""
+    import torch
+    from retina_amd import GpuAgg
+    pods = W.make_pods(10_000, seed=2)
+    n, chunk = 100_000_000, 10_000_000
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, gpu_device)
+    v = LocalDense(W.LOCAL_FWD_DROP, pods.endpoints)
+    dev = torch.device("cuda", gpu_device)
+    cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(6)]
+    for k in range(n // chunk):
+        r = W.gen_records(chunk, pods, seed=1000 + k)
+        v.add(r)
+        for t, a in zip(cols, (r.src_ip, r.dst_ip, r.bytes, r.meta, r.ports, r.dns_id)):
+            t[k * chunk:(k + 1) * chunk].copy_(torch.from_numpy(a.view(np.int32)))
+    dc = GpuAgg.device_columns(*cols)
+    g.submit_device(dc, n)
+    got = g.snapshot()
+    want = v.series()
+    assert got == want, diff_series(got, want)
+    # determinism: a second pass doubles every series exactly
+    g.submit_device(dc, n)
+    got2 = g.snapshot()
+    assert got2 == {k: 2 * x for k, x in got.items()}
+    g.close()
+
+
+def test_host_fed_equals_device_and_chunking(gpu_device):
+    pods = W.make_pods(2_000, seed=3)
+    recs = W.gen_records(3_000_000, pods, seed=3, drop_frac=0.1, retrans_frac=0.05, dns_frac=0.1,
+                         udp_frac=0.1, n_queries=2000)
+    sp = W.LOCAL_FWD_DROP + W.C5_SPEC
+    a = engine_series(recs, pods, sp, False, gpu_device, host_fed=True, chunks=1)
+    b = engine_series(recs, pods, sp, False, gpu_device, host_fed=False, chunks=7)
+    assert a == b, diff_series(a, b)

@@ -1,0 +1,51 @@
+"""Pins the two fast checkers to the per-flow oracle: the C port (oracle/ref_cpu.c, also
+the bench CPU baseline) and the numpy restatement (oracle/vectorized.py) used at full
+batch sizes."""
+
+import zlib
+
+import pytest
+
+from oracle.ref_cpu import RefCPU, values_only
+from oracle.vectorized import LocalDense
+from retina_amd import workloads as W
+
+from .helpers import oracle_series
+from .test_gpu_parity import CASES
+
+
+@pytest.fixture(scope="module")
+def pods():
+    return W.make_pods(400, seed=11)
+
+
+@pytest.mark.parametrize("cid,sp,remote,gen", CASES, ids=[c[0] for c in CASES])
+def test_ref_cpu_matches_oracle(pods, cid, sp, remote, gen):
+    recs = W.gen_records(12_000, pods, seed=zlib.crc32(cid.encode()) & 0xFFFF, **gen)
+    want = values_only(oracle_series(recs, pods, sp, remote))
+    r = RefCPU(sp, pods.endpoints, remote, recs.dns)
+    r.process(recs)
+    got = r.series()
+    r.close()
+    assert got == want
+
+
+def test_ref_cpu_rejects_panicking_specs(pods):
+    with pytest.raises(ValueError):
+        RefCPU([{"metric_name": "dns_foo", "source_labels": ["podname"]}], pods.endpoints, False)
+    with pytest.raises(ValueError):  # local context without sourceLabels: nil srcCtx
+        RefCPU([{"metric_name": "forward_count"}], pods.endpoints, False)
+
+
+@pytest.mark.parametrize("labels", [["namespace", "podname"], ["workload"], ["service"],
+                                    ["podname", "workload", "service"]])
+def test_vectorized_matches_oracle(pods, labels):
+    sp = [{"metric_name": m, "source_labels": labels}
+          for m in ("forward_count", "forward_bytes", "drop_count", "drop_bytes", "tcp_flag_gauges",
+                    "tcp_retransmission_count")]
+    recs = W.gen_records(15_000, pods, seed=5, drop_frac=0.1, retrans_frac=0.05, udp_frac=0.15,
+                         other_proto_frac=0.05, odd_frac=0.1)
+    want = oracle_series(recs, pods, sp, False)
+    v = LocalDense(sp, pods.endpoints)
+    v.add(recs)
+    assert v.series() == want
