@@ -105,7 +105,23 @@ GA_HD uint64_t fmix64(uint64_t k) {
 constexpr uint64_t kIpEmpty = ~0ULL;
 constexpr uint32_t kSlotBits = 21;
 constexpr uint32_t kMaxSlot = (1u << kSlotBits) - 2;  // slot ids 0..kMaxSlot
-GA_HD uint32_t ip_hash(uint32_t ip) { return (uint32_t)fmix64((uint64_t)ip ^ 0x9E3779B97F4A7C15ULL); }
+GA_HD uint32_t ip_hash(uint32_t ip) {  // murmur3 fmix32: 2 mul + 3 xorshift
+  ip ^= ip >> 16;
+  ip *= 0x85ebca6bu;
+  ip ^= ip >> 13;
+  ip *= 0xc2b2ae35u;
+  ip ^= ip >> 16;
+  return ip;
+}
+// Dense bins kept in LDS per workgroup: u64 = count << 40 | bytes (bytes < 2^16 per
+// update, <= 2^24 records per workgroup between flushes => both fields exact).
+constexpr uint32_t kLdsBytes = 160 * 1024;
+constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - 2;  // + one word for the spill counter
+constexpr uint32_t kLdsByteLimit = 1u << 16;
+constexpr uint64_t kLdsCountOne = 1ULL << 40;
+constexpr uint64_t kLdsBytesMask = kLdsCountOne - 1;
+constexpr uint64_t kMaxRecordsPerBlock = 1ULL << 24;
+constexpr uint32_t kMaxSpillWindows = 16;
 GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
 }

@@ -7,12 +7,20 @@
 // tcpflags.go:68-132, tcpretrans.go:247-298, dns.go:462-540), plus the count-min /
 // HyperLogLog sketch updates (new).
 //
-// Dense local-context counters are privatised per workgroup in LDS when the group
-// key space fits (see DenseLds below) and flushed once per workgroup with coalesced
-// 64-bit atomics; everything else goes straight to HBM with device-scope atomics.
+// Memory plan:
+//  * records stream from HBM once, 16 B per lane per column (dwordx4) when aligned;
+//  * the IP table (<= a few MB) stays in each XCD's L2;
+//  * dense counters [0, L) are privatised per workgroup in LDS (one 1024-thread
+//    workgroup per CU, 160 KB) as packed count<<40|bytes words and flushed once per
+//    workgroup with coalesced 64-bit atomics;
+//  * dense counters >= L are appended to a per-workgroup spill list (no global
+//    atomics, no global counter) and folded by spill_window_kernel, which holds one
+//    160 KB window of them in LDS per workgroup;
+//  * sparse (remote-context / ip / port / DNS) keys go to an HBM hash table.
 #include <hip/hip_runtime.h>
 
 #include "gpuagg_internal.h"
+#include "gpuagg_launch.h"
 
 namespace gpuagg {
 
@@ -40,19 +48,43 @@ struct DevCols {
   const uint32_t *src, *dst, *bytes, *meta, *ports, *dns;
 };
 
+struct KArgs {
+  DevCols c;
+  uint64_t n;
+  uint64_t chunk;  // records per workgroup (multiple of 4)
+  DevIpTable t;
+  DevDense d;
+  DevSparse s;
+  DevSketch sk;
+  uint32_t lds_bins;  // L: dense bins privatised in LDS
+  uint32_t spill_cap;
+  unsigned long long *spill;  // [gridDim.x][spill_cap] or null
+  uint32_t *spill_count;      // [gridDim.x]
+  Plan p;
+};
+
 struct Lk {
   int32_t slot;  // -1: not a pod (flow.Endpoint stays nil)
   uint32_t api;  // endpoint is the kubernetes-apiserver pseudo pod (types.go:358-368)
 };
 
-__device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
-  uint32_t h = ip_hash(ip) & t.mask;
-  for (;;) {
-    const uint64_t e = t.slots[h];
-    if (e == kIpEmpty) return Lk{-1, 0};
-    if ((uint32_t)e == ip) return Lk{(int32_t)((e >> 32) & ((1u << kSlotBits) - 1)), (uint32_t)(e >> 53) & 1u};
+__device__ __forceinline__ Lk lk_from(uint64_t e) {
+  if (e == kIpEmpty) return Lk{-1, 0};
+  return Lk{(int32_t)((e >> 32) & ((1u << kSlotBits) - 1)), (uint32_t)(e >> 53) & 1u};
+}
+
+// Resolves a probe chain whose first entry was already loaded.
+__device__ __forceinline__ Lk ip_resolve(const DevIpTable &t, uint32_t ip, uint32_t h, uint64_t e) {
+  while (e != kIpEmpty && (uint32_t)e != ip) {
     h = (h + 1) & t.mask;
+    e = t.slots[h];
   }
+  return lk_from(e);
+}
+
+__device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
+  const uint32_t h = ip_hash(ip) & t.mask;
+  return ip_resolve(t, ip, h, t.slots[h]);
 }
 
 // Insert-or-add into the sparse table. No lane ever waits for another: a lane that
@@ -87,6 +119,33 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
   atomicAdd(s.dropped, 1ULL);
 }
 
+// Dense counter updates: LDS window, spill list, or (fallback) global atomics.
+struct DenseSink {
+  unsigned long long *lds;
+  uint32_t L;
+  unsigned int *spill_ctr;  // in LDS
+  unsigned long long *spill;
+  uint32_t spill_cap;
+  DevDense d;
+
+  __device__ __forceinline__ void add(uint64_t bin, uint32_t nbytes) const {
+    if (bin < L) {
+      if (nbytes < kLdsByteLimit) {
+        atomicAdd(&lds[bin], kLdsCountOne | nbytes);
+        return;
+      }
+    } else if (spill) {
+      const unsigned int pos = atomicAdd(spill_ctr, 1u);
+      if (pos < spill_cap) {
+        spill[pos] = (bin << 32) | nbytes;
+        return;
+      }
+    }
+    atomicAdd(&d.cnt[bin], 1ULL);
+    if (nbytes) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
+  }
+};
+
 // Side tuple of a context (types.go:418-505): only the fields the options read.
 struct SideKey {
   uint32_t ip, slot1, port17;
@@ -113,14 +172,8 @@ __device__ __forceinline__ bool family_matches(uint32_t fam, uint32_t verdict, u
   return false;
 }
 
-__device__ __forceinline__ void dense_add(const DevDense &d, uint64_t idx, uint32_t fam,
-                                          uint32_t nbytes) {
-  atomicAdd(&d.cnt[idx], 1ULL);
-  if (fam <= FAM_DROP && nbytes) atomicAdd(&d.byt[idx], (unsigned long long)nbytes);
-}
-
 // One record through every metric group.
-__device__ __forceinline__ void apply_groups(const Plan &p, const DevDense &d,
+__device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
                                              const DevSparse &s, uint32_t sip, uint32_t dip,
                                              uint32_t nbytes, uint32_t meta, uint32_t ports,
                                              uint32_t dns, const Lk &ls, const Lk &ld) {
@@ -135,7 +188,7 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DevDense &d,
     const GroupPlan gp = p.g[g];
     const uint32_t fam = gp.family;
     if (!family_matches(fam, verdict, proto, dnstype, flagmask)) continue;
-    const uint64_t addb = (fam <= FAM_DROP) ? nbytes : 0u;
+    const uint32_t addb = (fam <= FAM_DROP) ? nbytes : 0u;
 
     if (p.local) {
       // getLocalCtxValues (types.go:379-416): src -> egress, dst -> ingress, both
@@ -164,9 +217,9 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DevDense &d,
           const uint64_t key = gp.key_mode ? (uint64_t)lk.slot : 0u;
           const uint64_t row = gp.dense_base + (key * 2 + (uint64_t)side) * gp.nsub;
           if (fam == FAM_TCPFLAGS) {
-            for (uint32_t m = flagmask; m; m &= m - 1) dense_add(d, row + __builtin_ctz(m), fam, 0);
+            for (uint32_t m = flagmask; m; m &= m - 1) ds.add(row + __builtin_ctz(m), 0);
           } else {
-            dense_add(d, row + (fam == FAM_DROP ? reason : 0u), fam, nbytes);
+            ds.add(row + (fam == FAM_DROP ? reason : 0u), addb);
           }
         } else {
           const SideKey k = side == 0 ? side_key(gp.src_opts, dip, ld, dport, proto)
@@ -230,18 +283,120 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
 }
 
 template <bool kSketch>
-__global__ __launch_bounds__(256) void aggregate_kernel(DevCols c, uint32_t n, DevIpTable t,
-                                                        Plan p, DevDense d, DevSparse s,
-                                                        DevSketch sk) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t sip = c.src[i], dip = c.dst[i], nbytes = c.bytes[i], meta = c.meta[i];
-    const uint32_t ports = (p.need_ports || kSketch) ? c.ports[i] : 0u;
-    const uint32_t dns = p.need_dns ? c.dns[i] : 0u;
-    const Lk ls = ip_lookup(t, sip);
-    const Lk ld = ip_lookup(t, dip);
-    apply_groups(p, d, s, sip, dip, nbytes, meta, ports, dns, ls, ld);
-    if (kSketch) sketch_update(sk, sip, dip, ports, meta_proto(meta), ls);
+__device__ __forceinline__ void one_record(const KArgs &a, const DenseSink &ds, uint32_t sip,
+                                           uint32_t dip, uint32_t nb, uint32_t meta,
+                                           uint32_t ports, uint32_t dns, const Lk &ls,
+                                           const Lk &ld) {
+  apply_groups(a.p, ds, a.s, sip, dip, nb, meta, ports, dns, ls, ld);
+  if (kSketch) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
+}
+
+// One workgroup per CU when LDS bins are in use. Workgroup b aggregates the
+// contiguous record range [b*chunk, (b+1)*chunk).
+template <bool kVec, bool kSketch>
+__global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  const uint32_t L = a.lds_bins;
+  for (uint32_t i = threadIdx.x; i <= L; i += blockDim.x) lds[i] = 0ULL;
+  __syncthreads();
+  DenseSink ds{lds, L, (unsigned int *)&lds[L],
+               a.spill ? a.spill + (size_t)blockIdx.x * a.spill_cap : nullptr, a.spill_cap, a.d};
+
+  const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
+  const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
+  const bool need_ports = a.p.need_ports || kSketch;
+  const bool need_dns = a.p.need_dns;
+  uint64_t tail = start;
+  if (kVec && start < end) {
+    const uint64_t vend = start + ((end - start) & ~3ULL);
+    const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
+    const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
+    const uint4 *p4 = (const uint4 *)a.c.ports, *q4 = (const uint4 *)a.c.dns;
+    for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
+      const uint64_t v = i >> 2;
+      const uint4 vs = s4[v], vd = d4[v], vb = b4[v], vm = m4[v];
+      const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
+      const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
+      const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
+      uint32_t h[8];
+      uint64_t e[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = ip_hash(ip[k]) & a.t.mask;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = a.t.slots[h[k]];  // 8 independent probes in flight
+      Lk lk[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lk[k] = ip_resolve(a.t, ip[k], h[k], e[k]);
+      one_record<kSketch>(a, ds, vs.x, vd.x, vb.x, vm.x, vp.x, vq.x, lk[0], lk[4]);
+      one_record<kSketch>(a, ds, vs.y, vd.y, vb.y, vm.y, vp.y, vq.y, lk[1], lk[5]);
+      one_record<kSketch>(a, ds, vs.z, vd.z, vb.z, vm.z, vp.z, vq.z, lk[2], lk[6]);
+      one_record<kSketch>(a, ds, vs.w, vd.w, vb.w, vm.w, vp.w, vq.w, lk[3], lk[7]);
+    }
+    tail = vend;
+  }
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
+    const uint32_t sip = a.c.src[i], dip = a.c.dst[i];
+    const Lk ls = ip_lookup(a.t, sip), ld = ip_lookup(a.t, dip);
+    one_record<kSketch>(a, ds, sip, dip, a.c.bytes[i], a.c.meta[i], need_ports ? a.c.ports[i] : 0u,
+                        need_dns ? a.c.dns[i] : 0u, ls, ld);
+  }
+
+  __syncthreads();
+  // flush: consecutive lanes -> consecutive bins (256-B contiguous atomic wave-instructions)
+  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) {
+    const unsigned long long v = lds[i];
+    if (v) {
+      atomicAdd(&a.d.cnt[i], v >> 40);
+      const unsigned long long by = v & kLdsBytesMask;
+      if (by) atomicAdd(&a.d.byt[i], by);
+    }
+  }
+  if (a.spill && threadIdx.x == 0) {
+    const unsigned int c = *ds.spill_ctr;
+    a.spill_count[blockIdx.x] = c < a.spill_cap ? c : a.spill_cap;
+  }
+}
+
+// Folds the spill lists into dense counters, one LDS window of bins per workgroup.
+// Workgroups of the same spill partition share blockIdx % 8 (one XCD under the
+// observed round-robin placement -- speed only), so the 8..16 window passes over a
+// partition mostly hit that XCD's L2.
+__global__ __launch_bounds__(1024) void spill_window_kernel(
+    const unsigned long long *spill, const uint32_t *spill_count, uint32_t n_lists,
+    uint32_t spill_cap, uint32_t L, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
+  const uint32_t b = blockIdx.x;
+  const uint32_t w = (b >> 3) % nwin;
+  const uint32_t part = (b & 7u) + 8u * (b / (8u * nwin));
+  const uint32_t nparts = gridDim.x / nwin;
+  const uint64_t lo = (uint64_t)L + (uint64_t)w * W;
+  const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
+  __syncthreads();
+  for (uint32_t l = part; l < n_lists; l += nparts) {
+    const uint32_t cnt = spill_count[l];
+    const unsigned long long *e = spill + (size_t)l * spill_cap;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+      const unsigned long long v = e[j];
+      const uint64_t bin = v >> 32;
+      if (bin < lo || bin >= hi) continue;
+      const uint32_t nb = (uint32_t)v;
+      if (nb < kLdsByteLimit) {
+        atomicAdd(&win[bin - lo], kLdsCountOne | nb);
+      } else {
+        atomicAdd(&d.cnt[bin], 1ULL);
+        atomicAdd(&d.byt[bin], (unsigned long long)nb);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
+    const unsigned long long v = win[i];
+    if (v) {
+      atomicAdd(&d.cnt[lo + i], v >> 40);
+      const unsigned long long by = v & kLdsBytesMask;
+      if (by) atomicAdd(&d.byt[lo + i], by);
+    }
   }
 }
 
@@ -276,12 +431,7 @@ __global__ void sparse_import_kernel(DevSparse s, const unsigned long long *in, 
   }
 }
 
-}  // namespace gpuagg
-
 // ---- launch wrappers called by the host runtime ---------------------------------------
-#include "gpuagg_launch.h"
-
-namespace gpuagg {
 
 static DevSparse dev_sparse(const SparseView &v) {
   return DevSparse{(unsigned long long *)v.k0, (unsigned long long *)v.k1,
@@ -289,22 +439,47 @@ static DevSparse dev_sparse(const SparseView &v) {
                    (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped};
 }
 
+template <bool V, bool S>
+static hipError_t launch_agg(const KArgs &k, uint32_t blocks, uint32_t threads, size_t lds,
+                             hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute((const void *)aggregate_kernel<V, S>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((aggregate_kernel<V, S>), dim3(blocks), dim3(threads), lds, st, k);
+  return hipGetLastError();
+}
+
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st) {
-  DevCols c{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
-  DevIpTable t{a.ip_slots, a.ip_mask};
-  DevDense d{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
-  DevSparse s = dev_sparse(a.sparse);
-  DevSketch sk{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};
+  if (a.n == 0) return hipSuccess;
+  KArgs k{};
+  k.c = DevCols{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
+  k.n = a.n;
+  k.chunk = a.chunk;
+  k.t = DevIpTable{a.ip_slots, a.ip_mask};
+  k.d = DevDense{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
+  k.s = dev_sparse(a.sparse);
+  k.sk = DevSketch{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};
+  k.lds_bins = a.lds_bins;
+  k.spill = (unsigned long long *)a.spill;
+  k.spill_cap = a.spill_cap;
+  k.spill_count = a.spill_count;
+  k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  uint32_t blocks = (uint32_t)((a.n + 255) / 256);
-  if (blocks > a.max_blocks) blocks = a.max_blocks;
-  if (blocks == 0) return hipSuccess;
-  if (sketch)
-    hipLaunchKernelGGL(aggregate_kernel<true>, dim3(blocks), dim3(256), 0, st, c, (uint32_t)a.n, t,
-                       a.plan, d, s, sk);
+  const size_t lds = ((size_t)a.lds_bins + 1) * 8;
+  hipError_t e;
+  if (a.vec)
+    e = sketch ? launch_agg<true, true>(k, a.blocks, a.threads, lds, st)
+               : launch_agg<true, false>(k, a.blocks, a.threads, lds, st);
   else
-    hipLaunchKernelGGL(aggregate_kernel<false>, dim3(blocks), dim3(256), 0, st, c, (uint32_t)a.n,
-                       t, a.plan, d, s, sk);
+    e = sketch ? launch_agg<false, true>(k, a.blocks, a.threads, lds, st)
+               : launch_agg<false, false>(k, a.blocks, a.threads, lds, st);
+  if (e != hipSuccess || !a.spill) return e;
+  e = hipFuncSetAttribute((const void *)spill_window_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)a.win_bins * 8, st,
+                     (const unsigned long long *)a.spill, a.spill_count, a.blocks, a.spill_cap,
+                     a.lds_bins, a.dense_len, a.win_bins, a.nwin, k.d);
   return hipGetLastError();
 }
 

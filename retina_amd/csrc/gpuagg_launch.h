@@ -30,7 +30,16 @@ struct LaunchArgs {
   uint32_t cms_depth, cms_wlog2;
   uint8_t *hll;
   uint32_t hll_p;
-  uint32_t max_blocks;
+  // geometry (see gpuagg_runtime.cpp: plan_launch)
+  uint32_t blocks, threads;
+  uint64_t chunk;       // records per workgroup, multiple of 4
+  bool vec;             // every column 16-byte aligned: dwordx4 loads
+  uint32_t lds_bins;    // dense bins [0, lds_bins) privatised in LDS
+  uint64_t dense_len;
+  uint64_t *spill;      // per-workgroup spill lists, or null
+  uint32_t spill_cap;
+  uint32_t *spill_count;
+  uint32_t win_bins, nwin, win_blocks;
 };
 
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st);

@@ -160,7 +160,12 @@ struct gpuagg_ctx {
   gpuagg_stats stats{};
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
-  uint32_t max_blocks = 2048;
+  uint32_t n_cu = 256;
+  // dense spill lists (per workgroup) for bins beyond the LDS window
+  uint64_t *d_spill = nullptr;
+  size_t spill_alloc = 0;
+  uint32_t *d_spill_count = nullptr;
+  size_t spill_count_alloc = 0;
 };
 
 // ------------------------------------------------------------------------------------
@@ -310,34 +315,75 @@ void drain_timing(gpuagg_ctx *c) {
 }
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
+  int rc = 0;
   if (n == 0) return GPUAGG_OK;
-  if (n > 0xFFFFFFFFull) return fail(c, GPUAGG_ERANGE, "batch of %zu rows exceeds 2^32-1", n);
   if (!c->ip_cap) return fail(c, GPUAGG_ESTATE, "gpuagg_set_endpoints was never called");
   if (c->plan.need_ports && !cv.ports) return fail(c, GPUAGG_EINVAL, "enabled metrics read the ports column");
   if ((c->cms_len) && !cv.ports) return fail(c, GPUAGG_EINVAL, "count-min reads the ports column");
   if (c->plan.need_dns && !cv.dns_id) return fail(c, GPUAGG_EINVAL, "enabled DNS metrics read the dns_id column");
   LaunchArgs a{};
-  a.cols = cv;
-  a.n = n;
   a.ip_slots = c->d_ip;
   a.ip_mask = (uint32_t)(c->ip_cap - 1);
   a.plan = c->plan;
   a.dense_cnt = c->d_dense_cnt;
   a.dense_byt = c->d_dense_byt;
+  a.dense_len = c->dense_len;
   a.sparse = c->sv;
   a.cms = c->d_cms;
   a.cms_depth = c->cms_len ? c->cfg.cms_depth : 0;
   a.cms_wlog2 = c->cfg.cms_width_log2;
   a.hll = c->d_hll;
   a.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
-  a.max_blocks = c->max_blocks;
+  // geometry: one 1024-thread workgroup per CU holding L dense bins in LDS
+  a.lds_bins = (uint32_t)std::min<uint64_t>(c->dense_len, kLdsMaxBins);
+  a.blocks = a.lds_bins ? c->n_cu : c->n_cu * 4;
+  a.threads = a.lds_bins ? 1024 : 256;
+  const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     HIPCHK(c, hipEventCreate(&e0));
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, c->stream));
   }
-  HIPCHK(c, launch_aggregate(a, c->stream));
+  for (uint64_t off = 0; off < n; off += per_launch) {
+    const uint64_t m = std::min<uint64_t>(per_launch, n - off);
+    auto sh = [off](const uint32_t *p) { return p ? p + off : nullptr; };
+    a.cols = ColsView{sh(cv.src_ip), sh(cv.dst_ip), sh(cv.bytes), sh(cv.meta), sh(cv.ports), sh(cv.dns_id)};
+    a.n = m;
+    a.chunk = ((m + a.blocks - 1) / a.blocks + 3) & ~3ULL;
+    auto al = [](const uint32_t *p) { return ((uintptr_t)p & 15u) == 0; };
+    a.vec = al(a.cols.src_ip) && al(a.cols.dst_ip) && al(a.cols.bytes) && al(a.cols.meta) &&
+            (!(c->plan.need_ports || c->cms_len) || al(a.cols.ports)) &&
+            (!c->plan.need_dns || al(a.cols.dns_id));
+    a.spill = nullptr;
+    a.spill_count = nullptr;
+    if (c->dense_len > a.lds_bins) {
+      const uint64_t rem = c->dense_len - a.lds_bins;
+      const uint32_t nwin = (uint32_t)((rem + kLdsMaxBins - 1) / kLdsMaxBins);
+      if (nwin <= kMaxSpillWindows && a.chunk * 2 < 0xFFFFFFFFull) {
+        a.spill_cap = (uint32_t)(2 * a.chunk);
+        const size_t need = (size_t)a.blocks * a.spill_cap;
+        if (need > c->spill_alloc) {
+          dev_free(c->d_spill);
+          c->spill_alloc = 0;
+          if ((rc = dev_alloc(c, &c->d_spill, need))) return rc;
+          c->spill_alloc = need;
+        }
+        if (a.blocks > c->spill_count_alloc) {
+          dev_free(c->d_spill_count);
+          c->spill_count_alloc = 0;
+          if ((rc = dev_alloc(c, &c->d_spill_count, a.blocks))) return rc;
+          c->spill_count_alloc = a.blocks;
+        }
+        a.spill = c->d_spill;
+        a.spill_count = c->d_spill_count;
+        a.nwin = nwin;
+        a.win_bins = (uint32_t)((rem + nwin - 1) / nwin);
+        a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
+      }
+    }
+    HIPCHK(c, launch_aggregate(a, c->stream));
+  }
   if (c->timing) {
     HIPCHK(c, hipEventRecord(e1, c->stream));
     c->pending_events.emplace_back(e0, e1);
@@ -372,7 +418,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GPUAGG_EDEVICE;  // built for gfx950 only
   if (hipSetDevice(c->device) != hipSuccess) return GPUAGG_EDEVICE;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return GPUAGG_EDEVICE;
-  c->max_blocks = (uint32_t)prop.multiProcessorCount * 8u;
+  c->n_cu = (uint32_t)prop.multiProcessorCount;
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
     if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) return GPUAGG_ENOMEM;
@@ -410,6 +456,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_export);
   dev_free(c->d_cms);
   dev_free(c->d_hll);
+  dev_free(c->d_spill);
+  dev_free(c->d_spill_count);
   for (auto &p : c->d_cols) dev_free(p);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -551,14 +599,29 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
         g.key_mode = (so & OPT_EP) ? 1 : 0;
         g.nkeys = g.key_mode ? c->cfg.max_slots : 1;
         g.nsub = (in.family == FAM_DROP || in.family == FAM_TCPFLAGS) ? 8 : 1;
-        g.dense_base = dense_total;
-        dense_total += g.nkeys * 2 * g.nsub;
       }
       groups.push_back(g);
       gi = (int)groups.size() - 1;
     }
     in.group = gi;
   }
+
+  // Dense bin layout, hottest family first: bins [0, L) live in LDS (kernels file), so
+  // forward counters (every forwarded flow) go before TCP-flag, drop and retransmit ones.
+  {
+    static const int prio[FAM_COUNT] = {0, 2, 1, 3, 9, 9};
+    std::vector<size_t> order;
+    for (size_t g = 0; g < groups.size(); ++g)
+      if (!groups[g].sparse) order.push_back(g);
+    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+      return prio[groups[x].family] < prio[groups[y].family];
+    });
+    for (size_t g : order) {
+      groups[g].dense_base = dense_total;
+      dense_total += groups[g].nkeys * 2 * groups[g].nsub;
+    }
+  }
+  if (dense_total >= (1ull << 32)) return fail(c, GPUAGG_ECAPACITY, "dense counter space >= 2^32 bins");
 
   Plan p{};
   p.local = local ? 1 : 0;

@@ -32,7 +32,7 @@ def oracle_series(recs: W.Records, pods: W.Pods, spec: List[dict], remote: bool)
 def make_engine(pods: W.Pods, spec: List[dict], remote: bool, device: int = 0,
                 recs: Optional[W.Records] = None, **kw):
     from retina_amd import GpuAgg
-    kw.setdefault("max_slots", max(16, len(pods.endpoints)))
+    kw.setdefault("max_slots", len(pods.endpoints) + 64)
     kw.setdefault("max_ips", max(16, len(pods.ips)))
     kw.setdefault("sparse_capacity_log2", 20)
     g = GpuAgg(device=device, remote_context=remote, **kw)
