@@ -159,6 +159,10 @@ int gpuagg_submit_device(gpuagg_ctx *ctx, const gpuagg_columns *dev_cols, size_t
 /* Wait for every submitted batch. */
 int gpuagg_sync(gpuagg_ctx *ctx);
 
+/* Zeroes every accumulated counter, table entry and sketch register, keeping the
+ * metric plan, endpoints and dictionaries (used after a multi-GPU epoch merge). */
+int gpuagg_reset(gpuagg_ctx *ctx);
+
 /* ------------------------------------------------------------------------------
  * Output: the Prometheus series the reference's GaugeVec/CounterVec would hold
  * (names under namespace "networkobservability", prometheusexporter.go:11,46-66).

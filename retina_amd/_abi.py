@@ -75,6 +75,7 @@ SIGNATURES = [
     ("gpuagg_submit", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_size_t]),
     ("gpuagg_submit_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t]),
     ("gpuagg_sync", C.c_int, [C.c_void_p]),
+    ("gpuagg_reset", C.c_int, [C.c_void_p]),
     ("gpuagg_snapshot", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     ("gpuagg_result_count", C.c_size_t, [C.c_void_p]),
     ("gpuagg_result_series", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p),

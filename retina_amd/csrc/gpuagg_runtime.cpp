@@ -807,6 +807,14 @@ int gpuagg_sync(gpuagg_ctx *c) {
   return GPUAGG_OK;
 }
 
+int gpuagg_reset(gpuagg_ctx *c) {
+  if (!c) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return reset_state(c);
+}
+
 int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
   if (!c || !out) return GPUAGG_EINVAL;
   *out = nullptr;

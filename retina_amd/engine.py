@@ -231,6 +231,9 @@ class GpuAgg:
     def sync(self) -> None:
         self._check(self.lib.gpuagg_sync(self.h))
 
+    def reset(self) -> None:
+        self._check(self.lib.gpuagg_reset(self.h))
+
     # -- output ------------------------------------------------------------------------
     def snapshot(self) -> Dict[SeriesKey, int]:
         r = C.c_void_p()
