@@ -1,0 +1,69 @@
+"""Ablation timings of the aggregation launch on one MI355X (diagnostics, not the bench).
+
+Runs the same resident 100M-record C2 batch through metric specs of increasing cost and
+prints one JSON line per variant with the HIP-event time per launch:
+  none      no metric groups: record loads + IP probes only
+  fwd       forward_count/bytes (dense, fully in LDS)
+  drop      drop_count/bytes    (dense, LDS window + spill lists + fold)
+  c2        forward + drop      (the bench spec)
+  c2-1kpods C2 spec with 1k pods (every dense bin in LDS, no spill)
+  remote    C1 remote spec (sparse table)
+"""
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import gen_device_records  # noqa: E402
+from retina_amd import GpuAgg  # noqa: E402
+from retina_amd import workloads as W  # noqa: E402
+
+FWD = W.LOCAL_FWD_DROP[:2]
+DROP = W.LOCAL_FWD_DROP[2:]
+
+
+def run(name, spec, pods, cols, n, remote=False, steps=5):
+    g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
+               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24)
+    g.reconcile(spec)
+    g.load_endpoints(pods.endpoints)
+    dc = GpuAgg.device_columns(*cols)
+    g.submit_device(dc, n)
+    g.sync()
+    g.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.submit_device(dc, n)
+    g.sync()
+    wall = (time.perf_counter() - t0) / steps
+    st = g.stats()
+    g.close()
+    ms = st["kernel_ms"] / max(1, st["kernel_launches"])
+    print(json.dumps({"variant": name, "records": n, "launch_ms": ms, "wall_ms": wall * 1e3,
+                      "grec_s": n / ms / 1e6, "hbm_frac_16B": 16 * n / (ms * 1e-3) / 8e12}), flush=True)
+
+
+def main():
+    n = int(os.environ.get("ABLATE_N", 100_000_000))
+    dev = torch.device("cuda", 0)
+    pods = W.make_pods(10_000, seed=2)
+    cols, _ = gen_device_records(n, pods, 2, dev, {})
+    run("none", [], pods, cols, n)
+    run("fwd", FWD, pods, cols, n)
+    run("drop", DROP, pods, cols, n)
+    run("c2", W.LOCAL_FWD_DROP, pods, cols, n)
+    small = W.make_pods(1_000, seed=2)
+    cols_s, _ = gen_device_records(n, small, 3, dev, {})
+    run("c2-1kpods", W.LOCAL_FWD_DROP, small, cols_s, n)
+    del cols_s
+    run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,6 +27,25 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o run \
         -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/${TAG}_prof.log" 2>&1
       rc=$?; echo "prof rc=$rc" >> "$OUT/${TAG}_prof.log"; [ $rc -ne 0 ] && exit $rc ;;
+    ablate)
+      timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
+      rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;
+    pmc)
+      # one counter group per pass (MI355X_MICROARCH.md: rocprofv3 PMC slots)
+      export TMPDIR=/tmp
+      rocprofv3 -L > "$OUT/${TAG}_counters.txt" 2>&1
+      i=0
+      for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_FLAT GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        i=$((i+1))
+        timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d "$OUT/${TAG}_pmc$i" -o run \
+          -- python3 "$R/bench.py" --records 20000000 --steps 2 --warmup 1 --no-cpu-baseline \
+          > "$OUT/${TAG}_pmc$i.log" 2>&1
+        rc=$?; echo "pmc$i rc=$rc" >> "$OUT/${TAG}_pmc$i.log"
+        [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+      done ;;
   esac
 done
 exit 0
