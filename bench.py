@@ -153,6 +153,7 @@ def main():
     elapsed = float(t.item())
 
     kernel_ms = stats["kernel_ms"] / max(1, stats["kernel_launches"])
+    fold_ms = stats["fold_ms"] / max(1, stats["kernel_launches"])
     achieved = BYTES_PER_RECORD * n / (kernel_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
@@ -193,6 +194,7 @@ def main():
             "traffic": traffic,
             "kernel": "aggregate_kernel",
             "kernel_ms": kernel_ms,
+            "other_kernels_ms": fold_ms,
             "bytes_per_record": BYTES_PER_RECORD,
         },
     }

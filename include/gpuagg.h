@@ -220,7 +220,8 @@ typedef struct gpuagg_stats {
   uint64_t sparse_entries;   /* occupied group-by table entries (at last sync)   */
   uint64_t sparse_dropped;   /* updates lost to a full group-by table            */
   uint64_t kernel_launches;  /* timed aggregation launches                       */
-  double kernel_ms;          /* summed device time of timed launches (HIP events) */
+  double kernel_ms;          /* summed device time of aggregate_kernel (HIP events)  */
+  double fold_ms;            /* summed device time of the spill fold kernel          */
 } gpuagg_stats;
 
 int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);

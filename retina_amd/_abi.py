@@ -56,7 +56,7 @@ class StateDesc(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("batches", C.c_uint64), ("sparse_entries", C.c_uint64),
                 ("sparse_dropped", C.c_uint64), ("kernel_launches", C.c_uint64),
-                ("kernel_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("fold_ms", C.c_double)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/gpuagg.h

@@ -113,6 +113,10 @@ GA_HD uint32_t ip_hash(uint32_t ip) {  // murmur3 fmix32: 2 mul + 3 xorshift
   ip ^= ip >> 16;
   return ip;
 }
+// Cuckoo IP table (2 choices, one 8-byte entry each): a lookup is exactly two
+// independent loads, no probe loop.  seed = (seed1, seed2) chosen by the host builder.
+GA_HD uint32_t ip_h1(uint32_t ip, uint32_t seed) { return ip_hash(ip ^ seed); }
+GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) { return ip_hash((ip ^ seed) * 0x9E3779B1u + 0x7F4A7C15u); }
 // Dense bins kept in LDS per workgroup: u64 = count << 40 | bytes (bytes < 2^16 per
 // update, <= 2^24 records per workgroup between flushes => both fields exact).
 constexpr uint32_t kLdsBytes = 160 * 1024;

@@ -27,6 +27,7 @@ namespace gpuagg {
 struct DevIpTable {
   const uint64_t *slots;
   uint32_t mask;
+  uint32_t seed;
 };
 struct DevDense {
   unsigned long long *cnt;
@@ -73,18 +74,18 @@ __device__ __forceinline__ Lk lk_from(uint64_t e) {
   return Lk{(int32_t)((e >> 32) & ((1u << kSlotBits) - 1)), (uint32_t)(e >> 53) & 1u};
 }
 
-// Resolves a probe chain whose first entry was already loaded.
-__device__ __forceinline__ Lk ip_resolve(const DevIpTable &t, uint32_t ip, uint32_t h, uint64_t e) {
-  while (e != kIpEmpty && (uint32_t)e != ip) {
-    h = (h + 1) & t.mask;
-    e = t.slots[h];
-  }
+// Cuckoo lookup: both candidate entries are loaded unconditionally (independent
+// loads, no probe loop); an EMPTY entry never matches a real key because the host
+// refuses 255.255.255.255 as a pod IP.
+__device__ __forceinline__ Lk ip_pick(uint32_t ip, uint64_t e1, uint64_t e2) {
+  const uint64_t e = ((uint32_t)e1 == ip) ? e1 : (((uint32_t)e2 == ip) ? e2 : kIpEmpty);
   return lk_from(e);
 }
 
 __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
-  const uint32_t h = ip_hash(ip) & t.mask;
-  return ip_resolve(t, ip, h, t.slots[h]);
+  const uint64_t e1 = t.slots[ip_h1(ip, t.seed) & t.mask];
+  const uint64_t e2 = t.slots[ip_h2(ip, t.seed) & t.mask];
+  return ip_pick(ip, e1, e2);
 }
 
 // Insert-or-add into the sparse table. No lane ever waits for another: a lane that
@@ -128,16 +129,23 @@ struct DenseSink {
   uint32_t spill_cap;
   DevDense d;
 
-  __device__ __forceinline__ void add(uint64_t bin, uint32_t nbytes) const {
+  __device__ __forceinline__ void add(uint32_t bin, uint32_t nbytes) const {
     if (bin < L) {
       if (nbytes < kLdsByteLimit) {
         atomicAdd(&lds[bin], kLdsCountOne | nbytes);
         return;
       }
     } else if (spill) {
-      const unsigned int pos = atomicAdd(spill_ctr, 1u);
+      // one LDS atomic per wave: the active lanes here are exactly the spilling ones
+      const unsigned long long act = __ballot(1);
+      const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+      unsigned int base = 0;
+      if (lane == leader) base = atomicAdd(spill_ctr, (unsigned int)__builtin_popcountll(act));
+      base = __shfl(base, (int)leader);
+      const unsigned int pos = base + (unsigned int)__builtin_popcountll(act & ((1ULL << lane) - 1ULL));
       if (pos < spill_cap) {
-        spill[pos] = (bin << 32) | nbytes;
+        spill[pos] = ((unsigned long long)bin << 32) | nbytes;
         return;
       }
     }
@@ -214,8 +222,8 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
         if (!ok) continue;
         const Lk &lk = side == 0 ? ld : ls;
         if (!gp.sparse) {
-          const uint64_t key = gp.key_mode ? (uint64_t)lk.slot : 0u;
-          const uint64_t row = gp.dense_base + (key * 2 + (uint64_t)side) * gp.nsub;
+          const uint32_t key = gp.key_mode ? (uint32_t)lk.slot : 0u;
+          const uint32_t row = (uint32_t)gp.dense_base + (key * 2u + (uint32_t)side) * gp.nsub;
           if (fam == FAM_TCPFLAGS) {
             for (uint32_t m = flagmask; m; m &= m - 1) ds.add(row + __builtin_ctz(m), 0);
           } else {
@@ -282,30 +290,15 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
   }
 }
 
-template <bool kSketch>
-__device__ __forceinline__ void one_record(const KArgs &a, const DenseSink &ds, uint32_t sip,
-                                           uint32_t dip, uint32_t nb, uint32_t meta,
-                                           uint32_t ports, uint32_t dns, const Lk &ls,
-                                           const Lk &ld) {
-  apply_groups(a.p, ds, a.s, sip, dip, nb, meta, ports, dns, ls, ld);
-  if (kSketch) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
-}
-
-// One workgroup per CU when LDS bins are in use. Workgroup b aggregates the
-// contiguous record range [b*chunk, (b+1)*chunk).
-template <bool kVec, bool kSketch>
-__global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
-  const uint32_t L = a.lds_bins;
-  for (uint32_t i = threadIdx.x; i <= L; i += blockDim.x) lds[i] = 0ULL;
-  __syncthreads();
-  DenseSink ds{lds, L, (unsigned int *)&lds[L],
-               a.spill ? a.spill + (size_t)blockIdx.x * a.spill_cap : nullptr, a.spill_cap, a.d};
-
+// ---- record streaming -------------------------------------------------------------
+// Workgroup b owns records [b*chunk, (b+1)*chunk). With kVec every lane takes 4
+// consecutive records per step (16-byte loads per column), issues the 16 IP-table
+// loads of their 8 addresses back to back, then walks the 4 records in a rolled loop
+// (register rotation keeps one copy of the per-record code).
+template <bool kVec, class F>
+__device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f) {
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
-  const bool need_ports = a.p.need_ports || kSketch;
-  const bool need_dns = a.p.need_dns;
   uint64_t tail = start;
   if (kVec && start < end) {
     const uint64_t vend = start + ((end - start) & ~3ULL);
@@ -318,33 +311,50 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
-      uint32_t h[8];
-      uint64_t e[8];
+      uint64_t e1[8], e2[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) h[k] = ip_hash(ip[k]) & a.t.mask;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) e[k] = a.t.slots[h[k]];  // 8 independent probes in flight
-      Lk lk[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) lk[k] = ip_resolve(a.t, ip[k], h[k], e[k]);
-      one_record<kSketch>(a, ds, vs.x, vd.x, vb.x, vm.x, vp.x, vq.x, lk[0], lk[4]);
-      one_record<kSketch>(a, ds, vs.y, vd.y, vb.y, vm.y, vp.y, vq.y, lk[1], lk[5]);
-      one_record<kSketch>(a, ds, vs.z, vd.z, vb.z, vm.z, vp.z, vq.z, lk[2], lk[6]);
-      one_record<kSketch>(a, ds, vs.w, vd.w, vb.w, vm.w, vp.w, vq.w, lk[3], lk[7]);
+      for (int k = 0; k < 8; ++k) {
+        e1[k] = a.t.slots[ip_h1(ip[k], a.t.seed) & a.t.mask];
+        e2[k] = a.t.slots[ip_h2(ip[k], a.t.seed) & a.t.mask];
+      }
+      Lk ls0 = ip_pick(ip[0], e1[0], e2[0]), ls1 = ip_pick(ip[1], e1[1], e2[1]);
+      Lk ls2 = ip_pick(ip[2], e1[2], e2[2]), ls3 = ip_pick(ip[3], e1[3], e2[3]);
+      Lk ld0 = ip_pick(ip[4], e1[4], e2[4]), ld1 = ip_pick(ip[5], e1[5], e2[5]);
+      Lk ld2 = ip_pick(ip[6], e1[6], e2[6]), ld3 = ip_pick(ip[7], e1[7], e2[7]);
+      uint32_t s0 = vs.x, s1 = vs.y, s2 = vs.z, s3 = vs.w, d0 = vd.x, d1 = vd.y, d2 = vd.z, d3 = vd.w;
+      uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
+      uint32_t p0 = vp.x, p1 = vp.y, p2 = vp.z, p3 = vp.w, q0 = vq.x, q1 = vq.y, q2 = vq.z, q3 = vq.w;
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        f(s0, d0, b0, m0, p0, q0, ls0, ld0);
+        s0 = s1; s1 = s2; s2 = s3; d0 = d1; d1 = d2; d2 = d3;
+        b0 = b1; b1 = b2; b2 = b3; m0 = m1; m1 = m2; m2 = m3;
+        p0 = p1; p1 = p2; p2 = p3; q0 = q1; q1 = q2; q2 = q3;
+        ls0 = ls1; ls1 = ls2; ls2 = ls3; ld0 = ld1; ld1 = ld2; ld2 = ld3;
+      }
     }
     tail = vend;
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
     const uint32_t sip = a.c.src[i], dip = a.c.dst[i];
-    const Lk ls = ip_lookup(a.t, sip), ld = ip_lookup(a.t, dip);
-    one_record<kSketch>(a, ds, sip, dip, a.c.bytes[i], a.c.meta[i], need_ports ? a.c.ports[i] : 0u,
-                        need_dns ? a.c.dns[i] : 0u, ls, ld);
+    f(sip, dip, a.c.bytes[i], a.c.meta[i], need_ports ? a.c.ports[i] : 0u, need_dns ? a.c.dns[i] : 0u,
+      ip_lookup(a.t, sip), ip_lookup(a.t, dip));
   }
+}
 
+// LDS setup and the once-per-workgroup flush shared by both aggregation kernels.
+__device__ __forceinline__ DenseSink dense_sink_init(const KArgs &a, unsigned long long *lds) {
+  for (uint32_t i = threadIdx.x; i <= a.lds_bins; i += blockDim.x) lds[i] = 0ULL;
   __syncthreads();
-  // flush: consecutive lanes -> consecutive bins (256-B contiguous atomic wave-instructions)
-  for (uint32_t i = threadIdx.x; i < L; i += blockDim.x) {
-    const unsigned long long v = lds[i];
+  return DenseSink{lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins],
+                   a.spill ? a.spill + (size_t)blockIdx.x * a.spill_cap : nullptr, a.spill_cap, a.d};
+}
+
+__device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds) {
+  __syncthreads();
+  // consecutive lanes -> consecutive bins: each wave-instruction adds 512 contiguous bytes
+  for (uint32_t i = threadIdx.x; i < a.lds_bins; i += blockDim.x) {
+    const unsigned long long v = ds.lds[i];
     if (v) {
       atomicAdd(&a.d.cnt[i], v >> 40);
       const unsigned long long by = v & kLdsBytesMask;
@@ -355,6 +365,78 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
     const unsigned int c = *ds.spill_ctr;
     a.spill_count[blockIdx.x] = c < a.spill_cap ? c : a.spill_cap;
   }
+}
+
+// Generic aggregation: any plan (dense, sparse, DNS, remote context, sketches).
+template <bool kVec, bool kSketch>
+__global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  const DenseSink ds = dense_sink_init(a, lds);
+  for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
+                        [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports,
+                            uint32_t dns, const Lk &ls, const Lk &ld) {
+                          apply_groups(a.p, ds, a.s, sip, dip, nb, meta, ports, dns, ls, ld);
+                          if (kSketch) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
+                        });
+  dense_flush(a, ds);
+}
+
+// Dense local-context fast path: every group is endpoint-keyed (forward / drop /
+// tcpflags / tcpretrans with namespace|podname|workload|service options).  The NG
+// group descriptors are compile-time indexed, so they live in SGPRs for the whole
+// kernel; bin arithmetic is 32-bit.
+template <int NG, bool kVec>
+__global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  const DenseSink ds = dense_sink_init(a, lds);
+  const int ng = a.p.ngroups;
+  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  bool any_flags = false;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    fam[g] = g < ng ? a.p.g[g].family : (uint32_t)FAM_COUNT;
+    base[g] = (uint32_t)a.p.g[g].dense_base;
+    nsub[g] = a.p.g[g].nsub;
+    keyed[g] = a.p.g[g].key_mode;
+    any_flags |= fam[g] == FAM_TCPFLAGS;
+  }
+  for_each_record<kVec>(a, false, false,
+                        [&](uint32_t, uint32_t, uint32_t nb, uint32_t meta, uint32_t, uint32_t,
+                            const Lk &ls, const Lk &ld) {
+    const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
+    const bool s_ok = ls.slot >= 0 && !ls.api;  // getLocalCtxValues (types.go:379-416)
+    const bool d_ok = ld.slot >= 0 && !ld.api;
+    if (!s_ok && !d_ok) return;
+    const uint32_t flagmask = (any_flags && verdict == kVerdictForwarded && proto == 6)
+                                  ? flag_label_mask(meta_flags(meta)) : 0u;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const uint32_t f = fam[g];
+      bool hit;
+      if (f == FAM_FWD) hit = verdict == kVerdictForwarded;
+      else if (f == FAM_DROP) hit = verdict == kVerdictDropped;
+      else if (f == FAM_RETRANS) hit = verdict == kVerdictRetrans;
+      else if (f == FAM_TCPFLAGS) hit = flagmask != 0;
+      else hit = false;
+      if (!hit) continue;
+      const uint32_t kd = keyed[g] ? (uint32_t)ld.slot : 0u, ks = keyed[g] ? (uint32_t)ls.slot : 0u;
+      const uint32_t row_d = base[g] + (kd * 2u) * nsub[g];        // side 0: ingress (dst)
+      const uint32_t row_s = base[g] + (ks * 2u + 1u) * nsub[g];   // side 1: egress (src)
+      if (f == FAM_TCPFLAGS) {
+        for (uint32_t m = flagmask; m; m &= m - 1) {
+          const uint32_t bit = (uint32_t)__builtin_ctz(m);
+          if (d_ok) ds.add(row_d + bit, 0);
+          if (s_ok) ds.add(row_s + bit, 0);
+        }
+      } else {
+        const uint32_t sub = f == FAM_DROP ? reason : 0u;
+        const uint32_t add_b = f <= FAM_DROP ? nb : 0u;
+        if (d_ok) ds.add(row_d + sub, add_b);
+        if (s_ok) ds.add(row_s + sub, add_b);
+      }
+    }
+  });
+  dense_flush(a, ds);
 }
 
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.
@@ -439,23 +521,23 @@ static DevSparse dev_sparse(const SparseView &v) {
                    (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped};
 }
 
-template <bool V, bool S>
-static hipError_t launch_agg(const KArgs &k, uint32_t blocks, uint32_t threads, size_t lds,
-                             hipStream_t st) {
-  hipError_t e = hipFuncSetAttribute((const void *)aggregate_kernel<V, S>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+template <class K>
+static hipError_t launch_k(K kern, const KArgs &k, uint32_t blocks, uint32_t threads, size_t lds,
+                           hipStream_t st) {
+  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((aggregate_kernel<V, S>), dim3(blocks), dim3(threads), lds, st, k);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), lds, st, k);
   return hipGetLastError();
 }
 
-hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st) {
+hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between) {
   if (a.n == 0) return hipSuccess;
   KArgs k{};
   k.c = DevCols{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
   k.n = a.n;
   k.chunk = a.chunk;
-  k.t = DevIpTable{a.ip_slots, a.ip_mask};
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed};
   k.d = DevDense{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
   k.s = dev_sparse(a.sparse);
   k.sk = DevSketch{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};
@@ -466,14 +548,28 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st) {
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   const size_t lds = ((size_t)a.lds_bins + 1) * 8;
+  const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
-  if (a.vec)
-    e = sketch ? launch_agg<true, true>(k, a.blocks, a.threads, lds, st)
-               : launch_agg<true, false>(k, a.blocks, a.threads, lds, st);
-  else
-    e = sketch ? launch_agg<false, true>(k, a.blocks, a.threads, lds, st)
-               : launch_agg<false, false>(k, a.blocks, a.threads, lds, st);
-  if (e != hipSuccess || !a.spill) return e;
+  switch (a.dense_ng) {  // dense local-context fast path, groups rounded up to 1/2/4/8
+    case 1: e = a.vec ? launch_k(dense_local_kernel<1, true>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<1, false>, k, B, T, lds, st); break;
+    case 2: e = a.vec ? launch_k(dense_local_kernel<2, true>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<2, false>, k, B, T, lds, st); break;
+    case 4: e = a.vec ? launch_k(dense_local_kernel<4, true>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<4, false>, k, B, T, lds, st); break;
+    case 8: e = a.vec ? launch_k(dense_local_kernel<8, true>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<8, false>, k, B, T, lds, st); break;
+    default:
+      if (a.vec)
+        e = sketch ? launch_k(aggregate_kernel<true, true>, k, B, T, lds, st)
+                   : launch_k(aggregate_kernel<true, false>, k, B, T, lds, st);
+      else
+        e = sketch ? launch_k(aggregate_kernel<false, true>, k, B, T, lds, st)
+                   : launch_k(aggregate_kernel<false, false>, k, B, T, lds, st);
+  }
+  if (e != hipSuccess) return e;
+  if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
+  if (!a.spill) return hipSuccess;
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;

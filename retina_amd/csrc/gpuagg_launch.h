@@ -23,6 +23,7 @@ struct LaunchArgs {
   size_t n;
   const uint64_t *ip_slots;
   uint32_t ip_mask;
+  uint32_t ip_seed;
   Plan plan;
   uint64_t *dense_cnt, *dense_byt;
   SparseView sparse;
@@ -40,9 +41,11 @@ struct LaunchArgs {
   uint32_t spill_cap;
   uint32_t *spill_count;
   uint32_t win_bins, nwin, win_blocks;
+  uint32_t dense_ng;    // 0: generic kernel; 1/2/4/8: dense local-context kernel
 };
 
-hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st);
+// `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
+hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between);
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);
 hipError_t launch_sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t out_cap,
                                 uint64_t *counter, hipStream_t st);

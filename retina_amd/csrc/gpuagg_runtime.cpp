@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -130,6 +131,7 @@ struct gpuagg_ctx {
   // IP table
   uint64_t *d_ip = nullptr;
   size_t ip_cap = 0;  // slots
+  uint32_t ip_seed = 0;
   uint64_t ip_version = 0;
 
   // dense counters
@@ -159,7 +161,7 @@ struct gpuagg_ctx {
   // stats / timing
   gpuagg_stats stats{};
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+  std::vector<std::array<hipEvent_t, 3>> pending_events;  // start, after aggregate, after fold
   uint32_t n_cu = 256;
   // dense spill lists (per workgroup) for bins beyond the LDS window
   uint64_t *d_spill = nullptr;
@@ -303,13 +305,14 @@ int ensure_sparse(gpuagg_ctx *c) {
 
 void drain_timing(gpuagg_ctx *c) {
   for (auto &ev : c->pending_events) {
-    float ms = 0.f;
-    if (hipEventSynchronize(ev.second) == hipSuccess && hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) {
+    float ms = 0.f, fold = 0.f;
+    if (hipEventSynchronize(ev[2]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess &&
+        hipEventElapsedTime(&fold, ev[1], ev[2]) == hipSuccess) {
       c->stats.kernel_ms += ms;
+      c->stats.fold_ms += fold;
       c->stats.kernel_launches += 1;
     }
-    hipEventDestroy(ev.first);
-    hipEventDestroy(ev.second);
+    for (hipEvent_t e : ev) hipEventDestroy(e);
   }
   c->pending_events.clear();
 }
@@ -324,6 +327,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   LaunchArgs a{};
   a.ip_slots = c->d_ip;
   a.ip_mask = (uint32_t)(c->ip_cap - 1);
+  a.ip_seed = c->ip_seed;
   a.plan = c->plan;
   a.dense_cnt = c->d_dense_cnt;
   a.dense_byt = c->d_dense_byt;
@@ -334,17 +338,23 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.cms_wlog2 = c->cfg.cms_width_log2;
   a.hll = c->d_hll;
   a.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
+  // dense local-context fast path: every group dense, no sketches
+  a.dense_ng = 0;
+  if (c->plan.local && c->plan.ngroups > 0 && !a.cms_depth && !a.hll_p) {
+    bool all_dense = true;
+    for (int g = 0; g < c->plan.ngroups; ++g) all_dense &= !c->plan.g[g].sparse;
+    if (all_dense)
+      for (uint32_t ng : {1u, 2u, 4u, 8u})
+        if ((uint32_t)c->plan.ngroups <= ng) {
+          a.dense_ng = ng;
+          break;
+        }
+  }
   // geometry: one 1024-thread workgroup per CU holding L dense bins in LDS
   a.lds_bins = (uint32_t)std::min<uint64_t>(c->dense_len, kLdsMaxBins);
   a.blocks = a.lds_bins ? c->n_cu : c->n_cu * 4;
   a.threads = a.lds_bins ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->timing) {
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
-    HIPCHK(c, hipEventRecord(e0, c->stream));
-  }
   for (uint64_t off = 0; off < n; off += per_launch) {
     const uint64_t m = std::min<uint64_t>(per_launch, n - off);
     auto sh = [off](const uint32_t *p) { return p ? p + off : nullptr; };
@@ -382,11 +392,16 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
       }
     }
-    HIPCHK(c, launch_aggregate(a, c->stream));
-  }
-  if (c->timing) {
-    HIPCHK(c, hipEventRecord(e1, c->stream));
-    c->pending_events.emplace_back(e0, e1);
+    std::array<hipEvent_t, 3> ev{};
+    if (c->timing) {
+      for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
+      HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    }
+    HIPCHK(c, launch_aggregate(a, c->stream, c->timing ? ev[1] : nullptr));
+    if (c->timing) {
+      HIPCHK(c, hipEventRecord(ev[2], c->stream));
+      c->pending_events.push_back(ev);
+    }
   }
   c->stats.records += n;
   c->stats.batches += 1;
@@ -692,25 +707,44 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   int rc = bind(c);
   if (rc) return rc;
   if (n > c->cfg.max_ips) return fail(c, GPUAGG_ECAPACITY, "%zu IPs exceed max_ips=%u", n, c->cfg.max_ips);
-  size_t cap = 16;
-  while (cap < 2 * n) cap <<= 1;
-  std::vector<uint64_t> tab(cap, kIpEmpty);
+  // last writer wins for an IP held twice (cache.go:204-233)
+  std::unordered_map<uint32_t, uint64_t> last;
+  last.reserve(n * 2 + 1);
   for (size_t i = 0; i < n; ++i) {
     if (slot[i] < 0 || (size_t)slot[i] >= c->slots.size())
       return fail(c, GPUAGG_EINVAL, "entry %zu: slot %d was not interned", i, slot[i]);
     if (ipv4[i] == 0xFFFFFFFFu) return fail(c, GPUAGG_ERANGE, "255.255.255.255 cannot be a pod IP");
-    uint32_t h = ip_hash(ipv4[i]) & (uint32_t)(cap - 1);
-    for (;;) {
-      if (tab[h] == kIpEmpty) {
-        tab[h] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
-        break;
+    last[ipv4[i]] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
+  }
+  // cuckoo build: load <= ~45%, re-seed on a failed insertion, grow after 8 seeds
+  size_t cap = 64;
+  while (cap * 45 < last.size() * 100) cap <<= 1;
+  std::vector<uint64_t> tab;
+  uint32_t seed = 0x2545F491u;
+  for (int attempt = 0;; ++attempt) {
+    if (attempt && attempt % 8 == 0) cap <<= 1;
+    seed = (uint32_t)fmix64((uint64_t)seed + 0x9E3779B97F4A7C15ULL * (attempt + 1));
+    tab.assign(cap, kIpEmpty);
+    const uint32_t mask = (uint32_t)(cap - 1);
+    bool ok = true;
+    for (const auto &kv : last) {
+      uint64_t cur = kv.second;
+      uint32_t h = ip_h1((uint32_t)cur, seed) & mask;
+      int kicks = 0;
+      for (;;) {
+        std::swap(cur, tab[h]);
+        if (cur == kIpEmpty) break;
+        if (++kicks > 500) {
+          ok = false;
+          break;
+        }
+        const uint32_t h1 = ip_h1((uint32_t)cur, seed) & mask, h2 = ip_h2((uint32_t)cur, seed) & mask;
+        h = (h == h1) ? h2 : h1;  // move the evicted key to its other choice
       }
-      if ((uint32_t)tab[h] == ipv4[i]) {  // duplicate IP: last writer wins (cache.go:227-230)
-        tab[h] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
-        break;
-      }
-      h = (h + 1) & (uint32_t)(cap - 1);
+      if (!ok) break;
     }
+    if (ok) break;
+    if (cap > ((size_t)1 << 30)) return fail(c, GPUAGG_ECAPACITY, "IP table cannot be built");
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches use the old table
   if (cap != c->ip_cap) {
@@ -720,6 +754,7 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   }
   HIPCHK(c, hipMemcpy(c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
   c->ip_cap = cap;
+  c->ip_seed = seed;
   c->ip_version = version;
   return GPUAGG_OK;
 }
@@ -1066,6 +1101,7 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   c->timing = enabled != 0;
   if (!enabled) {
     c->stats.kernel_ms = 0;
+    c->stats.fold_ms = 0;
     c->stats.kernel_launches = 0;
   }
   return GPUAGG_OK;

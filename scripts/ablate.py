@@ -45,7 +45,8 @@ def run(name, spec, pods, cols, n, remote=False, steps=5):
     st = g.stats()
     g.close()
     ms = st["kernel_ms"] / max(1, st["kernel_launches"])
-    print(json.dumps({"variant": name, "records": n, "launch_ms": ms, "wall_ms": wall * 1e3,
+    fold = st["fold_ms"] / max(1, st["kernel_launches"])
+    print(json.dumps({"variant": name, "records": n, "launch_ms": ms, "fold_ms": fold, "wall_ms": wall * 1e3,
                       "grec_s": n / ms / 1e6, "hbm_frac_16B": 16 * n / (ms * 1e-3) / 8e12}), flush=True)
 
 
