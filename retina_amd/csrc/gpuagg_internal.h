@@ -80,7 +80,7 @@ struct GroupPlan {
   uint32_t nsub;     // dense: sub-bins per (key, side): 1 or 8
   uint64_t dense_base;
   uint32_t key_mode;  // dense: 0 constant key, 1 slot key
-  uint32_t pad;
+  uint32_t nbins;     // dense: bins of this group (nkeys * 2 * nsub)
 };
 
 struct Plan {
@@ -115,16 +115,32 @@ GA_HD uint32_t ip_hash(uint32_t ip) {  // murmur3 fmix32: 2 mul + 3 xorshift
 }
 // Cuckoo IP table (2 choices, one 8-byte entry each): a lookup is exactly two
 // independent loads, no probe loop.  seed = (seed1, seed2) chosen by the host builder.
-GA_HD uint32_t ip_h1(uint32_t ip, uint32_t seed) { return ip_hash(ip ^ seed); }
-GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) { return ip_hash((ip ^ seed) * 0x9E3779B1u + 0x7F4A7C15u); }
-// Dense bins kept in LDS per workgroup: u64 = count << 40 | bytes (bytes < 2^16 per
-// update, <= 2^24 records per workgroup between flushes => both fields exact).
+// One multiply per choice (32-bit multiplies are quarter rate on CDNA).
+GA_HD uint32_t ip_pre(uint32_t ip, uint32_t seed) {
+  const uint32_t x = ip ^ seed;
+  return x ^ (x >> 16);
+}
+GA_HD uint32_t ip_h1(uint32_t ip, uint32_t seed) {
+  const uint32_t h = ip_pre(ip, seed) * 0x9E3779B1u;
+  return h ^ (h >> 15);
+}
+GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) {
+  const uint32_t h = ip_pre(ip, seed) * 0x85EBCA77u;
+  return h ^ (h >> 13);
+}
+// Dense bins kept in LDS per workgroup: u64 = count << 44 | bytes.  A workgroup
+// aggregates <= 2^20 records between flushes and an update carries < 2^24 bytes in
+// LDS (bigger packets add their bytes with a global atomic), so both fields are exact.
+// LDS layout: bins [0, L), 64 per-lane dummy words [L, L+64) that absorb predicated-
+// off updates, the spill counter at L+64.
 constexpr uint32_t kLdsBytes = 160 * 1024;
-constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - 2;  // + one word for the spill counter
-constexpr uint32_t kLdsByteLimit = 1u << 16;
-constexpr uint64_t kLdsCountOne = 1ULL << 40;
+constexpr uint32_t kLdsExtraWords = 65;
+constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
+constexpr uint32_t kLdsCountShift = 44;
+constexpr uint32_t kLdsByteLimit = 1u << 24;
+constexpr uint64_t kLdsCountOne = 1ULL << kLdsCountShift;
 constexpr uint64_t kLdsBytesMask = kLdsCountOne - 1;
-constexpr uint64_t kMaxRecordsPerBlock = 1ULL << 24;
+constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^20, multiple of 4
 constexpr uint32_t kMaxSpillWindows = 16;
 GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);

@@ -129,14 +129,10 @@ struct DenseSink {
   uint32_t spill_cap;
   DevDense d;
 
-  __device__ __forceinline__ void add(uint32_t bin, uint32_t nbytes) const {
-    if (bin < L) {
-      if (nbytes < kLdsByteLimit) {
-        atomicAdd(&lds[bin], kLdsCountOne | nbytes);
-        return;
-      }
-    } else if (spill) {
-      // one LDS atomic per wave: the active lanes here are exactly the spilling ones
+  // Appends (bin, bytes) to this workgroup's spill list: one LDS atomic per wave
+  // (the active lanes here are exactly the spilling ones); global atomics if full.
+  __device__ __forceinline__ void spill_add(uint32_t bin, uint32_t nbytes) const {
+    if (spill) {
       const unsigned long long act = __ballot(1);
       const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
       const uint32_t leader = (uint32_t)__builtin_ctzll(act);
@@ -151,6 +147,15 @@ struct DenseSink {
     }
     atomicAdd(&d.cnt[bin], 1ULL);
     if (nbytes) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
+  }
+
+  __device__ __forceinline__ void add(uint32_t bin, uint32_t nbytes) const {
+    if (bin < L) {
+      atomicAdd(&lds[bin], kLdsCountOne | (nbytes < kLdsByteLimit ? nbytes : 0u));
+      if (nbytes >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
+      return;
+    }
+    spill_add(bin, nbytes);
   }
 };
 
@@ -344,9 +349,9 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
 
 // LDS setup and the once-per-workgroup flush shared by both aggregation kernels.
 __device__ __forceinline__ DenseSink dense_sink_init(const KArgs &a, unsigned long long *lds) {
-  for (uint32_t i = threadIdx.x; i <= a.lds_bins; i += blockDim.x) lds[i] = 0ULL;
+  for (uint32_t i = threadIdx.x; i < a.lds_bins + kLdsExtraWords; i += blockDim.x) lds[i] = 0ULL;
   __syncthreads();
-  return DenseSink{lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins],
+  return DenseSink{lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins + 64],
                    a.spill ? a.spill + (size_t)blockIdx.x * a.spill_cap : nullptr, a.spill_cap, a.d};
 }
 
@@ -356,7 +361,7 @@ __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds)
   for (uint32_t i = threadIdx.x; i < a.lds_bins; i += blockDim.x) {
     const unsigned long long v = ds.lds[i];
     if (v) {
-      atomicAdd(&a.d.cnt[i], v >> 40);
+      atomicAdd(&a.d.cnt[i], v >> kLdsCountShift);
       const unsigned long long by = v & kLdsBytesMask;
       if (by) atomicAdd(&a.d.byt[i], by);
     }
@@ -389,8 +394,11 @@ template <int NG, bool kVec>
 __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
   const DenseSink ds = dense_sink_init(a, lds);
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t dummy = a.lds_bins + lane;  // absorbs predicated-off updates, never flushed
   const int ng = a.p.ngroups;
   uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  bool inl[NG];
   bool any_flags = false;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
@@ -398,6 +406,7 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
     base[g] = (uint32_t)a.p.g[g].dense_base;
     nsub[g] = a.p.g[g].nsub;
     keyed[g] = a.p.g[g].key_mode;
+    inl[g] = base[g] + a.p.g[g].nbins <= a.lds_bins;  // whole group in the LDS window
     any_flags |= fam[g] == FAM_TCPFLAGS;
   }
   for_each_record<kVec>(a, false, false,
@@ -406,33 +415,52 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
     const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
     const bool s_ok = ls.slot >= 0 && !ls.api;  // getLocalCtxValues (types.go:379-416)
     const bool d_ok = ld.slot >= 0 && !ld.api;
-    if (!s_ok && !d_ok) return;
+    const bool big = nb >= kLdsByteLimit;       // bytes of such packets go to global atomics
     const uint32_t flagmask = (any_flags && verdict == kVerdictForwarded && proto == 6)
                                   ? flag_label_mask(meta_flags(meta)) : 0u;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const uint32_t f = fam[g];
-      bool hit;
-      if (f == FAM_FWD) hit = verdict == kVerdictForwarded;
-      else if (f == FAM_DROP) hit = verdict == kVerdictDropped;
-      else if (f == FAM_RETRANS) hit = verdict == kVerdictRetrans;
-      else if (f == FAM_TCPFLAGS) hit = flagmask != 0;
-      else hit = false;
-      if (!hit) continue;
+      if (f == FAM_COUNT) continue;
       const uint32_t kd = keyed[g] ? (uint32_t)ld.slot : 0u, ks = keyed[g] ? (uint32_t)ls.slot : 0u;
       const uint32_t row_d = base[g] + (kd * 2u) * nsub[g];        // side 0: ingress (dst)
       const uint32_t row_s = base[g] + (ks * 2u + 1u) * nsub[g];   // side 1: egress (src)
       if (f == FAM_TCPFLAGS) {
-        for (uint32_t m = flagmask; m; m &= m - 1) {
-          const uint32_t bit = (uint32_t)__builtin_ctz(m);
-          if (d_ok) ds.add(row_d + bit, 0);
-          if (s_ok) ds.add(row_s + bit, 0);
+        uint32_t m = flagmask;
+        if (inl[g]) {
+          while (__ballot(m != 0)) {  // trips = most flags any lane of the wave has
+            const bool v = m != 0;
+            const uint32_t bit = v ? (uint32_t)__builtin_ctz(m) : 0u;
+            atomicAdd(&lds[v && d_ok ? row_d + bit : dummy], kLdsCountOne);
+            atomicAdd(&lds[v && s_ok ? row_s + bit : dummy], kLdsCountOne);
+            m &= m - 1;
+          }
+        } else {
+          for (; m; m &= m - 1) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            if (d_ok) ds.spill_add(row_d + bit, 0);
+            if (s_ok) ds.spill_add(row_s + bit, 0);
+          }
         }
-      } else {
-        const uint32_t sub = f == FAM_DROP ? reason : 0u;
-        const uint32_t add_b = f <= FAM_DROP ? nb : 0u;
-        if (d_ok) ds.add(row_d + sub, add_b);
-        if (s_ok) ds.add(row_s + sub, add_b);
+        continue;
+      }
+      bool hit;
+      if (f == FAM_FWD) hit = verdict == kVerdictForwarded;
+      else if (f == FAM_DROP) hit = verdict == kVerdictDropped;
+      else hit = verdict == kVerdictRetrans;
+      const uint32_t sub = f == FAM_DROP ? reason : 0u;
+      const uint32_t add_b = f <= FAM_DROP ? nb : 0u;
+      if (inl[g]) {
+        const unsigned long long val = kLdsCountOne | (big ? 0u : add_b);
+        atomicAdd(&lds[hit && d_ok ? row_d + sub : dummy], val);
+        atomicAdd(&lds[hit && s_ok ? row_s + sub : dummy], val);
+        if (big && hit && add_b) {
+          if (d_ok) atomicAdd(&a.d.byt[row_d + sub], (unsigned long long)add_b);
+          if (s_ok) atomicAdd(&a.d.byt[row_s + sub], (unsigned long long)add_b);
+        }
+      } else if (hit) {
+        if (d_ok) ds.spill_add(row_d + sub, add_b);
+        if (s_ok) ds.spill_add(row_s + sub, add_b);
       }
     }
   });
@@ -463,19 +491,15 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
       const uint64_t bin = v >> 32;
       if (bin < lo || bin >= hi) continue;
       const uint32_t nb = (uint32_t)v;
-      if (nb < kLdsByteLimit) {
-        atomicAdd(&win[bin - lo], kLdsCountOne | nb);
-      } else {
-        atomicAdd(&d.cnt[bin], 1ULL);
-        atomicAdd(&d.byt[bin], (unsigned long long)nb);
-      }
+      atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
+      if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
     }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
     const unsigned long long v = win[i];
     if (v) {
-      atomicAdd(&d.cnt[lo + i], v >> 40);
+      atomicAdd(&d.cnt[lo + i], v >> kLdsCountShift);
       const unsigned long long by = v & kLdsBytesMask;
       if (by) atomicAdd(&d.byt[lo + i], by);
     }
@@ -547,7 +571,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.spill_count = a.spill_count;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  const size_t lds = ((size_t)a.lds_bins + 1) * 8;
+  const size_t lds = ((size_t)a.lds_bins + kLdsExtraWords) * 8;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   switch (a.dense_ng) {  // dense local-context fast path, groups rounded up to 1/2/4/8

@@ -351,7 +351,18 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         }
   }
   // geometry: one 1024-thread workgroup per CU holding L dense bins in LDS
-  a.lds_bins = (uint32_t)std::min<uint64_t>(c->dense_len, kLdsMaxBins);
+  // LDS window: the longest prefix of whole dense groups (hottest first) that fits
+  a.lds_bins = 0;
+  {
+    std::vector<std::pair<uint64_t, uint64_t>> spans;  // (base, bins) of dense groups
+    for (int g = 0; g < c->plan.ngroups; ++g)
+      if (!c->plan.g[g].sparse) spans.emplace_back(c->plan.g[g].dense_base, c->plan.g[g].nbins);
+    std::sort(spans.begin(), spans.end());
+    for (auto &sp : spans) {
+      if (sp.first != a.lds_bins || sp.first + sp.second > kLdsMaxBins) break;
+      a.lds_bins = (uint32_t)(sp.first + sp.second);
+    }
+  }
   a.blocks = a.lds_bins ? c->n_cu : c->n_cu * 4;
   a.threads = a.lds_bins ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
@@ -651,6 +662,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
     gp.nsub = groups[g].nsub;
     gp.dense_base = groups[g].dense_base;
     gp.key_mode = groups[g].key_mode;
+    gp.nbins = groups[g].sparse ? 0u : (uint32_t)(groups[g].nkeys * 2 * groups[g].nsub);
     if ((gp.src_opts | gp.dst_opts) & OPT_PORT) p.need_ports = 1;
     if (gp.family == FAM_DNS_REQ || gp.family == FAM_DNS_RESP) p.need_dns = 1;
     any_sparse |= groups[g].sparse;
