@@ -27,6 +27,10 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o run \
         -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/${TAG}_prof.log" 2>&1
       rc=$?; echo "prof rc=$rc" >> "$OUT/${TAG}_prof.log"; [ $rc -ne 0 ] && exit $rc ;;
+    micro)
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/mb scripts/microbench.hip > "$OUT/${TAG}_micro.err" 2>&1 || exit 1
+      timeout -k 10 300 /tmp/mb > "$OUT/${TAG}_micro.jsonl" 2>> "$OUT/${TAG}_micro.err"
+      rc=$?; echo "micro rc=$rc" >> "$OUT/${TAG}_micro.err"; [ $rc -ne 0 ] && exit $rc ;;
     ablate)
       timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
       rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;
