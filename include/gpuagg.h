@@ -60,7 +60,11 @@ typedef struct gpuagg_config {
   uint32_t cms_depth;            /* count-min rows (0 = sketches off)                */
   uint32_t cms_width_log2;       /* count-min columns = 2^this                       */
   uint32_t hll_precision;        /* HyperLogLog p (registers 2^p per source pod; 0=off) */
+  uint32_t flags;                /* GPUAGG_FLAG_* (0 = defaults)                     */
 } gpuagg_config;
+
+/* gpuagg_config.flags */
+#define GPUAGG_FLAG_NO_LDS_IP_TABLE 1u /* keep the IP table in HBM/L2 only (diagnostics) */
 
 int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out);
 void gpuagg_destroy(gpuagg_ctx *ctx);

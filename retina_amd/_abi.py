@@ -25,7 +25,9 @@ class Config(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("remote_context", C.c_int32),
                 ("max_slots", C.c_uint32), ("max_ips", C.c_uint32),
                 ("sparse_capacity_log2", C.c_uint32), ("cms_depth", C.c_uint32),
-                ("cms_width_log2", C.c_uint32), ("hll_precision", C.c_uint32)]
+                ("cms_width_log2", C.c_uint32), ("hll_precision", C.c_uint32),
+                ("flags", C.c_uint32)]
+FLAG_NO_LDS_IP_TABLE = 1
 
 
 class MetricOptions(C.Structure):

@@ -132,9 +132,9 @@ GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) {
 // aggregates <= 2^20 records between flushes and an update carries < 2^24 bytes in
 // LDS (bigger packets add their bytes with a global atomic), so both fields are exact.
 // LDS layout: bins [0, L), 64 per-lane dummy words [L, L+64) that absorb predicated-
-// off updates, the spill counter at L+64.
+// off updates, then 16 u32 spill-window counters.
 constexpr uint32_t kLdsBytes = 160 * 1024;
-constexpr uint32_t kLdsExtraWords = 65;
+constexpr uint32_t kLdsExtraWords = 64 + 8;  // 64 dummies + 16 u32 spill-window counters
 constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
 constexpr uint32_t kLdsCountShift = 44;
 constexpr uint32_t kLdsByteLimit = 1u << 24;
@@ -142,6 +142,27 @@ constexpr uint64_t kLdsCountOne = 1ULL << kLdsCountShift;
 constexpr uint64_t kLdsBytesMask = kLdsCountOne - 1;
 constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^20, multiple of 4
 constexpr uint32_t kMaxSpillWindows = 16;
+
+// ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------
+// Bucketized cuckoo: 2 candidate buckets of 4 keys (16 B, one ds_read_b128 each),
+// keys u32 (0xFFFFFFFF = empty), values u16 slot ids in a parallel array.  Only built
+// for pods that are not the apiserver pseudo pod: in local context such an endpoint is
+// treated exactly like "no endpoint" (types.go:407-413).
+constexpr uint32_t kIplWays = 4;
+constexpr uint32_t kIplEmptyKey = 0xFFFFFFFFu;
+constexpr uint32_t kIplNoSlot = 0xFFFFu;
+constexpr uint32_t kIplMaxBytes = 112 * 1024;
+GA_HD uint32_t ipl_bucket(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)h * nb) >> 32); }
+GA_HD uint32_t ipl_image_bytes(uint32_t nb) {  // keys, then u16 values, 16-byte aligned
+  return nb * kIplWays * 4 + ((nb * kIplWays * 2 + 15) & ~15u);
+}
+// 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
+// correct the rare carry / wrap exactly with global atomics; count-only families
+// (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).
+constexpr uint32_t kL4CountShift = 20;
+constexpr uint32_t kL4BytesMask = (1u << kL4CountShift) - 1;
+constexpr uint32_t kL4ByteLimit = 1u << kL4CountShift;
+constexpr uint32_t kL4ExtraBytes = 64 * 4 + kMaxSpillWindows * 4;  // dummies + spill counters
 GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
 }

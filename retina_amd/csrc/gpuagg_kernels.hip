@@ -57,10 +57,16 @@ struct KArgs {
   DevDense d;
   DevSparse s;
   DevSketch sk;
-  uint32_t lds_bins;  // L: dense bins privatised in LDS
+  uint32_t lds_bins;  // L: dense bins privatised in LDS (u64 words; tier-1: u32 words)
+  // spill lists: per workgroup, one list per fold window of `win_bins` bins starting at
+  // dense bin `spill_lo`; list (b, w) at spill + (b*nwin + w)*spill_cap
   uint32_t spill_cap;
-  unsigned long long *spill;  // [gridDim.x][spill_cap] or null
-  uint32_t *spill_count;      // [gridDim.x]
+  uint32_t nwin, win_bins, spill_lo;
+  unsigned long long *spill;  // or null: bins >= lds_bins use global atomics
+  uint32_t *spill_count;      // [gridDim.x * nwin]
+  // tier-1: LDS image of the IP table
+  const uint8_t *ipl;
+  uint32_t ipl_nb, ipl_seed, ipl_bytes;
   Plan p;
 };
 
@@ -120,28 +126,39 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
   atomicAdd(s.dropped, 1ULL);
 }
 
-// Dense counter updates: LDS window, spill list, or (fallback) global atomics.
+// Exact add of one (count 1, bytes nb) update into a packed u64 LDS word
+// (count:20 | bytes:44) when a workgroup may exceed the field widths: the lane whose
+// add carries out of the bytes field or wraps the count field books the difference
+// into the global counters (rare).  Sum over all adds is exact.
+__device__ __forceinline__ void lds_add64_exact(unsigned long long *w, uint32_t gbin, uint32_t nb,
+                                                const DevDense &d) {
+  const uint32_t b = nb < kLdsByteLimit ? nb : 0u;
+  const unsigned long long old = atomicAdd(w, kLdsCountOne | b);
+  if (nb >= kLdsByteLimit) atomicAdd(&d.byt[gbin], (unsigned long long)nb);
+  const unsigned long long carry = ((old & kLdsBytesMask) + b) >> kLdsCountShift;
+  const unsigned long long wrap = ((old >> kLdsCountShift) + 1ULL + carry) >> (64 - kLdsCountShift);
+  if (carry) {
+    atomicAdd(&d.byt[gbin], kLdsCountOne);
+    atomicAdd(&d.cnt[gbin], ~0ULL);  // the carry also bumped the count field
+  }
+  if (wrap) atomicAdd(&d.cnt[gbin], 1ULL << (64 - kLdsCountShift));
+}
+
+// Dense counter updates: LDS window, bucketed spill lists, or (fallback) global atomics.
 struct DenseSink {
-  unsigned long long *lds;
+  unsigned long long *lds;  // u64 bins (generic / dense_local kernels)
   uint32_t L;
-  unsigned int *spill_ctr;  // in LDS
+  unsigned int *ctr;        // per-window spill counters (LDS)
   unsigned long long *spill;
-  uint32_t spill_cap;
+  uint32_t spill_cap, win_bins, spill_lo;
   DevDense d;
 
-  // Appends (bin, bytes) to this workgroup's spill list: one LDS atomic per wave
-  // (the active lanes here are exactly the spilling ones); global atomics if full.
   __device__ __forceinline__ void spill_add(uint32_t bin, uint32_t nbytes) const {
     if (spill) {
-      const unsigned long long act = __ballot(1);
-      const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-      unsigned int base = 0;
-      if (lane == leader) base = atomicAdd(spill_ctr, (unsigned int)__builtin_popcountll(act));
-      base = __shfl(base, (int)leader);
-      const unsigned int pos = base + (unsigned int)__builtin_popcountll(act & ((1ULL << lane) - 1ULL));
+      const uint32_t w = (bin - spill_lo) / win_bins;
+      const unsigned int pos = atomicAdd(&ctr[w], 1u);
       if (pos < spill_cap) {
-        spill[pos] = ((unsigned long long)bin << 32) | nbytes;
+        spill[(size_t)w * spill_cap + pos] = ((unsigned long long)bin << 32) | nbytes;
         return;
       }
     }
@@ -158,6 +175,19 @@ struct DenseSink {
     spill_add(bin, nbytes);
   }
 };
+
+__device__ __forceinline__ DenseSink make_sink(const KArgs &a, unsigned long long *lds, uint32_t L,
+                                               unsigned int *ctr) {
+  return DenseSink{lds, L, ctr,
+                   a.spill ? a.spill + (size_t)blockIdx.x * a.nwin * a.spill_cap : nullptr,
+                   a.spill_cap, a.win_bins, a.spill_lo, a.d};
+}
+
+__device__ __forceinline__ void spill_counts_out(const KArgs &a, const unsigned int *ctr) {
+  if (a.spill)
+    for (uint32_t w = threadIdx.x; w < a.nwin; w += blockDim.x)
+      a.spill_count[blockIdx.x * a.nwin + w] = ctr[w] < a.spill_cap ? ctr[w] : a.spill_cap;
+}
 
 // Side tuple of a context (types.go:418-505): only the fields the options read.
 struct SideKey {
@@ -351,8 +381,7 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
 __device__ __forceinline__ DenseSink dense_sink_init(const KArgs &a, unsigned long long *lds) {
   for (uint32_t i = threadIdx.x; i < a.lds_bins + kLdsExtraWords; i += blockDim.x) lds[i] = 0ULL;
   __syncthreads();
-  return DenseSink{lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins + 64],
-                   a.spill ? a.spill + (size_t)blockIdx.x * a.spill_cap : nullptr, a.spill_cap, a.d};
+  return make_sink(a, lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins + 64]);
 }
 
 __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds) {
@@ -366,10 +395,7 @@ __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds)
       if (by) atomicAdd(&a.d.byt[i], by);
     }
   }
-  if (a.spill && threadIdx.x == 0) {
-    const unsigned int c = *ds.spill_ctr;
-    a.spill_count[blockIdx.x] = c < a.spill_cap ? c : a.spill_cap;
-  }
+  spill_counts_out(a, ds.ctr);
 }
 
 // Generic aggregation: any plan (dense, sparse, DNS, remote context, sketches).
@@ -467,32 +493,205 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   dense_flush(a, ds);
 }
 
+// ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
+// Lookup in the LDS cuckoo image: two 16-byte bucket reads, 8 compares, one u16 read.
+__device__ __forceinline__ uint32_t ipl_key_index(uint32_t ip, uint32_t b1, uint32_t b2,
+                                                  const uint4 &k1, const uint4 &k2) {
+  uint32_t j = 0xFFFFFFFFu;
+  j = k1.x == ip ? b1 * 4 + 0 : j;
+  j = k1.y == ip ? b1 * 4 + 1 : j;
+  j = k1.z == ip ? b1 * 4 + 2 : j;
+  j = k1.w == ip ? b1 * 4 + 3 : j;
+  j = k2.x == ip ? b2 * 4 + 0 : j;
+  j = k2.y == ip ? b2 * 4 + 1 : j;
+  j = k2.z == ip ? b2 * 4 + 2 : j;
+  j = k2.w == ip ? b2 * 4 + 3 : j;
+  return j;
+}
+
+struct L4Ctx {
+  uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then 16 spill-window counters
+  uint32_t L4, dummy;
+  DevDense d;
+  // bytes families: count:12 | bytes:20, corrected exactly (kL4* in gpuagg_internal.h)
+  __device__ __forceinline__ void add_bytes(bool valid, uint32_t bin, uint32_t nb) const {
+    const bool big = nb >= kL4ByteLimit;
+    const uint32_t b = big ? 0u : nb;
+    const uint32_t old = atomicAdd(&bins[valid ? bin : dummy], (1u << kL4CountShift) | b);
+    if (!valid) return;
+    if (big) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+    const uint32_t carry = ((old & kL4BytesMask) + b) >> kL4CountShift;
+    const uint32_t wrap = ((old >> kL4CountShift) + 1u + carry) >> (32 - kL4CountShift);
+    if (carry | wrap) {
+      if (carry) {
+        atomicAdd(&d.byt[bin], (unsigned long long)kL4ByteLimit);
+        atomicAdd(&d.cnt[bin], ~0ULL);
+      }
+      if (wrap) atomicAdd(&d.cnt[bin], 1ULL << (32 - kL4CountShift));
+    }
+  }
+  __device__ __forceinline__ void add_count(bool valid, uint32_t bin) const {
+    atomicAdd(&bins[valid ? bin : dummy], 1u);
+  }
+};
+
+template <int NG, bool kVec>
+__global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t nb = a.ipl_nb;
+  const uint32_t *keys = (const uint32_t *)smem;
+  const uint16_t *vals = (const uint16_t *)(smem + (size_t)nb * 16);
+  uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
+  const uint32_t L4 = a.lds_bins;
+  for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
+    ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
+  for (uint32_t i = threadIdx.x; i < L4 + 64 + kMaxSpillWindows; i += blockDim.x) bins[i] = 0u;
+  __syncthreads();
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const L4Ctx l4{bins, L4, L4 + lane, a.d};
+  const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
+  const int ng = a.p.ngroups;
+  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  bool inl[NG];
+  bool any_flags = false;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    fam[g] = g < ng ? a.p.g[g].family : (uint32_t)FAM_COUNT;
+    base[g] = (uint32_t)a.p.g[g].dense_base;
+    nsub[g] = a.p.g[g].nsub;
+    keyed[g] = a.p.g[g].key_mode;
+    inl[g] = base[g] + a.p.g[g].nbins <= L4;
+    any_flags |= fam[g] == FAM_TCPFLAGS;
+  }
+  auto record = [&](uint32_t nbytes, uint32_t meta, int32_t ss, int32_t sd) {
+    const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
+    const bool s_ok = ss >= 0, d_ok = sd >= 0;  // apiserver IPs are not in the image
+    const uint32_t flagmask = (any_flags && verdict == kVerdictForwarded && proto == 6)
+                                  ? flag_label_mask(meta_flags(meta)) : 0u;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const uint32_t f = fam[g];
+      if (f == FAM_COUNT) continue;
+      const uint32_t kd = keyed[g] ? (uint32_t)sd : 0u, ks = keyed[g] ? (uint32_t)ss : 0u;
+      const uint32_t row_d = base[g] + (kd * 2u) * nsub[g];
+      const uint32_t row_s = base[g] + (ks * 2u + 1u) * nsub[g];
+      if (f == FAM_TCPFLAGS) {
+        uint32_t m = flagmask;
+        if (inl[g]) {
+          while (__ballot(m != 0)) {
+            const bool v = m != 0;
+            const uint32_t bit = v ? (uint32_t)__builtin_ctz(m) : 0u;
+            l4.add_count(v && d_ok, row_d + bit);
+            l4.add_count(v && s_ok, row_s + bit);
+            m &= m - 1;
+          }
+        } else {
+          for (; m; m &= m - 1) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            if (d_ok) ds.spill_add(row_d + bit, 0);
+            if (s_ok) ds.spill_add(row_s + bit, 0);
+          }
+        }
+        continue;
+      }
+      bool hit;
+      if (f == FAM_FWD) hit = verdict == kVerdictForwarded;
+      else if (f == FAM_DROP) hit = verdict == kVerdictDropped;
+      else hit = verdict == kVerdictRetrans;
+      const uint32_t sub = f == FAM_DROP ? reason : 0u;
+      if (inl[g]) {
+        if (f <= FAM_DROP) {
+          l4.add_bytes(hit && d_ok, row_d + sub, nbytes);
+          l4.add_bytes(hit && s_ok, row_s + sub, nbytes);
+        } else {
+          l4.add_count(hit && d_ok, row_d + sub);
+          l4.add_count(hit && s_ok, row_s + sub);
+        }
+      } else if (hit) {
+        const uint32_t add_b = f <= FAM_DROP ? nbytes : 0u;
+        if (d_ok) ds.spill_add(row_d + sub, add_b);
+        if (s_ok) ds.spill_add(row_s + sub, add_b);
+      }
+    }
+  };
+  auto find = [&](uint32_t ip) -> uint32_t {  // slot id or kIplNoSlot
+    const uint32_t b1 = ipl_bucket(ip_h1(ip, a.ipl_seed), nb), b2 = ipl_bucket(ip_h2(ip, a.ipl_seed), nb);
+    const uint4 k1 = *(const uint4 *)&keys[b1 * 4], k2 = *(const uint4 *)&keys[b2 * 4];
+    const uint32_t j = ipl_key_index(ip, b1, b2, k1, k2);
+    return j == 0xFFFFFFFFu ? kIplNoSlot : (uint32_t)vals[j];
+  };
+  auto slot_of = [](uint32_t v) { return v == kIplNoSlot ? -1 : (int32_t)v; };
+
+  const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
+  const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
+  uint64_t tail = start;
+  if (kVec && start < end) {
+    const uint64_t vend = start + ((end - start) & ~3ULL);
+    const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
+    const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
+    for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
+      const uint64_t v = i >> 2;
+      const uint4 vs = s4[v], vd = d4[v], vb = b4[v], vm = m4[v];
+      uint32_t f0 = find(vs.x), f1 = find(vs.y), f2 = find(vs.z), f3 = find(vs.w);
+      uint32_t g0 = find(vd.x), g1 = find(vd.y), g2 = find(vd.z), g3 = find(vd.w);
+      uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        record(b0, m0, slot_of(f0), slot_of(g0));
+        b0 = b1; b1 = b2; b2 = b3; m0 = m1; m1 = m2; m2 = m3;
+        f0 = f1; f1 = f2; f2 = f3; g0 = g1; g1 = g2; g2 = g3;
+      }
+    }
+    tail = vend;
+  }
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x)
+    record(a.c.bytes[i], a.c.meta[i], slot_of(find(a.c.src[i])), slot_of(find(a.c.dst[i])));
+
+  __syncthreads();
+  // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    if (fam[g] == FAM_COUNT || !inl[g]) continue;
+    const bool with_bytes = fam[g] <= FAM_DROP;
+    const uint32_t hi = base[g] + a.p.g[g].nbins;
+    for (uint32_t i = base[g] + threadIdx.x; i < hi; i += blockDim.x) {
+      const uint32_t w = bins[i];
+      if (!w) continue;
+      if (with_bytes) {
+        atomicAdd(&a.d.cnt[i], (unsigned long long)(w >> kL4CountShift));
+        const uint32_t by = w & kL4BytesMask;
+        if (by) atomicAdd(&a.d.byt[i], (unsigned long long)by);
+      } else {
+        atomicAdd(&a.d.cnt[i], (unsigned long long)w);
+      }
+    }
+  }
+  spill_counts_out(a, bins + L4 + 64);
+}
+
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.
-// Workgroups of the same spill partition share blockIdx % 8 (one XCD under the
-// observed round-robin placement -- speed only), so the 8..16 window passes over a
-// partition mostly hit that XCD's L2.
+// List (A-workgroup l, window w) holds only window w's updates, so every entry is read
+// once.  Workgroups of one partition share blockIdx % 8 (one XCD under the observed
+// round-robin placement -- speed only).
 __global__ __launch_bounds__(1024) void spill_window_kernel(
     const unsigned long long *spill, const uint32_t *spill_count, uint32_t n_lists,
-    uint32_t spill_cap, uint32_t L, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d) {
+    uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
   const uint32_t b = blockIdx.x;
   const uint32_t w = (b >> 3) % nwin;
   const uint32_t part = (b & 7u) + 8u * (b / (8u * nwin));
   const uint32_t nparts = gridDim.x / nwin;
-  const uint64_t lo = (uint64_t)L + (uint64_t)w * W;
+  const uint64_t lo = (uint64_t)lo0 + (uint64_t)w * W;
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
   __syncthreads();
   for (uint32_t l = part; l < n_lists; l += nparts) {
-    const uint32_t cnt = spill_count[l];
-    const unsigned long long *e = spill + (size_t)l * spill_cap;
+    const uint32_t cnt = spill_count[(size_t)l * nwin + w];
+    const unsigned long long *e = spill + ((size_t)l * nwin + w) * spill_cap;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
       const unsigned long long v = e[j];
-      const uint64_t bin = v >> 32;
-      if (bin < lo || bin >= hi) continue;
-      const uint32_t nb = (uint32_t)v;
-      atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
-      if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+      const uint32_t bin = (uint32_t)(v >> 32);
+      lds_add64_exact(&win[bin - lo], bin, (uint32_t)v, d);
     }
   }
   __syncthreads();
@@ -568,13 +767,29 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.lds_bins = a.lds_bins;
   k.spill = (unsigned long long *)a.spill;
   k.spill_cap = a.spill_cap;
+  k.nwin = a.nwin;
+  k.win_bins = a.win_bins;
+  k.spill_lo = a.spill_lo;
   k.spill_count = a.spill_count;
+  k.ipl = a.ipl;
+  k.ipl_nb = a.ipl_nb;
+  k.ipl_seed = a.ipl_seed;
+  k.ipl_bytes = a.ipl_bytes;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  const size_t lds = ((size_t)a.lds_bins + kLdsExtraWords) * 8;
+  const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
+                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
-  switch (a.dense_ng) {  // dense local-context fast path, groups rounded up to 1/2/4/8
+  switch (a.tier1 ? 100 + a.dense_ng : a.dense_ng) {
+    case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<1, false>, k, B, T, lds, st); break;
+    case 102: e = a.vec ? launch_k(dense_lds_kernel<2, true>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<2, false>, k, B, T, lds, st); break;
+    case 104: e = a.vec ? launch_k(dense_lds_kernel<4, true>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<4, false>, k, B, T, lds, st); break;
+    case 108: e = a.vec ? launch_k(dense_lds_kernel<8, true>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<8, false>, k, B, T, lds, st); break;  // dense local-context fast path, groups rounded up to 1/2/4/8
     case 1: e = a.vec ? launch_k(dense_local_kernel<1, true>, k, B, T, lds, st)
                       : launch_k(dense_local_kernel<1, false>, k, B, T, lds, st); break;
     case 2: e = a.vec ? launch_k(dense_local_kernel<2, true>, k, B, T, lds, st)
@@ -599,7 +814,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)a.win_bins * 8, st,
                      (const unsigned long long *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.lds_bins, a.dense_len, a.win_bins, a.nwin, k.d);
+                     a.spill_lo, a.dense_len, a.win_bins, a.nwin, k.d);
   return hipGetLastError();
 }
 

@@ -41,7 +41,11 @@ struct LaunchArgs {
   uint32_t spill_cap;
   uint32_t *spill_count;
   uint32_t win_bins, nwin, win_blocks;
+  uint32_t spill_lo;    // first spilled dense bin (fold windows start here)
   uint32_t dense_ng;    // 0: generic kernel; 1/2/4/8: dense local-context kernel
+  bool tier1;           // dense kernel with the IP table and u32 bins in LDS
+  const uint8_t *ipl;
+  uint32_t ipl_nb, ipl_seed, ipl_bytes;
 };
 
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.

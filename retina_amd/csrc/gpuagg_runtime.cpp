@@ -132,6 +132,10 @@ struct gpuagg_ctx {
   uint64_t *d_ip = nullptr;
   size_t ip_cap = 0;  // slots
   uint32_t ip_seed = 0;
+  // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
+  uint8_t *d_ipl = nullptr;
+  size_t ipl_alloc = 0;
+  uint32_t ipl_nb = 0, ipl_seed = 0, ipl_bytes = 0;
   uint64_t ip_version = 0;
 
   // dense counters
@@ -352,15 +356,31 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   }
   // geometry: one 1024-thread workgroup per CU holding L dense bins in LDS
   // LDS window: the longest prefix of whole dense groups (hottest first) that fits
-  a.lds_bins = 0;
-  {
-    std::vector<std::pair<uint64_t, uint64_t>> spans;  // (base, bins) of dense groups
-    for (int g = 0; g < c->plan.ngroups; ++g)
-      if (!c->plan.g[g].sparse) spans.emplace_back(c->plan.g[g].dense_base, c->plan.g[g].nbins);
-    std::sort(spans.begin(), spans.end());
+  std::vector<std::pair<uint64_t, uint64_t>> spans;  // (base, bins) of dense groups
+  for (int g = 0; g < c->plan.ngroups; ++g)
+    if (!c->plan.g[g].sparse) spans.emplace_back(c->plan.g[g].dense_base, c->plan.g[g].nbins);
+  std::sort(spans.begin(), spans.end());
+  auto prefix = [&](uint64_t limit) {
+    uint32_t L = 0;
     for (auto &sp : spans) {
-      if (sp.first != a.lds_bins || sp.first + sp.second > kLdsMaxBins) break;
-      a.lds_bins = (uint32_t)(sp.first + sp.second);
+      if (sp.first != L || sp.first + sp.second > limit) break;
+      L = (uint32_t)(sp.first + sp.second);
+    }
+    return L;
+  };
+  a.lds_bins = prefix(kLdsMaxBins);
+  // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
+  a.tier1 = false;
+  if (a.dense_ng && c->ipl_bytes && !spans.empty() &&
+      c->ipl_bytes + kL4ExtraBytes < kLdsBytes) {
+    const uint32_t L4 = prefix((kLdsBytes - c->ipl_bytes - kL4ExtraBytes) / 4);
+    if (L4 > 0) {
+      a.tier1 = true;
+      a.lds_bins = L4;
+      a.ipl = c->d_ipl;
+      a.ipl_nb = c->ipl_nb;
+      a.ipl_seed = c->ipl_seed;
+      a.ipl_bytes = c->ipl_bytes;
     }
   }
   a.blocks = a.lds_bins ? c->n_cu : c->n_cu * 4;
@@ -378,27 +398,31 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
             (!c->plan.need_dns || al(a.cols.dns_id));
     a.spill = nullptr;
     a.spill_count = nullptr;
+    a.nwin = 0;
     if (c->dense_len > a.lds_bins) {
+      // bins past the LDS window: per-workgroup spill lists bucketed by fold window
       const uint64_t rem = c->dense_len - a.lds_bins;
       const uint32_t nwin = (uint32_t)((rem + kLdsMaxBins - 1) / kLdsMaxBins);
-      if (nwin <= kMaxSpillWindows && a.chunk * 2 < 0xFFFFFFFFull) {
-        a.spill_cap = (uint32_t)(2 * a.chunk);
-        const size_t need = (size_t)a.blocks * a.spill_cap;
+      const uint64_t cap = 2 * a.chunk / nwin + 4096;  // overflow falls back to global atomics
+      if (nwin <= kMaxSpillWindows && cap < 0xFFFFFFFFull) {
+        a.spill_cap = (uint32_t)cap;
+        const size_t need = (size_t)a.blocks * nwin * a.spill_cap;
         if (need > c->spill_alloc) {
           dev_free(c->d_spill);
           c->spill_alloc = 0;
           if ((rc = dev_alloc(c, &c->d_spill, need))) return rc;
           c->spill_alloc = need;
         }
-        if (a.blocks > c->spill_count_alloc) {
+        if ((size_t)a.blocks * nwin > c->spill_count_alloc) {
           dev_free(c->d_spill_count);
           c->spill_count_alloc = 0;
-          if ((rc = dev_alloc(c, &c->d_spill_count, a.blocks))) return rc;
-          c->spill_count_alloc = a.blocks;
+          if ((rc = dev_alloc(c, &c->d_spill_count, (size_t)a.blocks * nwin))) return rc;
+          c->spill_count_alloc = (size_t)a.blocks * nwin;
         }
         a.spill = c->d_spill;
         a.spill_count = c->d_spill_count;
         a.nwin = nwin;
+        a.spill_lo = a.lds_bins;
         a.win_bins = (uint32_t)((rem + nwin - 1) / nwin);
         a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
       }
@@ -470,6 +494,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
     delete b;
   }
   dev_free(c->d_ip);
+  dev_free(c->d_ipl);
   dev_free(c->d_dense_cnt);
   dev_free(c->d_dense_byt);
   dev_free(c->sv.k0);
@@ -766,6 +791,83 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   }
   HIPCHK(c, hipMemcpy(c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
   c->ip_cap = cap;
+  // LDS image: non-apiserver pods only (local context treats the apiserver pseudo pod
+  // like no endpoint), u16 slot ids
+  c->ipl_bytes = 0;
+  if (!(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
+    std::vector<std::pair<uint32_t, uint32_t>> ents;
+    bool fits = true;
+    for (const auto &kv : last) {
+      const uint32_t sl = (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1));
+      if ((kv.second >> 53) & 1) continue;
+      if (sl >= kIplNoSlot) fits = false;
+      ents.emplace_back(kv.first, sl);
+    }
+    uint32_t nb = std::max<uint32_t>(1, (uint32_t)((ents.size() * 100 + 85 * kIplWays - 1) / (85 * kIplWays)));
+    std::vector<uint32_t> keys;
+    std::vector<uint16_t> vals;
+    uint32_t iseed = 0x6A09E667u;
+    bool built = false;
+    for (int attempt = 0; fits && attempt < 64 && ipl_image_bytes(nb) <= kIplMaxBytes; ++attempt) {
+      if (attempt && attempt % 8 == 0) nb = nb + nb / 16 + 1;
+      iseed = (uint32_t)fmix64((uint64_t)iseed + 0xBB67AE8584CAA73BULL * (attempt + 1));
+      keys.assign((size_t)nb * kIplWays, kIplEmptyKey);
+      vals.assign((size_t)nb * kIplWays, (uint16_t)kIplNoSlot);
+      bool ok = true;
+      uint64_t rng = iseed | 1;
+      for (const auto &e : ents) {
+        uint32_t k = e.first;
+        uint16_t v = (uint16_t)e.second;
+        uint32_t b = ipl_bucket(ip_h1(k, iseed), nb);
+        int kicks = 0;
+        for (;;) {
+          const uint32_t b1 = ipl_bucket(ip_h1(k, iseed), nb), b2 = ipl_bucket(ip_h2(k, iseed), nb);
+          int slot = -1;
+          for (uint32_t bb : {b1, b2}) {
+            for (uint32_t w = 0; w < kIplWays && slot < 0; ++w)
+              if (keys[(size_t)bb * kIplWays + w] == kIplEmptyKey) slot = (int)(bb * kIplWays + w);
+            if (slot >= 0) break;
+          }
+          if (slot >= 0) {
+            keys[slot] = k;
+            vals[slot] = v;
+            break;
+          }
+          if (++kicks > 1000) {
+            ok = false;
+            break;
+          }
+          // evict a random resident of the bucket not used last time
+          b = (b == b1) ? b2 : b1;
+          rng ^= rng << 13, rng ^= rng >> 7, rng ^= rng << 17;
+          const size_t victim = (size_t)b * kIplWays + (rng % kIplWays);
+          std::swap(k, keys[victim]);
+          std::swap(v, vals[victim]);
+        }
+        if (!ok) break;
+      }
+      if (ok) {
+        built = true;
+        break;
+      }
+    }
+    if (built) {
+      const uint32_t bytes = ipl_image_bytes(nb);
+      std::vector<uint8_t> img(bytes, 0);
+      memcpy(img.data(), keys.data(), keys.size() * 4);
+      memcpy(img.data() + keys.size() * 4, vals.data(), vals.size() * 2);
+      if (bytes > c->ipl_alloc) {
+        dev_free(c->d_ipl);
+        c->ipl_alloc = 0;
+        if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
+        c->ipl_alloc = bytes;
+      }
+      HIPCHK(c, hipMemcpy(c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_nb = nb;
+      c->ipl_seed = iseed;
+      c->ipl_bytes = bytes;
+    }
+  }
   c->ip_seed = seed;
   c->ip_version = version;
   return GPUAGG_OK;

@@ -7,6 +7,7 @@ prints one JSON line per variant with the HIP-event time per launch:
   drop      drop_count/bytes    (dense, LDS window + spill lists + fold)
   c2        forward + drop      (the bench spec)
   c2-1kpods C2 spec with 1k pods (every dense bin in LDS, no spill)
+  *-hbm-ip-table  same with FLAG_NO_LDS_IP_TABLE (IP table in HBM, u64 LDS bins)
   remote    C1 remote spec (sparse table)
 """
 
@@ -28,9 +29,9 @@ FWD = W.LOCAL_FWD_DROP[:2]
 DROP = W.LOCAL_FWD_DROP[2:]
 
 
-def run(name, spec, pods, cols, n, remote=False, steps=5):
+def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0):
     g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
-               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24)
+               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     dc = GpuAgg.device_columns(*cols)
@@ -59,6 +60,8 @@ def main():
     run("fwd", FWD, pods, cols, n)
     run("drop", DROP, pods, cols, n)
     run("c2", W.LOCAL_FWD_DROP, pods, cols, n)
+    run("fwd-hbm-ip-table", FWD, pods, cols, n, flags=1)
+    run("c2-hbm-ip-table", W.LOCAL_FWD_DROP, pods, cols, n, flags=1)
     small = W.make_pods(1_000, seed=2)
     cols_s, _ = gen_device_records(n, small, 3, dev, {})
     run("c2-1kpods", W.LOCAL_FWD_DROP, small, cols_s, n)

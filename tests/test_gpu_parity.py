@@ -172,3 +172,18 @@ def test_sketches_bit_exact(gpu_device):
     est = g.cms_estimate(int(recs.src_ip[0]), int(recs.dst_ip[0]), int(recs.ports[0]), int(recs.meta[0] & 0xFF))
     assert est >= 1
     g.close()
+
+
+TIER0 = [c for c in CASES if c[0] in ("local-dense-ns-pod", "local-dense-workload", "odd-rows-local")]
+
+
+@pytest.mark.parametrize("cid,sp,remote,gen", TIER0, ids=[c[0] for c in TIER0])
+def test_parity_without_lds_ip_table(gpu_device, cid, sp, remote, gen):
+    """The dense kernel with the IP table in HBM (FLAG_NO_LDS_IP_TABLE) stays exact."""
+    from retina_amd import _abi
+    pods = W.make_pods(400, seed=11)
+    recs = W.gen_records(30_000, pods, seed=zlib.crc32(cid.encode()) & 0xFFFF, **gen)
+    want = oracle_series(recs, pods, sp, remote)
+    got = engine_series(recs, pods, sp, remote, gpu_device, host_fed=True, chunks=3,
+                        flags=_abi.FLAG_NO_LDS_IP_TABLE)
+    assert got == want, diff_series(got, want)

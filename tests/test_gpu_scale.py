@@ -70,3 +70,35 @@ def test_host_fed_equals_device_and_chunking(gpu_device):
     a = engine_series(recs, pods, sp, False, gpu_device, host_fed=True, chunks=1)
     b = engine_series(recs, pods, sp, False, gpu_device, host_fed=False, chunks=7)
     assert a == b, diff_series(a, b)
+
+
+@pytest.mark.parametrize("flags", [0, 1], ids=["tier1", "no-lds-ip-table"])
+def test_packed_field_overflow_exact(gpu_device, flags):
+    """Packed LDS counters (u32 count:12|bytes:20 in tier-1, u64 count:20|bytes:44 in the
+    fold windows) must carry exactly.  One hot pod pair, 40M records: every LDS count field
+    wraps many times and byte fields carry; forward bins live in LDS, drop bins are
+    spilled and folded (10k pods).  Expected = a 4-record batch x 10M (linearity)."""
+    import torch
+    from retina_amd import GpuAgg
+    pods = W.make_pods(10_000, seed=5)
+    base = W.gen_records(400, pods, seed=5, pod_frac=1.0, drop_frac=0.5)
+    verdict = (base.meta >> 8) & 0xFF
+    ok = (base.src_ip != base.dst_ip)
+    f = int(np.flatnonzero((verdict == W.V_FWD) & ok)[0])
+    d = int(np.flatnonzero((verdict == W.V_DROP) & ok)[0])
+    idx = np.array([f, f, d, f])
+    nbytes = np.array([1_000_000, 5_000_000, 8_400_000, (1 << 20) - 1], np.uint32)
+    four = W.Records(base.src_ip[idx], base.dst_ip[idx], nbytes, base.meta[idx], base.ports[idx],
+                     base.dns_id[idx])
+    reps = 10_000_000
+    v = LocalDense(W.LOCAL_FWD_DROP, pods.endpoints)
+    v.add(four)
+    want = {k: x * reps for k, x in v.series().items()}
+    dev = torch.device("cuda", gpu_device)
+    cols = [torch.from_numpy(np.tile(a, reps).view(np.int32)).to(dev)
+            for a in (four.src_ip, four.dst_ip, four.bytes, four.meta, four.ports, four.dns_id)]
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, gpu_device, flags=flags)
+    g.submit_device(GpuAgg.device_columns(*cols), 4 * reps)
+    got = g.snapshot()
+    g.close()
+    assert got == want, diff_series(got, want)
