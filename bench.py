@@ -91,7 +91,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from retina_amd import GpuAgg
+    from retina_amd import GpuAgg, _abi
     from retina_amd import workloads as W
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -192,7 +192,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "aggregate_kernel",
+            "kernel": _abi.KERNEL_NAMES.get(int(stats["last_kernel"])),
             "kernel_ms": kernel_ms,
             "other_kernels_ms": fold_ms,
             "bytes_per_record": BYTES_PER_RECORD,

@@ -224,9 +224,15 @@ typedef struct gpuagg_stats {
   uint64_t sparse_entries;   /* occupied group-by table entries (at last sync)   */
   uint64_t sparse_dropped;   /* updates lost to a full group-by table            */
   uint64_t kernel_launches;  /* timed aggregation launches                       */
-  double kernel_ms;          /* summed device time of aggregate_kernel (HIP events)  */
+  double kernel_ms;          /* summed device time of the aggregation kernel (HIP events) */
   double fold_ms;            /* summed device time of the spill fold kernel          */
+  uint32_t last_kernel;      /* kernel of the last launch: GPUAGG_KERNEL_*           */
 } gpuagg_stats;
+
+#define GPUAGG_KERNEL_NONE 0u          /* nothing launched yet                        */
+#define GPUAGG_KERNEL_GENERIC 1u       /* aggregate_kernel: any plan                  */
+#define GPUAGG_KERNEL_DENSE_HBM_IP 2u  /* dense_local_kernel: IP table in HBM         */
+#define GPUAGG_KERNEL_DENSE_LDS_IP 3u  /* dense_lds_kernel: IP table + u32 bins in LDS */
 
 int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
 /* Enables HIP-event timing of the aggregation kernel on the ctx's stream. */

@@ -58,7 +58,10 @@ class StateDesc(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("batches", C.c_uint64), ("sparse_entries", C.c_uint64),
                 ("sparse_dropped", C.c_uint64), ("kernel_launches", C.c_uint64),
-                ("kernel_ms", C.c_double), ("fold_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("fold_ms", C.c_double), ("last_kernel", C.c_uint32)]
+
+
+KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel"}
 
 
 # (name, restype, argtypes) for every entry point declared in include/gpuagg.h

@@ -134,28 +134,46 @@ GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) {
 // LDS layout: bins [0, L), 64 per-lane dummy words [L, L+64) that absorb predicated-
 // off updates, then 16 u32 spill-window counters.
 constexpr uint32_t kLdsBytes = 160 * 1024;
-constexpr uint32_t kLdsExtraWords = 64 + 8;  // 64 dummies + 16 u32 spill-window counters
+constexpr uint32_t kMaxSpillWindows = 32;
+constexpr uint32_t kLdsExtraWords = 64 + kMaxSpillWindows / 2;  // 64 dummies + u32 spill-window counters
 constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
 constexpr uint32_t kLdsCountShift = 44;
 constexpr uint32_t kLdsByteLimit = 1u << 24;
 constexpr uint64_t kLdsCountOne = 1ULL << kLdsCountShift;
 constexpr uint64_t kLdsBytesMask = kLdsCountOne - 1;
 constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^20, multiple of 4
-constexpr uint32_t kMaxSpillWindows = 16;
+// fold windows: 2^14 u64 bins (128 KiB of LDS) so a spilled bin's window is a shift
+constexpr uint32_t kFoldWindowShift = 14, kFoldWindowBins = 1u << kFoldWindowShift;
 
 // ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------
-// Bucketized cuckoo: 2 candidate buckets of 4 keys (16 B, one ds_read_b128 each),
+// Bucketized cuckoo: 2 candidate buckets of 2 keys (8 B, one ds_read_b64 each),
 // keys u32 (0xFFFFFFFF = empty), values u16 slot ids in a parallel array.  Only built
 // for pods that are not the apiserver pseudo pod: in local context such an endpoint is
 // treated exactly like "no endpoint" (types.go:407-413).
-constexpr uint32_t kIplWays = 4;
+constexpr uint32_t kIplWays = 2;  // 2 choices x 2-way buckets: one ds_read_b64 per choice
 constexpr uint32_t kIplEmptyKey = 0xFFFFFFFFu;
 constexpr uint32_t kIplNoSlot = 0xFFFFu;
 constexpr uint32_t kIplMaxBytes = 112 * 1024;
-GA_HD uint32_t ipl_bucket(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)h * nb) >> 32); }
-GA_HD uint32_t ipl_image_bytes(uint32_t nb) {  // keys, then u16 values, 16-byte aligned
-  return nb * kIplWays * 4 + ((nb * kIplWays * 2 + 15) & ~15u);
+constexpr uint32_t kIplMaxBuckets = 1u << 16;  // bucket math uses 24-bit multiplies
+// 24-bit multiplies are full rate on CDNA (32-bit ones are quarter rate)
+GA_HD uint32_t mul_u24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+GA_HD uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
 }
+// Both bucket choices of an IP (nb < 2^16).  The fold x ^ x>>12 brings the high byte,
+// which varies most in little-endian pod IPs, into the multiplied 24 bits.
+GA_HD void ipl_buckets(uint32_t ip, uint32_t seed, uint32_t nb, uint32_t &b1, uint32_t &b2) {
+  uint32_t x = ip ^ seed;
+  x ^= x >> 12;
+  const uint32_t h1 = mul_u24(x, 0x9E3779u);
+  const uint32_t h2 = mul_u24(x ^ (x >> 7), 0xC2B2AFu);
+  b1 = mulhi_u24(h1 >> 8, nb << 8);  // = (h1>>8) * nb >> 24
+  b2 = mulhi_u24(h2 >> 8, nb << 8);
+}
+GA_HD uint32_t ipl_image_bytes(uint32_t nb) {  // keys, then u16 values, 16-byte aligned
+  return ((nb * kIplWays * 4 + 15) & ~15u) + ((nb * kIplWays * 2 + 15) & ~15u);
+}
+GA_HD uint32_t ipl_vals_offset(uint32_t nb) { return (nb * kIplWays * 4 + 15) & ~15u; }
 // 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
 // correct the rare carry / wrap exactly with global atomics; count-only families
 // (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).

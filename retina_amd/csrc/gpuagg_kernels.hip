@@ -58,10 +58,10 @@ struct KArgs {
   DevSparse s;
   DevSketch sk;
   uint32_t lds_bins;  // L: dense bins privatised in LDS (u64 words; tier-1: u32 words)
-  // spill lists: per workgroup, one list per fold window of `win_bins` bins starting at
+  // spill lists: per workgroup, one list per fold window of 2^win_shift bins starting at
   // dense bin `spill_lo`; list (b, w) at spill + (b*nwin + w)*spill_cap
   uint32_t spill_cap;
-  uint32_t nwin, win_bins, spill_lo;
+  uint32_t nwin, win_shift, spill_lo;
   unsigned long long *spill;  // or null: bins >= lds_bins use global atomics
   uint32_t *spill_count;      // [gridDim.x * nwin]
   // tier-1: LDS image of the IP table
@@ -150,15 +150,15 @@ struct DenseSink {
   uint32_t L;
   unsigned int *ctr;        // per-window spill counters (LDS)
   unsigned long long *spill;
-  uint32_t spill_cap, win_bins, spill_lo;
+  uint32_t spill_cap, win_shift, spill_lo;
   DevDense d;
 
   __device__ __forceinline__ void spill_add(uint32_t bin, uint32_t nbytes) const {
     if (spill) {
-      const uint32_t w = (bin - spill_lo) / win_bins;
+      const uint32_t w = (bin - spill_lo) >> win_shift;
       const unsigned int pos = atomicAdd(&ctr[w], 1u);
-      if (pos < spill_cap) {
-        spill[(size_t)w * spill_cap + pos] = ((unsigned long long)bin << 32) | nbytes;
+      if (pos < spill_cap) {  // w < 16 and spill_cap < 2^24: 24-bit multiply
+        spill[mul_u24(w, spill_cap) + pos] = ((unsigned long long)bin << 32) | nbytes;
         return;
       }
     }
@@ -180,7 +180,7 @@ __device__ __forceinline__ DenseSink make_sink(const KArgs &a, unsigned long lon
                                                unsigned int *ctr) {
   return DenseSink{lds, L, ctr,
                    a.spill ? a.spill + (size_t)blockIdx.x * a.nwin * a.spill_cap : nullptr,
-                   a.spill_cap, a.win_bins, a.spill_lo, a.d};
+                   a.spill_cap, a.win_shift, a.spill_lo, a.d};
 }
 
 __device__ __forceinline__ void spill_counts_out(const KArgs &a, const unsigned int *ctr) {
@@ -449,8 +449,9 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
       const uint32_t f = fam[g];
       if (f == FAM_COUNT) continue;
       const uint32_t kd = keyed[g] ? (uint32_t)ld.slot : 0u, ks = keyed[g] ? (uint32_t)ls.slot : 0u;
-      const uint32_t row_d = base[g] + (kd * 2u) * nsub[g];        // side 0: ingress (dst)
-      const uint32_t row_s = base[g] + (ks * 2u + 1u) * nsub[g];   // side 1: egress (src)
+      // slots < 2^16, nsub <= 64: 24-bit multiplies (full rate)
+      const uint32_t row_d = base[g] + mul_u24(kd * 2u, nsub[g]);        // side 0: ingress (dst)
+      const uint32_t row_s = base[g] + mul_u24(ks * 2u + 1u, nsub[g]);   // side 1: egress (src)
       if (f == FAM_TCPFLAGS) {
         uint32_t m = flagmask;
         if (inl[g]) {
@@ -494,19 +495,25 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
 }
 
 // ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
-// Lookup in the LDS cuckoo image: two 16-byte bucket reads, 8 compares, one u16 read.
-__device__ __forceinline__ uint32_t ipl_key_index(uint32_t ip, uint32_t b1, uint32_t b2,
-                                                  const uint4 &k1, const uint4 &k2) {
+// Probe of the LDS cuckoo image: two 8-byte bucket reads and 4 compares give the index
+// of the matching key (or ~0u); the u16 slot id is read separately so all key reads of
+// a thread's records can be in flight together.
+__device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32_t nb, uint32_t seed,
+                                                    uint32_t ip) {
+  uint32_t b1, b2;
+  ipl_buckets(ip, seed, nb, b1, b2);
+  const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
   uint32_t j = 0xFFFFFFFFu;
-  j = k1.x == ip ? b1 * 4 + 0 : j;
-  j = k1.y == ip ? b1 * 4 + 1 : j;
-  j = k1.z == ip ? b1 * 4 + 2 : j;
-  j = k1.w == ip ? b1 * 4 + 3 : j;
-  j = k2.x == ip ? b2 * 4 + 0 : j;
-  j = k2.y == ip ? b2 * 4 + 1 : j;
-  j = k2.z == ip ? b2 * 4 + 2 : j;
-  j = k2.w == ip ? b2 * 4 + 3 : j;
+  j = k1.x == ip ? b1 * 2 : j;
+  j = k1.y == ip ? b1 * 2 + 1 : j;
+  j = k2.x == ip ? b2 * 2 : j;
+  j = k2.y == ip ? b2 * 2 + 1 : j;
   return j;
+}
+
+__device__ __forceinline__ int32_t ipl_slot(const uint16_t *vals, uint32_t j) {
+  const uint32_t v = vals[j == 0xFFFFFFFFu ? 0u : j];  // unconditional read: no branch
+  return (j == 0xFFFFFFFFu || v == kIplNoSlot) ? -1 : (int32_t)v;
 }
 
 struct L4Ctx {
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nb = a.ipl_nb;
   const uint32_t *keys = (const uint32_t *)smem;
-  const uint16_t *vals = (const uint16_t *)(smem + (size_t)nb * 16);
+  const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
   uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
   const uint32_t L4 = a.lds_bins;
   for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
@@ -573,8 +580,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       const uint32_t f = fam[g];
       if (f == FAM_COUNT) continue;
       const uint32_t kd = keyed[g] ? (uint32_t)sd : 0u, ks = keyed[g] ? (uint32_t)ss : 0u;
-      const uint32_t row_d = base[g] + (kd * 2u) * nsub[g];
-      const uint32_t row_s = base[g] + (ks * 2u + 1u) * nsub[g];
+      const uint32_t row_d = base[g] + mul_u24(kd * 2u, nsub[g]);
+      const uint32_t row_s = base[g] + mul_u24(ks * 2u + 1u, nsub[g]);
       if (f == FAM_TCPFLAGS) {
         uint32_t m = flagmask;
         if (inl[g]) {
@@ -614,14 +621,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       }
     }
   };
-  auto find = [&](uint32_t ip) -> uint32_t {  // slot id or kIplNoSlot
-    const uint32_t b1 = ipl_bucket(ip_h1(ip, a.ipl_seed), nb), b2 = ipl_bucket(ip_h2(ip, a.ipl_seed), nb);
-    const uint4 k1 = *(const uint4 *)&keys[b1 * 4], k2 = *(const uint4 *)&keys[b2 * 4];
-    const uint32_t j = ipl_key_index(ip, b1, b2, k1, k2);
-    return j == 0xFFFFFFFFu ? kIplNoSlot : (uint32_t)vals[j];
-  };
-  auto slot_of = [](uint32_t v) { return v == kIplNoSlot ? -1 : (int32_t)v; };
-
+  const uint32_t seed = a.ipl_seed;
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
   uint64_t tail = start;
@@ -632,20 +632,27 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
       const uint64_t v = i >> 2;
       const uint4 vs = s4[v], vd = d4[v], vb = b4[v], vm = m4[v];
-      uint32_t f0 = find(vs.x), f1 = find(vs.y), f2 = find(vs.z), f3 = find(vs.w);
-      uint32_t g0 = find(vd.x), g1 = find(vd.y), g2 = find(vd.z), g3 = find(vd.w);
+      const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
+      uint32_t j[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
+      int32_t sl[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
+      int32_t s0 = sl[0], s1 = sl[1], s2 = sl[2], s3 = sl[3], d0 = sl[4], d1 = sl[5], d2 = sl[6], d3 = sl[7];
       uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
-        record(b0, m0, slot_of(f0), slot_of(g0));
+        record(b0, m0, s0, d0);
         b0 = b1; b1 = b2; b2 = b3; m0 = m1; m1 = m2; m2 = m3;
-        f0 = f1; f1 = f2; f2 = f3; g0 = g1; g1 = g2; g2 = g3;
+        s0 = s1; s1 = s2; s2 = s3; d0 = d1; d1 = d2; d2 = d3;
       }
     }
     tail = vend;
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x)
-    record(a.c.bytes[i], a.c.meta[i], slot_of(find(a.c.src[i])), slot_of(find(a.c.dst[i])));
+    record(a.c.bytes[i], a.c.meta[i], ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i])),
+           ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i])));
 
   __syncthreads();
   // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
@@ -768,7 +775,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.spill = (unsigned long long *)a.spill;
   k.spill_cap = a.spill_cap;
   k.nwin = a.nwin;
-  k.win_bins = a.win_bins;
+  k.win_shift = a.win_shift;
   k.spill_lo = a.spill_lo;
   k.spill_count = a.spill_count;
   k.ipl = a.ipl;
@@ -812,9 +819,9 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)a.win_bins * 8, st,
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 << a.win_shift, st,
                      (const unsigned long long *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.spill_lo, a.dense_len, a.win_bins, a.nwin, k.d);
+                     a.spill_lo, a.dense_len, 1u << a.win_shift, a.nwin, k.d);
   return hipGetLastError();
 }
 

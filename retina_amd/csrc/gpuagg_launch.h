@@ -40,7 +40,7 @@ struct LaunchArgs {
   uint64_t *spill;      // per-workgroup spill lists, or null
   uint32_t spill_cap;
   uint32_t *spill_count;
-  uint32_t win_bins, nwin, win_blocks;
+  uint32_t win_shift, nwin, win_blocks;  // fold windows of 2^win_shift bins
   uint32_t spill_lo;    // first spilled dense bin (fold windows start here)
   uint32_t dense_ng;    // 0: generic kernel; 1/2/4/8: dense local-context kernel
   bool tier1;           // dense kernel with the IP table and u32 bins in LDS

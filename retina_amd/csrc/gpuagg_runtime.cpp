@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "gpuagg_internal.h"
+#include "ipl_build.h"
 #include "gpuagg_launch.h"
 
 using namespace gpuagg;
@@ -373,8 +374,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.tier1 = false;
   if (a.dense_ng && c->ipl_bytes && !spans.empty() &&
       c->ipl_bytes + kL4ExtraBytes < kLdsBytes) {
+    // (with no group in LDS every update spills, but the IP probes still stay on-chip)
     const uint32_t L4 = prefix((kLdsBytes - c->ipl_bytes - kL4ExtraBytes) / 4);
-    if (L4 > 0) {
+    {
       a.tier1 = true;
       a.lds_bins = L4;
       a.ipl = c->d_ipl;
@@ -383,8 +385,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.ipl_bytes = c->ipl_bytes;
     }
   }
-  a.blocks = a.lds_bins ? c->n_cu : c->n_cu * 4;
-  a.threads = a.lds_bins ? 1024 : 256;
+  a.blocks = (a.lds_bins || a.tier1) ? c->n_cu : c->n_cu * 4;
+  a.threads = (a.lds_bins || a.tier1) ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
   for (uint64_t off = 0; off < n; off += per_launch) {
     const uint64_t m = std::min<uint64_t>(per_launch, n - off);
@@ -402,9 +404,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     if (c->dense_len > a.lds_bins) {
       // bins past the LDS window: per-workgroup spill lists bucketed by fold window
       const uint64_t rem = c->dense_len - a.lds_bins;
-      const uint32_t nwin = (uint32_t)((rem + kLdsMaxBins - 1) / kLdsMaxBins);
+      const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
       const uint64_t cap = 2 * a.chunk / nwin + 4096;  // overflow falls back to global atomics
-      if (nwin <= kMaxSpillWindows && cap < 0xFFFFFFFFull) {
+      if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
         a.spill_cap = (uint32_t)cap;
         const size_t need = (size_t)a.blocks * nwin * a.spill_cap;
         if (need > c->spill_alloc) {
@@ -423,7 +425,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         a.spill_count = c->d_spill_count;
         a.nwin = nwin;
         a.spill_lo = a.lds_bins;
-        a.win_bins = (uint32_t)((rem + nwin - 1) / nwin);
+        a.win_shift = kFoldWindowShift;
         a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
       }
     }
@@ -440,6 +442,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   }
   c->stats.records += n;
   c->stats.batches += 1;
+  c->stats.last_kernel = a.tier1 ? GPUAGG_KERNEL_DENSE_LDS_IP
+                         : a.dense_ng ? GPUAGG_KERNEL_DENSE_HBM_IP : GPUAGG_KERNEL_GENERIC;
   return GPUAGG_OK;
 }
 
@@ -796,75 +800,21 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   c->ipl_bytes = 0;
   if (!(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
     std::vector<std::pair<uint32_t, uint32_t>> ents;
-    bool fits = true;
-    for (const auto &kv : last) {
-      const uint32_t sl = (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1));
-      if ((kv.second >> 53) & 1) continue;
-      if (sl >= kIplNoSlot) fits = false;
-      ents.emplace_back(kv.first, sl);
-    }
-    uint32_t nb = std::max<uint32_t>(1, (uint32_t)((ents.size() * 100 + 85 * kIplWays - 1) / (85 * kIplWays)));
-    std::vector<uint32_t> keys;
-    std::vector<uint16_t> vals;
-    uint32_t iseed = 0x6A09E667u;
-    bool built = false;
-    for (int attempt = 0; fits && attempt < 64 && ipl_image_bytes(nb) <= kIplMaxBytes; ++attempt) {
-      if (attempt && attempt % 8 == 0) nb = nb + nb / 16 + 1;
-      iseed = (uint32_t)fmix64((uint64_t)iseed + 0xBB67AE8584CAA73BULL * (attempt + 1));
-      keys.assign((size_t)nb * kIplWays, kIplEmptyKey);
-      vals.assign((size_t)nb * kIplWays, (uint16_t)kIplNoSlot);
-      bool ok = true;
-      uint64_t rng = iseed | 1;
-      for (const auto &e : ents) {
-        uint32_t k = e.first;
-        uint16_t v = (uint16_t)e.second;
-        uint32_t b = ipl_bucket(ip_h1(k, iseed), nb);
-        int kicks = 0;
-        for (;;) {
-          const uint32_t b1 = ipl_bucket(ip_h1(k, iseed), nb), b2 = ipl_bucket(ip_h2(k, iseed), nb);
-          int slot = -1;
-          for (uint32_t bb : {b1, b2}) {
-            for (uint32_t w = 0; w < kIplWays && slot < 0; ++w)
-              if (keys[(size_t)bb * kIplWays + w] == kIplEmptyKey) slot = (int)(bb * kIplWays + w);
-            if (slot >= 0) break;
-          }
-          if (slot >= 0) {
-            keys[slot] = k;
-            vals[slot] = v;
-            break;
-          }
-          if (++kicks > 1000) {
-            ok = false;
-            break;
-          }
-          // evict a random resident of the bucket not used last time
-          b = (b == b1) ? b2 : b1;
-          rng ^= rng << 13, rng ^= rng >> 7, rng ^= rng << 17;
-          const size_t victim = (size_t)b * kIplWays + (rng % kIplWays);
-          std::swap(k, keys[victim]);
-          std::swap(v, vals[victim]);
-        }
-        if (!ok) break;
-      }
-      if (ok) {
-        built = true;
-        break;
-      }
-    }
-    if (built) {
-      const uint32_t bytes = ipl_image_bytes(nb);
-      std::vector<uint8_t> img(bytes, 0);
-      memcpy(img.data(), keys.data(), keys.size() * 4);
-      memcpy(img.data() + keys.size() * 4, vals.data(), vals.size() * 2);
+    for (const auto &kv : last)
+      if (!((kv.second >> 53) & 1))
+        ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
+    IplImage im;
+    if (ipl_build(ents, &im)) {
+      const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
       }
-      HIPCHK(c, hipMemcpy(c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
-      c->ipl_nb = nb;
-      c->ipl_seed = iseed;
+      HIPCHK(c, hipMemcpy(c->d_ipl, im.bytes.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_nb = im.nb;
+      c->ipl_seed = im.seed;
       c->ipl_bytes = bytes;
     }
   }

@@ -1,0 +1,93 @@
+// Host builder of the LDS-resident IP table image used by the tier-1 dense kernel
+// (gpuagg_internal.h, "LDS-resident IP table").  Header-only so that a host-only test
+// (tests/ipl_build_test.cpp) exercises exactly the code the runtime runs.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "gpuagg_internal.h"
+
+namespace gpuagg {
+
+struct IplImage {
+  uint32_t nb = 0, seed = 0;
+  std::vector<uint8_t> bytes;  // ipl_image_bytes(nb): keys u32[nb*2], then vals u16[nb*2]
+};
+
+// (ip, slot) entries with distinct IPs.  Returns false when the set cannot be imaged
+// (a slot >= 0xFFFF, the key 0xFFFFFFFF, or no cuckoo placement within kIplMaxBytes);
+// the caller then keeps the IP table in HBM.
+inline bool ipl_build(const std::vector<std::pair<uint32_t, uint32_t>> &ents, IplImage *out,
+                      uint32_t load_pct = 88) {
+  for (const auto &e : ents)
+    if (e.second >= kIplNoSlot || e.first == kIplEmptyKey) return false;
+  uint32_t nb = (uint32_t)((ents.size() * 100 + load_pct * kIplWays - 1) / (load_pct * kIplWays));
+  if (nb == 0) nb = 1;
+  std::vector<uint32_t> keys;
+  std::vector<uint16_t> vals;
+  uint32_t seed = 0x6A09E667u;
+  for (int attempt = 0; attempt < 96; ++attempt) {
+    if (attempt && attempt % 8 == 0) nb = nb + nb / 16 + 1;
+    if (nb >= kIplMaxBuckets || ipl_image_bytes(nb) > kIplMaxBytes) return false;
+    seed = (uint32_t)fmix64((uint64_t)seed + 0xBB67AE8584CAA73BULL * (uint64_t)(attempt + 1));
+    keys.assign((size_t)nb * kIplWays, kIplEmptyKey);
+    vals.assign((size_t)nb * kIplWays, (uint16_t)kIplNoSlot);
+    bool ok = true;
+    uint64_t rng = seed | 1ULL;
+    for (const auto &e : ents) {
+      uint32_t k = e.first;
+      uint16_t v = (uint16_t)e.second;
+      uint32_t b1, b2;
+      ipl_buckets(k, seed, nb, b1, b2);
+      uint32_t b = b1;
+      for (int kicks = 0;; ++kicks) {
+        ipl_buckets(k, seed, nb, b1, b2);
+        int slot = -1;
+        for (uint32_t bb : {b1, b2}) {
+          for (uint32_t w = 0; w < kIplWays && slot < 0; ++w)
+            if (keys[(size_t)bb * kIplWays + w] == kIplEmptyKey) slot = (int)(bb * kIplWays + w);
+          if (slot >= 0) break;
+        }
+        if (slot >= 0) {
+          keys[slot] = k;
+          vals[slot] = v;
+          break;
+        }
+        if (kicks >= 2000) {
+          ok = false;
+          break;
+        }
+        // random walk: evict a random resident of the bucket not used last time
+        b = (b == b1) ? b2 : b1;
+        rng ^= rng << 13, rng ^= rng >> 7, rng ^= rng << 17;
+        const size_t victim = (size_t)b * kIplWays + (uint32_t)(rng % kIplWays);
+        std::swap(k, keys[victim]);
+        std::swap(v, vals[victim]);
+      }
+      if (!ok) break;
+    }
+    if (!ok) continue;
+    out->nb = nb;
+    out->seed = seed;
+    out->bytes.assign(ipl_image_bytes(nb), 0);
+    memcpy(out->bytes.data(), keys.data(), keys.size() * 4);
+    memcpy(out->bytes.data() + ipl_vals_offset(nb), vals.data(), vals.size() * 2);
+    return true;
+  }
+  return false;
+}
+
+// Host mirror of the kernel's probe (dense_lds_kernel): slot or kIplNoSlot.
+inline uint32_t ipl_probe(const uint8_t *img, uint32_t nb, uint32_t seed, uint32_t ip) {
+  uint32_t b1, b2;
+  ipl_buckets(ip, seed, nb, b1, b2);
+  const uint32_t *keys = (const uint32_t *)img;
+  const uint16_t *vals = (const uint16_t *)(img + ipl_vals_offset(nb));
+  for (uint32_t j : {b1 * 2, b1 * 2 + 1, b2 * 2, b2 * 2 + 1})
+    if (keys[j] == ip) return vals[j];
+  return kIplNoSlot;
+}
+
+}  // namespace gpuagg

@@ -45,11 +45,13 @@ for s in $STEPS; do
                  "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i+1))
         timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d "$OUT/${TAG}_pmc$i" -o run \
-          -- python3 "$R/bench.py" --records 20000000 --steps 2 --warmup 1 --no-cpu-baseline \
+          -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
           > "$OUT/${TAG}_pmc$i.log" 2>&1
         rc=$?; echo "pmc$i rc=$rc" >> "$OUT/${TAG}_pmc$i.log"
         [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
-      done ;;
+      done
+      python scripts/pmc_summary.py "$OUT/${TAG}_pmc_c2.json" dense_ 100000000 "$OUT/${TAG}_pmc4" "$OUT/${TAG}_pmc5" \
+        > /dev/null 2>> "$OUT/${TAG}_pmc5.log" ;;
   esac
 done
 exit 0

@@ -1,0 +1,66 @@
+"""The LDS IP-table builder (retina_amd/csrc/ipl_build.h), compiled host-only with g++:
+every endpoint IP is found with its slot by the host mirror of the kernel probe, absent
+IPs miss, and pod-IP sets up to the C2 size (10k pods, ~10.5k IPs) fit the image budget."""
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from retina_amd import workloads as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("ipl") / "ipl_build_test")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "retina_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "ipl_build_test.cpp"), "-o", exe], check=True)
+    return exe
+
+
+def run_sets(exe, sets):
+    lines = [str(len(sets))]
+    for ents in sets:
+        lines.append(str(len(ents)))
+        lines.extend("%d %d" % (ip, sl) for ip, sl in ents)
+    out = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                         check=True).stdout.split("\n")
+    res = []
+    for ln in out:
+        if ln.strip():
+            built, nb, seed, nbytes, load, found, absent = ln.split()
+            res.append(dict(built=int(built), nb=int(nb), bytes=int(nbytes), load=float(load),
+                            found=int(found), absent=int(absent)))
+    return res
+
+
+def pod_sets():
+    sets = []
+    for npods in (1, 7, 400, 2_000, 10_000):
+        p = W.make_pods(npods, seed=npods)
+        sets.append([(int(ip), int(o)) for ip, o in zip(p.ips, p.ip_owner)])
+    rng = np.random.default_rng(5)
+    ips = np.unique(rng.integers(0, 2**32 - 1, 12_000, dtype=np.uint64)).astype(np.uint32)
+    sets.append([(int(ip), i % 60_000) for i, ip in enumerate(ips)])           # random IPs
+    sets.append([(0x0A000000 + i, i) for i in range(9_000)])                    # sequential BE
+    return sets
+
+
+def test_builder_finds_every_key(harness):
+    sets = pod_sets()
+    for ents, r in zip(sets, run_sets(harness, sets)):
+        assert r["built"] == 1, (len(ents), r)
+        assert r["found"] == len(ents)
+        assert r["absent"] > 99_000
+        assert r["bytes"] <= 112 * 1024
+
+
+def test_builder_refuses_unimageable(harness):
+    too_many = [(0x0A000000 + i, i % 1000) for i in range(40_000)]   # > image budget
+    bad_slot = [(1, 0xFFFF)]                                         # slot id reserved
+    bad_key = [(0xFFFFFFFF, 3)]                                      # empty-key marker
+    r = run_sets(harness, [too_many, bad_slot, bad_key])
+    assert [x["built"] for x in r] == [0, 0, 0]
