@@ -625,13 +625,23 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
   uint64_t tail = start;
-  if (kVec && start < end) {
-    const uint64_t vend = start + ((end - start) & ~3ULL);
+  if (kVec && start + 4 <= end) {
+    // 4 records per thread per step; the next step's 64 bytes are loaded before this
+    // step's probes and updates run, so HBM reads stay in flight during the LDS work
+    const uint64_t v0 = start >> 2, vn = (end - start) >> 2, vend = v0 + vn;
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
-    for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
-      const uint64_t v = i >> 2;
-      const uint4 vs = s4[v], vd = d4[v], vb = b4[v], vm = m4[v];
+    uint64_t v = v0 + threadIdx.x;
+    const uint64_t vlast = vend - 1;  // vn >= 1
+    uint64_t vl = v < vend ? v : vlast;
+    uint4 ns = s4[vl], nd = d4[vl], nbv = b4[vl], nm = m4[vl];
+    for (; v < vend; v += blockDim.x) {
+      const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
+      vl = v + blockDim.x < vend ? v + blockDim.x : vlast;  // clamped: no branch
+      ns = s4[vl];
+      nd = d4[vl];
+      nbv = b4[vl];
+      nm = m4[vl];
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t j[8];
 #pragma unroll
@@ -648,7 +658,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
         s0 = s1; s1 = s2; s2 = s3; d0 = d1; d1 = d2; d2 = d3;
       }
     }
-    tail = vend;
+    tail = start + (vn << 2);
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x)
     record(a.c.bytes[i], a.c.meta[i], ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i])),
@@ -692,13 +702,39 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
   __syncthreads();
+  // fewer than 2^20 entries into this window copy: no packed field can overflow, so
+  // plain (no-return) LDS atomics suffice; otherwise the exact carrying add
+  uint64_t total = 0;
+  for (uint32_t l = part; l < n_lists; l += nparts) total += spill_count[(size_t)l * nwin + w];
+  const bool fast = total < (1ULL << 20);
   for (uint32_t l = part; l < n_lists; l += nparts) {
     const uint32_t cnt = spill_count[(size_t)l * nwin + w];
     const unsigned long long *e = spill + ((size_t)l * nwin + w) * spill_cap;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-      const unsigned long long v = e[j];
-      const uint32_t bin = (uint32_t)(v >> 32);
-      lds_add64_exact(&win[bin - lo], bin, (uint32_t)v, d);
+    if (fast) {
+      uint32_t j = threadIdx.x;
+      for (; j + 3 * blockDim.x < cnt; j += 4 * blockDim.x) {
+        unsigned long long v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = e[j + k * blockDim.x];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t bin = (uint32_t)(v[k] >> 32), nb = (uint32_t)v[k];
+          atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
+          if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+        }
+      }
+      for (; j < cnt; j += blockDim.x) {
+        const unsigned long long v = e[j];
+        const uint32_t bin = (uint32_t)(v >> 32), nb = (uint32_t)v;
+        atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
+        if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+      }
+    } else {
+      for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        const unsigned long long v = e[j];
+        const uint32_t bin = (uint32_t)(v >> 32);
+        lds_add64_exact(&win[bin - lo], bin, (uint32_t)v, d);
+      }
     }
   }
   __syncthreads();

@@ -75,9 +75,10 @@ def test_host_fed_equals_device_and_chunking(gpu_device):
 @pytest.mark.parametrize("flags", [0, 1], ids=["tier1", "no-lds-ip-table"])
 def test_packed_field_overflow_exact(gpu_device, flags):
     """Packed LDS counters (u32 count:12|bytes:20 in tier-1, u64 count:20|bytes:44 in the
-    fold windows) must carry exactly.  One hot pod pair, 40M records: every LDS count field
-    wraps many times and byte fields carry; forward bins live in LDS, drop bins are
-    spilled and folded (10k pods).  Expected = a 4-record batch x 10M (linearity)."""
+    other kernels and the fold windows) must carry exactly.  One hot pod pair, 60M
+    records: LDS count fields wrap many times, byte fields carry, packets >= 2^20 / 2^24
+    bytes take the global path, and the hot drop bins overflow their spill lists into
+    global atomics.  Expected = a 10-record batch x 6M (linearity)."""
     import torch
     from retina_amd import GpuAgg
     pods = W.make_pods(10_000, seed=5)
@@ -86,19 +87,21 @@ def test_packed_field_overflow_exact(gpu_device, flags):
     ok = (base.src_ip != base.dst_ip)
     f = int(np.flatnonzero((verdict == W.V_FWD) & ok)[0])
     d = int(np.flatnonzero((verdict == W.V_DROP) & ok)[0])
-    idx = np.array([f, f, d, f])
-    nbytes = np.array([1_000_000, 5_000_000, 8_400_000, (1 << 20) - 1], np.uint32)
-    four = W.Records(base.src_ip[idx], base.dst_ip[idx], nbytes, base.meta[idx], base.ports[idx],
-                     base.dns_id[idx])
-    reps = 10_000_000
+    idx = np.array([f, f, f] + [d] * 7)
+    nbytes = np.array([1_000_000, (1 << 20) - 1, 5_000_000] + [(1 << 24) - 1] * 6 + [20_000_000],
+                      np.uint32)
+    ten = W.Records(base.src_ip[idx], base.dst_ip[idx], nbytes, base.meta[idx], base.ports[idx],
+                    base.dns_id[idx])
+    reps = 6_000_000
     v = LocalDense(W.LOCAL_FWD_DROP, pods.endpoints)
-    v.add(four)
+    v.add(ten)
     want = {k: x * reps for k, x in v.series().items()}
     dev = torch.device("cuda", gpu_device)
     cols = [torch.from_numpy(np.tile(a, reps).view(np.int32)).to(dev)
-            for a in (four.src_ip, four.dst_ip, four.bytes, four.meta, four.ports, four.dns_id)]
+            for a in (ten.src_ip, ten.dst_ip, ten.bytes, ten.meta, ten.ports, ten.dns_id)]
     g = make_engine(pods, W.LOCAL_FWD_DROP, False, gpu_device, flags=flags)
-    g.submit_device(GpuAgg.device_columns(*cols), 4 * reps)
+    g.submit_device(GpuAgg.device_columns(*cols), len(ten) * reps)
     got = g.snapshot()
     g.close()
+    del cols
     assert got == want, diff_series(got, want)
