@@ -153,6 +153,17 @@ struct DenseSink {
   uint32_t spill_cap, win_shift, spill_lo;
   DevDense d;
 
+  __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> win_shift; }
+  // store one reserved spill entry (pos from the window counter); full list -> global
+  __device__ __forceinline__ void spill_put(uint32_t bin, uint32_t w, uint32_t pos, uint32_t nbytes) const {
+    if (pos < spill_cap) {
+      spill[mul_u24(w, spill_cap) + pos] = ((unsigned long long)bin << 32) | nbytes;
+      return;
+    }
+    atomicAdd(&d.cnt[bin], 1ULL);
+    if (nbytes) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
+  }
+
   __device__ __forceinline__ void spill_add(uint32_t bin, uint32_t nbytes) const {
     if (spill) {
       const uint32_t w = (bin - spill_lo) >> win_shift;
@@ -517,30 +528,160 @@ __device__ __forceinline__ int32_t ipl_slot(const uint16_t *vals, uint32_t j) {
 }
 
 struct L4Ctx {
-  uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then 16 spill-window counters
-  uint32_t L4, dummy;
+  uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
+  uint32_t dummy;  // this lane's dummy word: absorbs predicated-off updates
   DevDense d;
-  // bytes families: count:12 | bytes:20, corrected exactly (kL4* in gpuagg_internal.h)
-  __device__ __forceinline__ void add_bytes(bool valid, uint32_t bin, uint32_t nb) const {
-    const bool big = nb >= kL4ByteLimit;
-    const uint32_t b = big ? 0u : nb;
-    const uint32_t old = atomicAdd(&bins[valid ? bin : dummy], (1u << kL4CountShift) | b);
-    if (!valid) return;
-    if (big) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+  // Exact correction after a packed add (count:12 | bytes:20) returned `old`: a carry
+  // out of the bytes field, a wrap of the count field, or a packet too big for the
+  // field is booked into the global counters.  Rare; the test is 3 VALU ops.
+  __device__ __forceinline__ void fix(bool valid, uint32_t old, uint32_t nb, uint32_t bin) const {
+    const uint32_t b = nb < kL4ByteLimit ? nb : 0u;
+    if (!(valid && ((old & kL4BytesMask) + b > kL4BytesMask || old >= 0xFFE00000u ||
+                    nb >= kL4ByteLimit)))
+      return;
+    if (nb >= kL4ByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
     const uint32_t carry = ((old & kL4BytesMask) + b) >> kL4CountShift;
     const uint32_t wrap = ((old >> kL4CountShift) + 1u + carry) >> (32 - kL4CountShift);
-    if (carry | wrap) {
-      if (carry) {
-        atomicAdd(&d.byt[bin], (unsigned long long)kL4ByteLimit);
-        atomicAdd(&d.cnt[bin], ~0ULL);
-      }
-      if (wrap) atomicAdd(&d.cnt[bin], 1ULL << (32 - kL4CountShift));
+    if (carry) {
+      atomicAdd(&d.byt[bin], (unsigned long long)kL4ByteLimit);
+      atomicAdd(&d.cnt[bin], ~0ULL);  // the carry also bumped the count field
     }
-  }
-  __device__ __forceinline__ void add_count(bool valid, uint32_t bin) const {
-    atomicAdd(&bins[valid ? bin : dummy], 1u);
+    if (wrap) atomicAdd(&d.cnt[bin], 1ULL << (32 - kL4CountShift));
   }
 };
+static_assert(kL4CountShift == 20, "fix() thresholds assume count:12 | bytes:20");
+
+// Group descriptors of the dense local-context plan, compile-time indexed (SGPRs).
+template <int NG>
+struct DenseGroups {
+  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  bool inl[NG];
+  bool any_flags;
+  __device__ __forceinline__ DenseGroups(const Plan &p, uint32_t L) {
+    any_flags = false;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      fam[g] = g < p.ngroups ? p.g[g].family : (uint32_t)FAM_COUNT;
+      base[g] = (uint32_t)p.g[g].dense_base;
+      nsub[g] = p.g[g].nsub;
+      keyed[g] = p.g[g].key_mode;
+      inl[g] = base[g] + p.g[g].nbins <= L;
+      any_flags |= fam[g] == FAM_TCPFLAGS;
+    }
+  }
+};
+
+// R records of one thread through every group (tier-1).  Group-outer / record-inner:
+// a group's 2R returning LDS adds are all issued before any result is inspected, so
+// their latency overlaps.  ss/sd: source / destination slot or -1.
+template <int NG, int R>
+__device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx &l4,
+                                           const DenseSink &ds, const uint32_t (&nbytes)[R],
+                                           const uint32_t (&meta)[R], const int32_t (&ss)[R],
+                                           const int32_t (&sd)[R]) {
+  uint32_t verdict[R], reason[R], flagmask[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    verdict[k] = meta_verdict(meta[k]);
+    reason[k] = meta_reason(meta[k]);
+    flagmask[k] = (G.any_flags && verdict[k] == kVerdictForwarded && meta_proto(meta[k]) == 6)
+                      ? flag_label_mask(meta_flags(meta[k])) : 0u;
+  }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const uint32_t f = G.fam[g];
+    if (f == FAM_COUNT) continue;
+    uint32_t rd[R], rs[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // slots < 2^16, nsub <= 64: 24-bit multiplies
+      const uint32_t kd = G.keyed[g] ? (uint32_t)sd[k] : 0u, ks = G.keyed[g] ? (uint32_t)ss[k] : 0u;
+      rd[k] = G.base[g] + mul_u24(kd * 2u, G.nsub[g]);       // side 0: ingress (dst)
+      rs[k] = G.base[g] + mul_u24(ks * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
+    }
+    if (f == FAM_TCPFLAGS) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        uint32_t m = flagmask[k];
+        const bool d_ok = sd[k] >= 0, s_ok = ss[k] >= 0;
+        if (G.inl[g]) {
+          while (__ballot(m != 0)) {
+            const bool v = m != 0;
+            const uint32_t bit = v ? (uint32_t)__builtin_ctz(m) : 0u;
+            atomicAdd(&l4.bins[v && d_ok ? rd[k] + bit : l4.dummy], 1u);
+            atomicAdd(&l4.bins[v && s_ok ? rs[k] + bit : l4.dummy], 1u);
+            m &= m - 1;
+          }
+        } else {
+          for (; m; m &= m - 1) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            if (d_ok) ds.spill_add(rd[k] + bit, 0);
+            if (s_ok) ds.spill_add(rs[k] + bit, 0);
+          }
+        }
+      }
+      continue;
+    }
+    const uint32_t want = f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped
+                                                                          : kVerdictRetrans;
+    bool vd[R], vs[R];
+    uint32_t bd[R], bs[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const bool hit = verdict[k] == want;
+      const uint32_t sub = f == FAM_DROP ? reason[k] : 0u;
+      vd[k] = hit && sd[k] >= 0;
+      vs[k] = hit && ss[k] >= 0;
+      bd[k] = rd[k] + sub;
+      bs[k] = rs[k] + sub;
+    }
+    if (G.inl[g]) {
+      if (f <= FAM_DROP) {
+        uint32_t od[R], os[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const uint32_t add = (1u << kL4CountShift) | (nbytes[k] < kL4ByteLimit ? nbytes[k] : 0u);
+          od[k] = atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], add);
+          os[k] = atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], add);
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          l4.fix(vd[k], od[k], nbytes[k], bd[k]);
+          l4.fix(vs[k], os[k], nbytes[k], bs[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], 1u);
+          atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], 1u);
+        }
+      }
+    } else if (ds.spill) {
+      // spilled group: reserve all 2R list positions first (dummy word for lanes
+      // without an update), then store
+      uint32_t wd[R], ws[R], pd[R], ps[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        wd[k] = ds.window(bd[k]);
+        ws[k] = ds.window(bs[k]);
+        pd[k] = atomicAdd(vd[k] ? &ds.ctr[wd[k]] : &l4.bins[l4.dummy], 1u);
+        ps[k] = atomicAdd(vs[k] ? &ds.ctr[ws[k]] : &l4.bins[l4.dummy], 1u);
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
+        if (vd[k]) ds.spill_put(bd[k], wd[k], pd[k], add_b);
+        if (vs[k]) ds.spill_put(bs[k], ws[k], ps[k], add_b);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
+        if (vd[k]) ds.spill_add(bd[k], add_b);
+        if (vs[k]) ds.spill_add(bs[k], add_b);
+      }
+    }
+  }
+}
 
 template <int NG, bool kVec>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
@@ -555,72 +696,9 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   for (uint32_t i = threadIdx.x; i < L4 + 64 + kMaxSpillWindows; i += blockDim.x) bins[i] = 0u;
   __syncthreads();
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const L4Ctx l4{bins, L4, L4 + lane, a.d};
+  const L4Ctx l4{bins, L4 + lane, a.d};
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
-  const int ng = a.p.ngroups;
-  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
-  bool inl[NG];
-  bool any_flags = false;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    fam[g] = g < ng ? a.p.g[g].family : (uint32_t)FAM_COUNT;
-    base[g] = (uint32_t)a.p.g[g].dense_base;
-    nsub[g] = a.p.g[g].nsub;
-    keyed[g] = a.p.g[g].key_mode;
-    inl[g] = base[g] + a.p.g[g].nbins <= L4;
-    any_flags |= fam[g] == FAM_TCPFLAGS;
-  }
-  auto record = [&](uint32_t nbytes, uint32_t meta, int32_t ss, int32_t sd) {
-    const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
-    const bool s_ok = ss >= 0, d_ok = sd >= 0;  // apiserver IPs are not in the image
-    const uint32_t flagmask = (any_flags && verdict == kVerdictForwarded && proto == 6)
-                                  ? flag_label_mask(meta_flags(meta)) : 0u;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const uint32_t f = fam[g];
-      if (f == FAM_COUNT) continue;
-      const uint32_t kd = keyed[g] ? (uint32_t)sd : 0u, ks = keyed[g] ? (uint32_t)ss : 0u;
-      const uint32_t row_d = base[g] + mul_u24(kd * 2u, nsub[g]);
-      const uint32_t row_s = base[g] + mul_u24(ks * 2u + 1u, nsub[g]);
-      if (f == FAM_TCPFLAGS) {
-        uint32_t m = flagmask;
-        if (inl[g]) {
-          while (__ballot(m != 0)) {
-            const bool v = m != 0;
-            const uint32_t bit = v ? (uint32_t)__builtin_ctz(m) : 0u;
-            l4.add_count(v && d_ok, row_d + bit);
-            l4.add_count(v && s_ok, row_s + bit);
-            m &= m - 1;
-          }
-        } else {
-          for (; m; m &= m - 1) {
-            const uint32_t bit = (uint32_t)__builtin_ctz(m);
-            if (d_ok) ds.spill_add(row_d + bit, 0);
-            if (s_ok) ds.spill_add(row_s + bit, 0);
-          }
-        }
-        continue;
-      }
-      bool hit;
-      if (f == FAM_FWD) hit = verdict == kVerdictForwarded;
-      else if (f == FAM_DROP) hit = verdict == kVerdictDropped;
-      else hit = verdict == kVerdictRetrans;
-      const uint32_t sub = f == FAM_DROP ? reason : 0u;
-      if (inl[g]) {
-        if (f <= FAM_DROP) {
-          l4.add_bytes(hit && d_ok, row_d + sub, nbytes);
-          l4.add_bytes(hit && s_ok, row_s + sub, nbytes);
-        } else {
-          l4.add_count(hit && d_ok, row_d + sub);
-          l4.add_count(hit && s_ok, row_s + sub);
-        }
-      } else if (hit) {
-        const uint32_t add_b = f <= FAM_DROP ? nbytes : 0u;
-        if (d_ok) ds.spill_add(row_d + sub, add_b);
-        if (s_ok) ds.spill_add(row_s + sub, add_b);
-      }
-    }
-  };
+  const DenseGroups<NG> G(a.p, L4);
   const uint32_t seed = a.ipl_seed;
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -649,29 +727,27 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       int32_t sl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
-      int32_t s0 = sl[0], s1 = sl[1], s2 = sl[2], s3 = sl[3], d0 = sl[4], d1 = sl[5], d2 = sl[6], d3 = sl[7];
-      uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
-        record(b0, m0, s0, d0);
-        b0 = b1; b1 = b2; b2 = b3; m0 = m1; m1 = m2; m2 = m3;
-        s0 = s1; s1 = s2; s2 = s3; d0 = d1; d1 = d2; d2 = d3;
-      }
+      const int32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
+      const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
+      l4_records<NG, 4>(G, l4, ds, by, me, ss, sd);
     }
     tail = start + (vn << 2);
   }
-  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x)
-    record(a.c.bytes[i], a.c.meta[i], ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i])),
-           ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i])));
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
+    const int32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
+    const int32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
+    const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
+    l4_records<NG, 1>(G, l4, ds, by, me, ss, sd);
+  }
 
   __syncthreads();
   // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    if (fam[g] == FAM_COUNT || !inl[g]) continue;
-    const bool with_bytes = fam[g] <= FAM_DROP;
-    const uint32_t hi = base[g] + a.p.g[g].nbins;
-    for (uint32_t i = base[g] + threadIdx.x; i < hi; i += blockDim.x) {
+    if (G.fam[g] == FAM_COUNT || !G.inl[g]) continue;
+    const bool with_bytes = G.fam[g] <= FAM_DROP;
+    const uint32_t hi = G.base[g] + a.p.g[g].nbins;
+    for (uint32_t i = G.base[g] + threadIdx.x; i < hi; i += blockDim.x) {
       const uint32_t w = bins[i];
       if (!w) continue;
       if (with_bytes) {
