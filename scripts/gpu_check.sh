@@ -31,6 +31,10 @@ for s in $STEPS; do
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/mb scripts/microbench.hip > "$OUT/${TAG}_micro.err" 2>&1 || exit 1
       timeout -k 10 300 /tmp/mb > "$OUT/${TAG}_micro.jsonl" 2>> "$OUT/${TAG}_micro.err"
       rc=$?; echo "micro rc=$rc" >> "$OUT/${TAG}_micro.err"; [ $rc -ne 0 ] && exit $rc ;;
+    microlds)
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/mbl scripts/microbench_lds.hip > "$OUT/${TAG}_microlds.err" 2>&1 || exit 1
+      timeout -k 10 300 /tmp/mbl > "$OUT/${TAG}_microlds.jsonl" 2>> "$OUT/${TAG}_microlds.err"
+      rc=$?; echo "microlds rc=$rc" >> "$OUT/${TAG}_microlds.err"; [ $rc -ne 0 ] && exit $rc ;;
     ablate)
       timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
       rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;

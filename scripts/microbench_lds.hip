@@ -1,0 +1,174 @@
+// Ceilings for the tier-1 dense kernel's pieces on MI355X (diagnostic; not the product).
+// 100M records, 4 u32 columns, 256 workgroups x 1024 threads, 4 records per thread-step
+// with the next step prefetched.  Modes add one piece at a time:
+//   0 stream          loads only
+//   1 probe           + 8 LDS bucket probes per step (2 x ds_read_b64 + 4 compares each)
+//   2 probe+val       + the u16 slot reads
+//   3 +atomic_rtn     + 2 returning u32 LDS adds per record into 20k bins
+//   4 +atomic_nortn   mode 2 + 2 non-returning u32 LDS adds per record
+//   5 hash-only       loads + bucket hashing, no LDS reads
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/mbl scripts/microbench_lds.hip && /tmp/mbl
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "../retina_amd/csrc/gpuagg_internal.h"
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                       \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+using namespace gpuagg;
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, const uint4 *b4,
+                                             const uint4 *m4, uint64_t nvec, const uint8_t *img,
+                                             uint32_t nb, uint32_t img_bytes, uint32_t nbins,
+                                             unsigned long long *out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t *keys = (const uint32_t *)smem;
+  const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+  uint32_t *bins = (uint32_t *)(smem + img_bytes);
+  for (uint32_t i = threadIdx.x; i < img_bytes / 16; i += blockDim.x) ((uint4 *)smem)[i] = ((const uint4 *)img)[i];
+  for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) bins[i] = 0;
+  __syncthreads();
+  const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  const uint64_t v0 = blockIdx.x * per, vend = v0 + per < nvec ? v0 + per : nvec;
+  uint32_t acc = 0;
+  uint64_t v = v0 + threadIdx.x;
+  const uint64_t vlast = vend - 1;
+  uint64_t vl = v < vend ? v : vlast;
+  uint4 ns = s4[vl], nd = d4[vl], nbv = b4[vl], nm = m4[vl];
+  for (; v < vend; v += blockDim.x) {
+    const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
+    vl = v + blockDim.x < vend ? v + blockDim.x : vlast;
+    ns = s4[vl]; nd = d4[vl]; nbv = b4[vl]; nm = m4[vl];
+    const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
+    if (MODE == 0) {
+      acc += vs.x ^ vs.y ^ vs.z ^ vs.w ^ vd.x ^ vd.y ^ vd.z ^ vd.w ^ vb.x ^ vb.y ^ vb.z ^ vb.w ^ vm.x ^ vm.y ^ vm.z ^ vm.w;
+      continue;
+    }
+    if (MODE == 5) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t b1, b2;
+        ipl_buckets(ip[k], 12345u, nb, b1, b2);
+        acc += b1 ^ b2;
+      }
+      acc += vb.x ^ vm.x;
+      continue;
+    }
+    uint32_t j[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t b1, b2;
+      ipl_buckets(ip[k], 12345u, nb, b1, b2);
+      const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
+      uint32_t jj = 0xFFFFFFFFu;
+      jj = k1.x == ip[k] ? b1 * 2 : jj;
+      jj = k1.y == ip[k] ? b1 * 2 + 1 : jj;
+      jj = k2.x == ip[k] ? b2 * 2 : jj;
+      jj = k2.y == ip[k] ? b2 * 2 + 1 : jj;
+      j[k] = jj;
+    }
+    if (MODE == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += j[k];
+      acc += vb.x ^ vm.x;
+      continue;
+    }
+    uint32_t sl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sl[k] = vals[j[k] == 0xFFFFFFFFu ? 0u : j[k]];
+    if (MODE == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += sl[k];
+      acc += vb.x ^ vm.x;
+      continue;
+    }
+    const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w};
+    uint32_t od[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t add = (1u << 20) | (by[k] & 0xFFFFF);
+      const uint32_t bd = (sl[4 + k] * 2) & 16383u, bs = (sl[k] * 2 + 1) & 16383u;
+      if (MODE == 3) {
+        od[2 * k] = atomicAdd(&bins[bd], add);
+        od[2 * k + 1] = atomicAdd(&bins[bs], add);
+      } else {
+        atomicAdd(&bins[bd], add);
+        atomicAdd(&bins[bs], add);
+      }
+    }
+    if (MODE == 3) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += od[k] >> 31;
+    }
+    acc += vm.x;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) acc += bins[i];
+  atomicAdd(out, (unsigned long long)acc);
+}
+
+__global__ void fill(uint32_t *p, size_t n, uint32_t seed, uint32_t pod_mod) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    p[i] = pod_mod ? (10u | ((x % pod_mod) << 8)) : (x & 0x7FF);
+  }
+}
+
+int main() {
+  const size_t n = 100000000, nvec = n / 4;
+  uint32_t *col[4];
+  for (int i = 0; i < 4; ++i) {
+    CK(hipMalloc(&col[i], n * 4));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, col[i], n, 77u * (i + 1), i < 2 ? 12000u : 0u);
+  }
+  const uint32_t nb = 6000, img_bytes = ipl_image_bytes(nb), nbins = 20032;
+  uint8_t *img;
+  CK(hipMalloc(&img, img_bytes));
+  hipLaunchKernelGGL(fill, dim3(64), dim3(256), 0, 0, (uint32_t *)img, img_bytes / 4, 5u, 12000u);
+  unsigned long long *out;
+  CK(hipMalloc(&out, 8));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const size_t lds = img_bytes + nbins * 4;
+  const char *names[] = {"stream", "probe", "probe+val", "+atomic_rtn", "+atomic_nortn", "hash-only"};
+  for (int mode = 0; mode <= 5; ++mode) {
+    auto launch = [&]() {
+      switch (mode) {
+#define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, out); break;
+        L(0) L(1) L(2) L(3) L(4) L(5)
+#undef L
+      }
+    };
+    switch (mode) {
+#define A(M) case M: CK(hipFuncSetAttribute((const void *)kern<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840)); break;
+      A(0) A(1) A(2) A(3) A(4) A(5)
+#undef A
+    }
+    launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 10; ++r) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 10;
+    printf("{\"mode\": \"%s\", \"ms\": %.4f, \"GBps_16B\": %.1f}\n", names[mode], ms, 16.0 * n / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  }
+  return 0;
+}
