@@ -30,7 +30,7 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, const uint4 *b4,
                                              const uint4 *m4, uint64_t nvec, const uint8_t *img,
                                              uint32_t nb, uint32_t img_bytes, uint32_t nbins,
-                                             unsigned long long *out) {
+                                             uint32_t zero, unsigned long long *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t *keys = (const uint32_t *)smem;
   const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
@@ -97,7 +97,10 @@ __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, c
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t add = (1u << 20) | (by[k] & 0xFFFFF);
-      const uint32_t bd = (sl[4 + k] * 2) & 16383u, bs = (sl[k] * 2 + 1) & 16383u;
+      // realistic spread: bins from the IP's pod index (uniform over 12k); the slot
+      // value enters through a runtime zero mask so the reads stay live
+      const uint32_t bd = (((ip[4 + k] >> 8) * 2) + (sl[4 + k] & zero)) % 20032u;
+      const uint32_t bs = (((ip[k] >> 8) * 2 + 1) + (sl[k] & zero)) % 20032u;
       if (MODE == 3) {
         od[2 * k] = atomicAdd(&bins[bd], add);
         od[2 * k + 1] = atomicAdd(&bins[bs], add);
@@ -148,7 +151,7 @@ int main() {
   for (int mode = 0; mode <= 5; ++mode) {
     auto launch = [&]() {
       switch (mode) {
-#define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, out); break;
+#define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, 0u, out); break;
         L(0) L(1) L(2) L(3) L(4) L(5)
 #undef L
       }
