@@ -67,6 +67,8 @@ struct KArgs {
   // tier-1: LDS image of the IP table
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
+  uint32_t stage_a_stride;
   Plan p;
 };
 
@@ -741,21 +743,28 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   }
 
   __syncthreads();
-  // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
+  if (a.stage_a) {
+    // staged flush: plain 16-byte stores of this workgroup's bins; stage_reduce_kernel
+    // sums the copies (a global atomic per bin per workgroup costs more)
+    uint4 *dst = (uint4 *)(a.stage_a + (size_t)blockIdx.x * a.stage_a_stride);
+    for (uint32_t i = threadIdx.x; i < a.stage_a_stride / 4; i += blockDim.x) dst[i] = ((const uint4 *)bins)[i];
+  } else {
+    // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
 #pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    if (G.fam[g] == FAM_COUNT || !G.inl[g]) continue;
-    const bool with_bytes = G.fam[g] <= FAM_DROP;
-    const uint32_t hi = G.base[g] + a.p.g[g].nbins;
-    for (uint32_t i = G.base[g] + threadIdx.x; i < hi; i += blockDim.x) {
-      const uint32_t w = bins[i];
-      if (!w) continue;
-      if (with_bytes) {
-        atomicAdd(&a.d.cnt[i], (unsigned long long)(w >> kL4CountShift));
-        const uint32_t by = w & kL4BytesMask;
-        if (by) atomicAdd(&a.d.byt[i], (unsigned long long)by);
-      } else {
-        atomicAdd(&a.d.cnt[i], (unsigned long long)w);
+    for (int g = 0; g < NG; ++g) {
+      if (G.fam[g] == FAM_COUNT || !G.inl[g]) continue;
+      const bool with_bytes = G.fam[g] <= FAM_DROP;
+      const uint32_t hi = G.base[g] + a.p.g[g].nbins;
+      for (uint32_t i = G.base[g] + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t w = bins[i];
+        if (!w) continue;
+        if (with_bytes) {
+          atomicAdd(&a.d.cnt[i], (unsigned long long)(w >> kL4CountShift));
+          const uint32_t by = w & kL4BytesMask;
+          if (by) atomicAdd(&a.d.byt[i], (unsigned long long)by);
+        } else {
+          atomicAdd(&a.d.cnt[i], (unsigned long long)w);
+        }
       }
     }
   }
@@ -768,7 +777,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
 // round-robin placement -- speed only).
 __global__ __launch_bounds__(1024) void spill_window_kernel(
     const unsigned long long *spill, const uint32_t *spill_count, uint32_t n_lists,
-    uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d) {
+    uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d,
+    unsigned long long *stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
   const uint32_t b = blockIdx.x;
   const uint32_t w = (b >> 3) % nwin;
@@ -814,6 +824,11 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
     }
   }
   __syncthreads();
+  if (stage) {  // staged: this window partial, whole, for stage_reduce_b_kernel
+    uint4 *dst = (uint4 *)(stage + ((size_t)b * W));
+    for (uint32_t i = threadIdx.x; i < W / 2; i += blockDim.x) dst[i] = ((const uint4 *)win)[i];
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
     const unsigned long long v = win[i];
     if (v) {
@@ -822,6 +837,48 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
       if (by) atomicAdd(&d.byt[lo + i], by);
     }
   }
+}
+
+// Sums the tier-1 workgroups' staged u32 bins: blockIdx.y takes 1/gridDim.y of the
+// copies, so each bin gets gridDim.y global atomics instead of one per workgroup.
+__global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *stage, uint32_t ncopies,
+                                                             uint32_t stride, uint32_t L4, Plan p,
+                                                             DevDense d) {
+  const uint32_t bin = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bin >= L4) return;
+  bool packed = false;
+  for (int g = 0; g < p.ngroups; ++g)
+    if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
+      packed = p.g[g].family <= FAM_DROP;
+  const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * blockIdx.y) / gridDim.y);
+  const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (blockIdx.y + 1)) / gridDim.y);
+  unsigned long long cnt = 0, byt = 0;
+  for (uint32_t c = c0; c < c1; ++c) {
+    const uint32_t w = stage[(size_t)c * stride + bin];
+    cnt += packed ? (w >> kL4CountShift) : w;
+    byt += packed ? (w & kL4BytesMask) : 0u;
+  }
+  if (cnt) atomicAdd(&d.cnt[bin], cnt);
+  if (byt) atomicAdd(&d.byt[bin], byt);
+}
+
+// Sums the fold partials of every partition of a window (layout of spill_window_kernel).
+__global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long long *stage,
+                                                             uint32_t nwin, uint32_t nparts,
+                                                             uint32_t W, uint32_t lo0,
+                                                             uint64_t dense_len, DevDense d) {
+  const uint32_t off = blockIdx.x * blockDim.x + threadIdx.x;  // over nwin * W bins
+  const uint32_t w = off / W, i = off % W;
+  if (w >= nwin || lo0 + (uint64_t)off >= dense_len) return;
+  unsigned long long cnt = 0, byt = 0;
+  for (uint32_t part = 0; part < nparts; ++part) {
+    const uint32_t b = (part & 7u) + 8u * (w + nwin * (part >> 3));  // inverse of the fold map
+    const unsigned long long v = stage[(size_t)b * W + i];
+    cnt += v >> kLdsCountShift;
+    byt += v & kLdsBytesMask;
+  }
+  if (cnt) atomicAdd(&d.cnt[lo0 + off], cnt);
+  if (byt) atomicAdd(&d.byt[lo0 + off], byt);
 }
 
 __global__ void sparse_init_kernel(unsigned long long *k2, size_t n) {
@@ -894,6 +951,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_nb = a.ipl_nb;
   k.ipl_seed = a.ipl_seed;
   k.ipl_bytes = a.ipl_bytes;
+  k.stage_a = a.stage_a;
+  k.stage_a_stride = a.stage_a_stride;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
@@ -927,13 +986,24 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   }
   if (e != hipSuccess) return e;
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
+  if (a.stage_a) {
+    hipLaunchKernelGGL(stage_reduce_a_kernel, dim3((a.lds_bins + 255) / 256, 8), dim3(256), 0, st,
+                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (!a.spill) return hipSuccess;
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 << a.win_shift, st,
+  const uint32_t W = 1u << a.win_shift;
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
                      (const unsigned long long *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.spill_lo, a.dense_len, 1u << a.win_shift, a.nwin, k.d);
+                     a.spill_lo, a.dense_len, W, a.nwin, k.d, (unsigned long long *)a.stage_b);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (a.stage_b)
+    hipLaunchKernelGGL(stage_reduce_b_kernel, dim3((a.nwin * W + 255) / 256), dim3(256), 0, st,
+                       (const unsigned long long *)a.stage_b, a.nwin, a.win_blocks / a.nwin, W,
+                       a.spill_lo, a.dense_len, k.d);
   return hipGetLastError();
 }
 

@@ -46,6 +46,10 @@ struct LaunchArgs {
   bool tier1;           // dense kernel with the IP table and u32 bins in LDS
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  // staged flushes (null: flush with global atomics)
+  uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
+  uint32_t stage_a_stride;
+  uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
 };
 
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.

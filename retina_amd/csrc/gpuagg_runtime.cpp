@@ -173,6 +173,11 @@ struct gpuagg_ctx {
   size_t spill_alloc = 0;
   uint32_t *d_spill_count = nullptr;
   size_t spill_count_alloc = 0;
+  // staged flushes: per-workgroup LDS bins (tier-1) and per-partition fold windows
+  uint32_t *d_stage_a = nullptr;
+  size_t stage_a_alloc = 0;
+  uint64_t *d_stage_b = nullptr;
+  size_t stage_b_alloc = 0;
 };
 
 // ------------------------------------------------------------------------------------
@@ -209,10 +214,22 @@ int dev_alloc(gpuagg_ctx *c, T **p, size_t count) {
     return fail(c, GPUAGG_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
   return GPUAGG_OK;
 }
+
 template <class T>
 void dev_free(T *&p) {
   if (p) hipFree((void *)p);
   p = nullptr;
+}
+
+// Grows a lazily allocated device buffer to at least `count` elements.
+template <class T>
+int ensure_buf(gpuagg_ctx *c, T **p, size_t *alloc, size_t count) {
+  if (count <= *alloc) return GPUAGG_OK;
+  dev_free(*p);
+  *alloc = 0;
+  if (int rc = dev_alloc(c, p, count)) return rc;
+  *alloc = count;
+  return GPUAGG_OK;
 }
 
 uint8_t parse_opts(const char *const *labels, uint32_t n) {  // NewCtxOption (types.go:300-327)
@@ -401,6 +418,14 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.spill = nullptr;
     a.spill_count = nullptr;
     a.nwin = 0;
+    a.stage_b = nullptr;
+    a.stage_a = nullptr;
+    if (a.tier1 && a.lds_bins) {  // per-workgroup copies of the LDS bins, summed after
+      a.stage_a_stride = (a.lds_bins + 3u) & ~3u;
+      if ((rc = ensure_buf(c, &c->d_stage_a, &c->stage_a_alloc, (size_t)a.blocks * a.stage_a_stride)))
+        return rc;
+      a.stage_a = c->d_stage_a;
+    }
     if (c->dense_len > a.lds_bins) {
       // bins past the LDS window: per-workgroup spill lists bucketed by fold window
       const uint64_t rem = c->dense_len - a.lds_bins;
@@ -417,6 +442,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         }
         if ((size_t)a.blocks * nwin > c->spill_count_alloc) {
           dev_free(c->d_spill_count);
+  dev_free(c->d_stage_a);
+  dev_free(c->d_stage_b);
           c->spill_count_alloc = 0;
           if ((rc = dev_alloc(c, &c->d_spill_count, (size_t)a.blocks * nwin))) return rc;
           c->spill_count_alloc = (size_t)a.blocks * nwin;
@@ -427,6 +454,10 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         a.spill_lo = a.lds_bins;
         a.win_shift = kFoldWindowShift;
         a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
+        // fold partials are stored (not atomically added) and summed by a reduce pass
+        const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
+        if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
+        a.stage_b = c->d_stage_b;
       }
     }
     std::array<hipEvent_t, 3> ev{};
