@@ -225,6 +225,7 @@ void dev_free(T *&p) {
 template <class T>
 int ensure_buf(gpuagg_ctx *c, T **p, size_t *alloc, size_t count) {
   if (count <= *alloc) return GPUAGG_OK;
+  if (*p) hipStreamSynchronize(c->stream);  // in-flight launches may still use the old buffer
   dev_free(*p);
   *alloc = 0;
   if (int rc = dev_alloc(c, p, count)) return rc;
@@ -434,20 +435,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
         a.spill_cap = (uint32_t)cap;
         const size_t need = (size_t)a.blocks * nwin * a.spill_cap;
-        if (need > c->spill_alloc) {
-          dev_free(c->d_spill);
-          c->spill_alloc = 0;
-          if ((rc = dev_alloc(c, &c->d_spill, need))) return rc;
-          c->spill_alloc = need;
-        }
-        if ((size_t)a.blocks * nwin > c->spill_count_alloc) {
-          dev_free(c->d_spill_count);
-  dev_free(c->d_stage_a);
-  dev_free(c->d_stage_b);
-          c->spill_count_alloc = 0;
-          if ((rc = dev_alloc(c, &c->d_spill_count, (size_t)a.blocks * nwin))) return rc;
-          c->spill_count_alloc = (size_t)a.blocks * nwin;
-        }
+        if ((rc = ensure_buf(c, &c->d_spill, &c->spill_alloc, need))) return rc;
+        if ((rc = ensure_buf(c, &c->d_spill_count, &c->spill_count_alloc, (size_t)a.blocks * nwin)))
+          return rc;
         a.spill = c->d_spill;
         a.spill_count = c->d_spill_count;
         a.nwin = nwin;
@@ -544,6 +534,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_hll);
   dev_free(c->d_spill);
   dev_free(c->d_spill_count);
+  dev_free(c->d_stage_a);
+  dev_free(c->d_stage_b);
   for (auto &p : c->d_cols) dev_free(p);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
