@@ -158,25 +158,39 @@ constexpr uint32_t kIplMaxBuckets = 1u << 16;  // bucket math uses 24-bit multip
 // 24-bit multiplies are full rate on CDNA (32-bit ones are quarter rate)
 GA_HD uint32_t mul_u24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
 GA_HD uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // one v_mul_hi_u32_u24; written as asm because the compiler otherwise folds a later
+  // shift of the result into a full 48-bit product (mul_lo + mul_hi + alignbit)
+  uint32_t r;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
   return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
+#endif
 }
-// Both bucket choices of an IP (nb < 2^16).  The fold x ^ x>>12 brings the high byte,
-// which varies most in little-endian pod IPs, into the multiplied 24 bits.
+// Both bucket choices of an IP (nb < 2^16).  The fold x ^ x>>12 (a bijection) brings
+// the high byte, which varies most in little-endian pod IPs, into the 24 bits the
+// multiplies see; the two choices use different multipliers.
 GA_HD void ipl_buckets(uint32_t ip, uint32_t seed, uint32_t nb, uint32_t &b1, uint32_t &b2) {
   uint32_t x = ip ^ seed;
   x ^= x >> 12;
-  const uint32_t h1 = mul_u24(x, 0x9E3779u);
-  const uint32_t h2 = mul_u24(x ^ (x >> 7), 0xC2B2AFu);
-  b1 = mulhi_u24(h1 >> 8, nb << 8);  // = (h1>>8) * nb >> 24
-  b2 = mulhi_u24(h2 >> 8, nb << 8);
+  b1 = mulhi_u24(mul_u24(x, 0x9E3779u) >> 8, nb << 8);  // = (h1>>8) * nb >> 24
+  b2 = mulhi_u24(mul_u24(x, 0xC2B2AFu) >> 8, nb << 8);
 }
-GA_HD uint32_t ipl_image_bytes(uint32_t nb) {  // keys, then u16 values, 16-byte aligned
-  return ((nb * kIplWays * 4 + 15) & ~15u) + ((nb * kIplWays * 2 + 15) & ~15u);
+// Image: keys u32[nb*2] (16-byte padded), then vals u16[nb*2 + 1]; the extra value at
+// index nb*2 is the "not found" sentinel (kIplNoSlot), so a probe needs no branch.
+GA_HD uint32_t ipl_image_bytes(uint32_t nb) {
+  return ((nb * kIplWays * 4 + 15) & ~15u) + ((nb * kIplWays * 2 + 2 + 15) & ~15u);
 }
 GA_HD uint32_t ipl_vals_offset(uint32_t nb) { return (nb * kIplWays * 4 + 15) & ~15u; }
 // 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
 // correct the rare carry / wrap exactly with global atomics; count-only families
 // (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).
+// tier-1 kernel signatures: per group 4 bits (family + 1 | in-LDS << 3), group 0 lowest
+constexpr uint32_t sig_group(uint32_t fam, bool inl) { return (fam + 1) | (inl ? 8u : 0u); }
+constexpr uint32_t kSigFwdLds = sig_group(0, true);                                  // FAM_FWD
+constexpr uint32_t kSigFwdLdsDropLds = kSigFwdLds | sig_group(1, true) << 4;         // + FAM_DROP
+constexpr uint32_t kSigFwdLdsDropSpill = kSigFwdLds | sig_group(1, false) << 4;
 constexpr uint32_t kL4CountShift = 20;
 constexpr uint32_t kL4BytesMask = (1u << kL4CountShift) - 1;
 constexpr uint32_t kL4ByteLimit = 1u << kL4CountShift;

@@ -516,7 +516,7 @@ __device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32
   uint32_t b1, b2;
   ipl_buckets(ip, seed, nb, b1, b2);
   const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
-  uint32_t j = 0xFFFFFFFFu;
+  uint32_t j = nb * 2;  // sentinel entry: kIplNoSlot
   j = k1.x == ip ? b1 * 2 : j;
   j = k1.y == ip ? b1 * 2 + 1 : j;
   j = k2.x == ip ? b2 * 2 : j;
@@ -524,10 +524,8 @@ __device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32
   return j;
 }
 
-__device__ __forceinline__ int32_t ipl_slot(const uint16_t *vals, uint32_t j) {
-  const uint32_t v = vals[j == 0xFFFFFFFFu ? 0u : j];  // unconditional read: no branch
-  return (j == 0xFFFFFFFFu || v == kIplNoSlot) ? -1 : (int32_t)v;
-}
+// slot id, or kIplNoSlot (not a pod, or the apiserver pseudo pod)
+__device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
 
 struct L4Ctx {
   uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
@@ -554,7 +552,10 @@ struct L4Ctx {
 static_assert(kL4CountShift == 20, "fix() thresholds assume count:12 | bytes:20");
 
 // Group descriptors of the dense local-context plan, compile-time indexed (SGPRs).
-template <int NG>
+// SIG != 0 also fixes every group's family and LDS residency at compile time (4 bits per
+// group: family + 1, bit 3 = in LDS; see tier1_signature), so the per-record family
+// dispatch folds away; SIG == 0 reads them from the plan.
+template <int NG, uint32_t SIG>
 struct DenseGroups {
   uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
   bool inl[NG];
@@ -563,11 +564,17 @@ struct DenseGroups {
     any_flags = false;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      fam[g] = g < p.ngroups ? p.g[g].family : (uint32_t)FAM_COUNT;
+      if (SIG) {
+        const uint32_t code = (SIG >> (4 * g)) & 7u;
+        fam[g] = code ? code - 1 : (uint32_t)FAM_COUNT;
+        inl[g] = (SIG >> (4 * g + 3)) & 1u;
+      } else {
+        fam[g] = g < p.ngroups ? p.g[g].family : (uint32_t)FAM_COUNT;
+        inl[g] = p.g[g].dense_base + p.g[g].nbins <= L;
+      }
       base[g] = (uint32_t)p.g[g].dense_base;
       nsub[g] = p.g[g].nsub;
       keyed[g] = p.g[g].key_mode;
-      inl[g] = base[g] + p.g[g].nbins <= L;
       any_flags |= fam[g] == FAM_TCPFLAGS;
     }
   }
@@ -575,12 +582,12 @@ struct DenseGroups {
 
 // R records of one thread through every group (tier-1).  Group-outer / record-inner:
 // a group's 2R returning LDS adds are all issued before any result is inspected, so
-// their latency overlaps.  ss/sd: source / destination slot or -1.
-template <int NG, int R>
-__device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx &l4,
+// their latency overlaps.  ss/sd: source / destination slot or kIplNoSlot.
+template <int NG, uint32_t SIG, int R>
+__device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const L4Ctx &l4,
                                            const DenseSink &ds, const uint32_t (&nbytes)[R],
-                                           const uint32_t (&meta)[R], const int32_t (&ss)[R],
-                                           const int32_t (&sd)[R]) {
+                                           const uint32_t (&meta)[R], const uint32_t (&ss)[R],
+                                           const uint32_t (&sd)[R]) {
   uint32_t verdict[R], reason[R], flagmask[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) {
@@ -596,7 +603,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx
     uint32_t rd[R], rs[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {  // slots < 2^16, nsub <= 64: 24-bit multiplies
-      const uint32_t kd = G.keyed[g] ? (uint32_t)sd[k] : 0u, ks = G.keyed[g] ? (uint32_t)ss[k] : 0u;
+      const uint32_t kd = G.keyed[g] ? sd[k] : 0u, ks = G.keyed[g] ? ss[k] : 0u;
       rd[k] = G.base[g] + mul_u24(kd * 2u, G.nsub[g]);       // side 0: ingress (dst)
       rs[k] = G.base[g] + mul_u24(ks * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
     }
@@ -604,7 +611,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         uint32_t m = flagmask[k];
-        const bool d_ok = sd[k] >= 0, s_ok = ss[k] >= 0;
+        const bool d_ok = sd[k] != kIplNoSlot, s_ok = ss[k] != kIplNoSlot;
         if (G.inl[g]) {
           while (__ballot(m != 0)) {
             const bool v = m != 0;
@@ -631,8 +638,8 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx
     for (int k = 0; k < R; ++k) {
       const bool hit = verdict[k] == want;
       const uint32_t sub = f == FAM_DROP ? reason[k] : 0u;
-      vd[k] = hit && sd[k] >= 0;
-      vs[k] = hit && ss[k] >= 0;
+      vd[k] = hit && sd[k] != kIplNoSlot;
+      vs[k] = hit && ss[k] != kIplNoSlot;
       bd[k] = rd[k] + sub;
       bs[k] = rs[k] + sub;
     }
@@ -685,7 +692,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG> &G, const L4Ctx
   }
 }
 
-template <int NG, bool kVec>
+template <int NG, bool kVec, uint32_t SIG>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t nb = a.ipl_nb;
@@ -700,7 +707,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const L4Ctx l4{bins, L4 + lane, a.d};
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
-  const DenseGroups<NG> G(a.p, L4);
+  const DenseGroups<NG, SIG> G(a.p, L4);
   const uint32_t seed = a.ipl_seed;
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -726,20 +733,20 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       uint32_t j[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
-      int32_t sl[8];
+      uint32_t sl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
-      const int32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
+      const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
       const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
-      l4_records<NG, 4>(G, l4, ds, by, me, ss, sd);
+      l4_records<NG, SIG, 4>(G, l4, ds, by, me, ss, sd);
     }
     tail = start + (vn << 2);
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
-    const int32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
-    const int32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
+    const uint32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
+    const uint32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
     const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
-    l4_records<NG, 1>(G, l4, ds, by, me, ss, sd);
+    l4_records<NG, SIG, 1>(G, l4, ds, by, me, ss, sd);
   }
 
   __syncthreads();
@@ -959,15 +966,28 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
                              : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
-  switch (a.tier1 ? 100 + a.dense_ng : a.dense_ng) {
-    case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<1, false>, k, B, T, lds, st); break;
-    case 102: e = a.vec ? launch_k(dense_lds_kernel<2, true>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<2, false>, k, B, T, lds, st); break;
-    case 104: e = a.vec ? launch_k(dense_lds_kernel<4, true>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<4, false>, k, B, T, lds, st); break;
-    case 108: e = a.vec ? launch_k(dense_lds_kernel<8, true>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<8, false>, k, B, T, lds, st); break;  // dense local-context fast path, groups rounded up to 1/2/4/8
+  int variant = a.tier1 ? 100 + (int)a.dense_ng : (int)a.dense_ng;
+  if (a.tier1) {
+    if (a.sig == kSigFwdLdsDropSpill) variant = 200;
+    else if (a.sig == kSigFwdLdsDropLds) variant = 201;
+    else if (a.sig == kSigFwdLds) variant = 202;
+  }
+  switch (variant) {
+    case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true, 0>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<1, false, 0>, k, B, T, lds, st); break;
+    case 102: e = a.vec ? launch_k(dense_lds_kernel<2, true, 0>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<2, false, 0>, k, B, T, lds, st); break;
+    case 104: e = a.vec ? launch_k(dense_lds_kernel<4, true, 0>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<4, false, 0>, k, B, T, lds, st); break;
+    case 108: e = a.vec ? launch_k(dense_lds_kernel<8, true, 0>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<8, false, 0>, k, B, T, lds, st); break;
+    // compile-time specialised signatures (tier1_signature): the common C2 shapes
+    case 200: e = a.vec ? launch_k(dense_lds_kernel<2, true, kSigFwdLdsDropSpill>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<2, false, kSigFwdLdsDropSpill>, k, B, T, lds, st); break;
+    case 201: e = a.vec ? launch_k(dense_lds_kernel<2, true, kSigFwdLdsDropLds>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<2, false, kSigFwdLdsDropLds>, k, B, T, lds, st); break;
+    case 202: e = a.vec ? launch_k(dense_lds_kernel<1, true, kSigFwdLds>, k, B, T, lds, st)
+                        : launch_k(dense_lds_kernel<1, false, kSigFwdLds>, k, B, T, lds, st); break;
     case 1: e = a.vec ? launch_k(dense_local_kernel<1, true>, k, B, T, lds, st)
                       : launch_k(dense_local_kernel<1, false>, k, B, T, lds, st); break;
     case 2: e = a.vec ? launch_k(dense_local_kernel<2, true>, k, B, T, lds, st)

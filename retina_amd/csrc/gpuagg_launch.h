@@ -44,6 +44,7 @@ struct LaunchArgs {
   uint32_t spill_lo;    // first spilled dense bin (fold windows start here)
   uint32_t dense_ng;    // 0: generic kernel; 1/2/4/8: dense local-context kernel
   bool tier1;           // dense kernel with the IP table and u32 bins in LDS
+  uint32_t sig;         // tier-1 group signature (kSig*), 0 when the plan has none
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   // staged flushes (null: flush with global atomics)

@@ -390,6 +390,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.lds_bins = prefix(kLdsMaxBins);
   // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
+  a.sig = 0;
   if (a.dense_ng && c->ipl_bytes && !spans.empty() &&
       c->ipl_bytes + kL4ExtraBytes < kLdsBytes) {
     // (with no group in LDS every update spills, but the IP probes still stay on-chip)
@@ -397,6 +398,14 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     {
       a.tier1 = true;
       a.lds_bins = L4;
+      a.sig = 0;
+      if (c->plan.ngroups <= 8) {  // groups in layout order, as the kernel indexes them
+        uint32_t sig = 0;
+        for (int g = 0; g < c->plan.ngroups; ++g)
+          sig |= sig_group(c->plan.g[g].family, c->plan.g[g].dense_base + c->plan.g[g].nbins <= L4)
+                 << (4 * g);
+        a.sig = sig;
+      }
       a.ipl = c->d_ipl;
       a.ipl_nb = c->ipl_nb;
       a.ipl_seed = c->ipl_seed;

@@ -33,7 +33,7 @@ inline bool ipl_build(const std::vector<std::pair<uint32_t, uint32_t>> &ents, Ip
     if (nb >= kIplMaxBuckets || ipl_image_bytes(nb) > kIplMaxBytes) return false;
     seed = (uint32_t)fmix64((uint64_t)seed + 0xBB67AE8584CAA73BULL * (uint64_t)(attempt + 1));
     keys.assign((size_t)nb * kIplWays, kIplEmptyKey);
-    vals.assign((size_t)nb * kIplWays, (uint16_t)kIplNoSlot);
+    vals.assign((size_t)nb * kIplWays + 1, (uint16_t)kIplNoSlot);  // + sentinel
     bool ok = true;
     uint64_t rng = seed | 1ULL;
     for (const auto &e : ents) {
@@ -85,9 +85,10 @@ inline uint32_t ipl_probe(const uint8_t *img, uint32_t nb, uint32_t seed, uint32
   ipl_buckets(ip, seed, nb, b1, b2);
   const uint32_t *keys = (const uint32_t *)img;
   const uint16_t *vals = (const uint16_t *)(img + ipl_vals_offset(nb));
-  for (uint32_t j : {b1 * 2, b1 * 2 + 1, b2 * 2, b2 * 2 + 1})
-    if (keys[j] == ip) return vals[j];
-  return kIplNoSlot;
+  uint32_t j = nb * kIplWays;  // sentinel
+  for (uint32_t c : {b1 * 2, b1 * 2 + 1, b2 * 2, b2 * 2 + 1})
+    if (keys[c] == ip) j = c;
+  return vals[j];
 }
 
 }  // namespace gpuagg
