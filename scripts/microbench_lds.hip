@@ -7,6 +7,9 @@
 //   3 +atomic_rtn     + 2 returning u32 LDS adds per record into 20k bins
 //   4 +atomic_nortn   mode 2 + 2 non-returning u32 LDS adds per record
 //   5 hash-only       loads + bucket hashing, no LDS reads
+//   6 +spill          mode 2 + 10% of records append 2 entries (8 B) to per-workgroup
+//                     lists bucketed into 10 windows (per-lane LDS counter reservation)
+//   7 +spill-nostore  mode 6 without the global stores (reservations only)
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/mbl scripts/microbench_lds.hip && /tmp/mbl
 #include <hip/hip_runtime.h>
 
@@ -30,14 +33,18 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, const uint4 *b4,
                                              const uint4 *m4, uint64_t nvec, const uint8_t *img,
                                              uint32_t nb, uint32_t img_bytes, uint32_t nbins,
-                                             uint32_t zero, unsigned long long *out) {
+                                             uint32_t zero, unsigned long long *out,
+                                             unsigned long long *spill, uint32_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t *keys = (const uint32_t *)smem;
   const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
   uint32_t *bins = (uint32_t *)(smem + img_bytes);
   for (uint32_t i = threadIdx.x; i < img_bytes / 16; i += blockDim.x) ((uint4 *)smem)[i] = ((const uint4 *)img)[i];
-  for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) bins[i] = 0;
+  for (uint32_t i = threadIdx.x; i < nbins + 64 + 32; i += blockDim.x) bins[i] = 0;
   __syncthreads();
+  uint32_t *ctr = bins + nbins + 64;
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  unsigned long long *my = spill + (size_t)blockIdx.x * 10 * cap;
   const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
   const uint64_t v0 = blockIdx.x * per, vend = v0 + per < nvec ? v0 + per : nvec;
   uint32_t acc = 0;
@@ -90,6 +97,30 @@ __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, c
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc += sl[k];
       acc += vb.x ^ vm.x;
+      continue;
+    }
+    if (MODE == 6 || MODE == 7) {
+      const uint32_t me[4] = {vm.x, vm.y, vm.z, vm.w}, by[4] = {vb.x, vb.y, vb.z, vb.w};
+      uint32_t wd[4], ws[4], pd[4], ps[4], bd[4], bs[4];
+      bool v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = (me[k] % 10u) == 0u;
+        bd[k] = (((ip[4 + k] >> 8) * 16) + (sl[4 + k] & zero)) % 160000u;
+        bs[k] = (((ip[k] >> 8) * 16 + 8) + (sl[k] & zero)) % 160000u;
+        wd[k] = bd[k] >> 14;
+        ws[k] = bs[k] >> 14;
+        pd[k] = atomicAdd(v[k] ? &ctr[wd[k]] : &bins[nbins + lane], 1u);
+        ps[k] = atomicAdd(v[k] ? &ctr[ws[k]] : &bins[nbins + lane], 1u);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (MODE == 6 && v[k]) {
+          if (pd[k] < cap) my[wd[k] * cap + pd[k]] = ((unsigned long long)bd[k] << 32) | by[k];
+          if (ps[k] < cap) my[ws[k] * cap + ps[k]] = ((unsigned long long)bs[k] << 32) | by[k];
+        }
+        acc += pd[k] + ps[k];
+      }
       continue;
     }
     const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w};
@@ -146,19 +177,23 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const size_t lds = img_bytes + nbins * 4;
-  const char *names[] = {"stream", "probe", "probe+val", "+atomic_rtn", "+atomic_nortn", "hash-only"};
-  for (int mode = 0; mode <= 5; ++mode) {
+  const size_t lds = img_bytes + nbins * 4 + 96 * 4;
+  const uint32_t cap = 16384;
+  unsigned long long *spill;
+  CK(hipMalloc(&spill, (size_t)256 * 10 * cap * 8));
+  const char *names[] = {"stream", "probe", "probe+val", "+atomic_rtn", "+atomic_nortn", "hash-only",
+                         "+spill", "+spill-nostore"};
+  for (int mode = 0; mode <= 7; ++mode) {
     auto launch = [&]() {
       switch (mode) {
-#define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, 0u, out); break;
-        L(0) L(1) L(2) L(3) L(4) L(5)
+#define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, 0u, out, spill, cap); break;
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7)
 #undef L
       }
     };
     switch (mode) {
 #define A(M) case M: CK(hipFuncSetAttribute((const void *)kern<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840)); break;
-      A(0) A(1) A(2) A(3) A(4) A(5)
+      A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7)
 #undef A
     }
     launch();
