@@ -10,6 +10,10 @@
 //   6 +spill          mode 2 + 10% of records append 2 entries (8 B) to per-workgroup
 //                     lists bucketed into 10 windows (per-lane LDS counter reservation)
 //   7 +spill-nostore  mode 6 without the global stores (reservations only)
+//   8 +spill-oddcap   mode 6 with a non-power-of-two list stride
+//   9 +spill4         mode 8 with 4-byte entries (bin in window:14 | bytes:18)
+//  10 +spill-1list    one list per workgroup, one 8-byte entry per spilled record,
+//                     wave-aggregated reservation (ballot) -> contiguous stores
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/mbl scripts/microbench_lds.hip && /tmp/mbl
 #include <hip/hip_runtime.h>
 
@@ -99,7 +103,23 @@ __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, c
       acc += vb.x ^ vm.x;
       continue;
     }
-    if (MODE == 6 || MODE == 7) {
+    if (MODE == 10) {
+      const uint32_t me[4] = {vm.x, vm.y, vm.z, vm.w}, by[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool v = (me[k] % 10u) == 0u;
+        const unsigned long long m = __ballot(v);
+        uint32_t base = 0;
+        if (lane == 0 && m) base = atomicAdd(&ctr[0], (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+        if (v && pos < 10 * cap)
+          my[pos] = ((unsigned long long)((sl[k] & 0xFFFFu) | ((sl[4 + k] & 0xFFFFu) << 16)) << 32) | by[k];
+      }
+      acc += vm.x;
+      continue;
+    }
+    if (MODE == 6 || MODE == 7 || MODE == 8 || MODE == 9) {
       const uint32_t me[4] = {vm.x, vm.y, vm.z, vm.w}, by[4] = {vb.x, vb.y, vb.z, vb.w};
       uint32_t wd[4], ws[4], pd[4], ps[4], bd[4], bs[4];
       bool v[4];
@@ -115,9 +135,14 @@ __global__ __launch_bounds__(1024) void kern(const uint4 *s4, const uint4 *d4, c
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (MODE == 6 && v[k]) {
+        if ((MODE == 6 || MODE == 8) && v[k]) {
           if (pd[k] < cap) my[wd[k] * cap + pd[k]] = ((unsigned long long)bd[k] << 32) | by[k];
           if (ps[k] < cap) my[ws[k] * cap + ps[k]] = ((unsigned long long)bs[k] << 32) | by[k];
+        }
+        if (MODE == 9 && v[k]) {
+          uint32_t *my4 = (uint32_t *)my;
+          if (pd[k] < cap) my4[wd[k] * cap + pd[k]] = ((bd[k] & 16383u) << 18) | (by[k] & 0x3FFFFu);
+          if (ps[k] < cap) my4[ws[k] * cap + ps[k]] = ((bs[k] & 16383u) << 18) | (by[k] & 0x3FFFFu);
         }
         acc += pd[k] + ps[k];
       }
@@ -178,22 +203,22 @@ int main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const size_t lds = img_bytes + nbins * 4 + 96 * 4;
-  const uint32_t cap = 16384;
   unsigned long long *spill;
-  CK(hipMalloc(&spill, (size_t)256 * 10 * cap * 8));
+  CK(hipMalloc(&spill, (size_t)256 * 10 * 16500 * 8));
   const char *names[] = {"stream", "probe", "probe+val", "+atomic_rtn", "+atomic_nortn", "hash-only",
-                         "+spill", "+spill-nostore"};
-  for (int mode = 0; mode <= 7; ++mode) {
+                         "+spill", "+spill-nostore", "+spill-oddcap", "+spill4", "+spill-1list"};
+  for (int mode = 0; mode <= 10; ++mode) {
+    const uint32_t cap = (mode == 8 || mode == 9) ? 16384 + 37 : 16384;
     auto launch = [&]() {
       switch (mode) {
 #define L(M) case M: hipLaunchKernelGGL(kern<M>, dim3(256), dim3(1024), lds, 0, (uint4 *)col[0], (uint4 *)col[1], (uint4 *)col[2], (uint4 *)col[3], (uint64_t)nvec, img, nb, img_bytes, nbins, 0u, out, spill, cap); break;
-        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10)
 #undef L
       }
     };
     switch (mode) {
 #define A(M) case M: CK(hipFuncSetAttribute((const void *)kern<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840)); break;
-      A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7)
+      A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7) A(8) A(9) A(10)
 #undef A
     }
     launch();
