@@ -19,6 +19,9 @@
 //  * sparse (remote-context / ip / port / DNS) keys go to an HBM hash table.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "gpuagg_internal.h"
 #include "gpuagg_launch.h"
 
@@ -972,6 +975,11 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     else if (a.sig == kSigFwdLdsDropLds) variant = 201;
     else if (a.sig == kSigFwdLds) variant = 202;
   }
+  static const bool trace = getenv("GPUAGG_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "gpuagg: launch variant=%d tier1=%d sig=0x%x ng=%u L=%u ipl_bytes=%u nwin=%u n=%llu\n",
+            variant, (int)a.tier1, a.sig, a.dense_ng, a.lds_bins, a.ipl_bytes, a.nwin,
+            (unsigned long long)a.n);
   switch (variant) {
     case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true, 0>, k, B, T, lds, st)
                         : launch_k(dense_lds_kernel<1, false, 0>, k, B, T, lds, st); break;

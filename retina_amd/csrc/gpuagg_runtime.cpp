@@ -696,16 +696,28 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
   // Dense bin layout, hottest family first: bins [0, L) live in LDS (kernels file), so
   // forward counters (every forwarded flow) go before TCP-flag, drop and retransmit ones.
   {
+    // Group indices follow the same order (dense groups in layout order, then sparse
+    // ones), so the tier-1 kernel's compile-time signatures see group 0 = hottest.
     static const int prio[FAM_COUNT] = {0, 2, 1, 3, 9, 9};
-    std::vector<size_t> order;
-    for (size_t g = 0; g < groups.size(); ++g)
-      if (!groups[g].sparse) order.push_back(g);
+    std::vector<size_t> order(groups.size());
+    for (size_t g = 0; g < groups.size(); ++g) order[g] = g;
     std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
-      return prio[groups[x].family] < prio[groups[y].family];
+      if (groups[x].sparse != groups[y].sparse) return !groups[x].sparse;
+      return !groups[x].sparse && prio[groups[x].family] < prio[groups[y].family];
     });
-    for (size_t g : order) {
-      groups[g].dense_base = dense_total;
-      dense_total += groups[g].nkeys * 2 * groups[g].nsub;
+    std::vector<Group> sorted;
+    std::vector<int> new_index(groups.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+      new_index[order[i]] = (int)i;
+      sorted.push_back(groups[order[i]]);
+    }
+    groups.swap(sorted);
+    for (auto &in : inst)
+      if (in.group >= 0) in.group = new_index[in.group];
+    for (auto &g : groups) {
+      if (g.sparse) continue;
+      g.dense_base = dense_total;
+      dense_total += g.nkeys * 2 * g.nsub;
     }
   }
   if (dense_total >= (1ull << 32)) return fail(c, GPUAGG_ECAPACITY, "dense counter space >= 2^32 bins");
