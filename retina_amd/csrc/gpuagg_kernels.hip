@@ -563,8 +563,10 @@ struct DenseGroups {
   uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
   bool inl[NG];
   bool any_flags;
+  bool any_spilled;  // some group's bins are outside LDS
   __device__ __forceinline__ DenseGroups(const Plan &p, uint32_t L) {
     any_flags = false;
+    any_spilled = false;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       if (SIG) {
@@ -579,14 +581,61 @@ struct DenseGroups {
       nsub[g] = p.g[g].nsub;
       keyed[g] = p.g[g].key_mode;
       any_flags |= fam[g] == FAM_TCPFLAGS;
+      any_spilled |= fam[g] != FAM_COUNT && !inl[g];
     }
+  }
+};
+
+// Does a record update group f (tier-1 families only: fwd / drop / tcpflags / retrans)?
+__device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t flagmask) {
+  if (f == FAM_TCPFLAGS) return flagmask != 0;
+  return verdict == (f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans);
+}
+
+// Wave-level compaction queue for the records that update a spilled group (one whose
+// bins are not in LDS).  Such records are rare (C2: the 10 % drops), so updating them
+// in place would issue every spill instruction for ~5 active lanes of 64.  Instead each
+// step pushes them into three queue registers (one entry per lane) with ds_permute --
+// LDS crossbar, no LDS memory -- and the spill code runs once per 64 queued records
+// with every lane busy.  Push = ballot + mbcnt + a bijective lane permutation: hits go
+// to queue positions [n, n + hits), misses to the remaining ones, so every lane
+// receives exactly one value.
+struct SpillQ {
+  uint32_t e0, e1, e2;  // queued entries: slots (ss | sd << 16), bytes, meta
+  uint32_t r0, r1, r2;  // this push's permuted values (wrap-around part on overflow)
+  uint32_t n;           // queued entries (wave-uniform), lanes [0, n)
+  // push; returns true when the queue holds 64 entries (caller flushes, then next())
+  __device__ __forceinline__ bool push(bool v, uint32_t lane, uint32_t a0, uint32_t a1, uint32_t a2) {
+    const uint64_t m = __ballot(v);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const uint32_t pos = v ? n + below : n + cnt + (lane - below);
+    const int addr = (int)((pos & 63u) << 2);
+    r0 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a0);
+    r1 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a1);
+    r2 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a2);
+    const bool got = lane >= n && lane < n + cnt;
+    e0 = got ? r0 : e0;
+    e1 = got ? r1 : e1;
+    e2 = got ? r2 : e2;
+    n += cnt;
+    return n >= 64;
+  }
+  // after flushing a full queue: the wrapped entries become the queue
+  __device__ __forceinline__ void next() {
+    e0 = r0;
+    e1 = r1;
+    e2 = r2;
+    n -= 64;
   }
 };
 
 // R records of one thread through every group (tier-1).  Group-outer / record-inner:
 // a group's 2R returning LDS adds are all issued before any result is inspected, so
 // their latency overlaps.  ss/sd: source / destination slot or kIplNoSlot.
-template <int NG, uint32_t SIG, int R>
+// kMode: 0 every group; 1 LDS groups only (spilled ones go through SpillQ); 2 spilled
+// groups only (the SpillQ flush).
+template <int NG, uint32_t SIG, int R, int kMode = 0>
 __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const L4Ctx &l4,
                                            const DenseSink &ds, const uint32_t (&nbytes)[R],
                                            const uint32_t (&meta)[R], const uint32_t (&ss)[R],
@@ -603,6 +652,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
   for (int g = 0; g < NG; ++g) {
     const uint32_t f = G.fam[g];
     if (f == FAM_COUNT) continue;
+    if ((kMode == 1 && !G.inl[g]) || (kMode == 2 && G.inl[g])) continue;
     uint32_t rd[R], rs[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {  // slots < 2^16, nsub <= 64: 24-bit multiplies
@@ -712,6 +762,15 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
   const DenseGroups<NG, SIG> G(a.p, L4);
   const uint32_t seed = a.ipl_seed;
+  SpillQ q{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
+  auto q_flush = [&](bool full) {
+    const bool valid = full || lane < q.n;
+    const uint32_t s1[1] = {valid ? (q.e0 & 0xFFFFu) : kIplNoSlot};
+    const uint32_t d1[1] = {valid ? (q.e0 >> 16) : kIplNoSlot};
+    const uint32_t b1[1] = {q.e1}, m1[1] = {q.e2};
+    l4_records<NG, SIG, 1, 2>(G, l4, ds, b1, m1, s1, d1);
+  };
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
   uint64_t tail = start;
@@ -721,13 +780,16 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t v0 = start >> 2, vn = (end - start) >> 2, vend = v0 + vn;
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
-    uint64_t v = v0 + threadIdx.x;
+    // the loop is wave-uniform (SpillQ's cross-lane pushes need every lane present):
+    // lanes past the end load a clamped vector and update nothing
+    const uint64_t vwave = v0 + (threadIdx.x & ~63u);
     const uint64_t vlast = vend - 1;  // vn >= 1
-    uint64_t vl = v < vend ? v : vlast;
+    uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
     uint4 ns = s4[vl], nd = d4[vl], nbv = b4[vl], nm = m4[vl];
-    for (; v < vend; v += blockDim.x) {
+    for (uint64_t vw = vwave; vw < vend; vw += blockDim.x) {
+      const bool act = vw + lane < vend;
       const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
-      vl = v + blockDim.x < vend ? v + blockDim.x : vlast;  // clamped: no branch
+      vl = vw + blockDim.x + lane < vend ? vw + blockDim.x + lane : vlast;  // clamped: no branch
       ns = s4[vl];
       nd = d4[vl];
       nbv = b4[vl];
@@ -738,10 +800,37 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
       uint32_t sl[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
+      for (int k = 0; k < 8; ++k) sl[k] = act ? ipl_slot(vals, j[k]) : kIplNoSlot;
       const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
       const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
-      l4_records<NG, SIG, 4>(G, l4, ds, by, me, ss, sd);
+      if (!G.any_spilled) {
+        l4_records<NG, SIG, 4, 0>(G, l4, ds, by, me, ss, sd);
+        continue;
+      }
+      l4_records<NG, SIG, 4, 1>(G, l4, ds, by, me, ss, sd);
+      // records that update a spilled group -> SpillQ (rolled: one copy of the flush)
+      uint32_t x0 = ss[0] | sd[0] << 16, x1 = ss[1] | sd[1] << 16, x2 = ss[2] | sd[2] << 16,
+               x3 = ss[3] | sd[3] << 16;
+      uint32_t y0 = by[0], y1 = by[1], y2 = by[2], y3 = by[3];
+      uint32_t z0 = me[0], z1 = me[1], z2 = me[2], z3 = me[3];
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t ver = meta_verdict(z0);
+        const uint32_t fm = (G.any_flags && ver == kVerdictForwarded && meta_proto(z0) == 6)
+                                ? flag_label_mask(meta_flags(z0)) : 0u;
+        bool need = false;
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          if (G.fam[g] != FAM_COUNT && !G.inl[g]) need |= fam_hit(G.fam[g], ver, fm);
+        need = need && x0 != 0xFFFFFFFFu;  // some side is a pod
+        if (q.push(need, lane, x0, y0, z0)) {
+          q_flush(true);
+          q.next();
+        }
+        x0 = x1; x1 = x2; x2 = x3;
+        y0 = y1; y1 = y2; y2 = y3;
+        z0 = z1; z1 = z2; z2 = z3;
+      }
     }
     tail = start + (vn << 2);
   }
@@ -751,6 +840,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
     l4_records<NG, SIG, 1>(G, l4, ds, by, me, ss, sd);
   }
+  if (G.any_spilled && q.n) q_flush(false);
 
   __syncthreads();
   if (a.stage_a) {
