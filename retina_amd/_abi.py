@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgpuagg.so")
+LIB_PATH = os.environ.get("GPUAGG_LIB") or os.path.join(HERE, "libgpuagg.so")
 
 ABI_VERSION = 1
 OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE = 0, -1, -2, -3, -4, -5, -6, -7

@@ -61,11 +61,12 @@ struct KArgs {
   DevSparse s;
   DevSketch sk;
   uint32_t lds_bins;  // L: dense bins privatised in LDS (u64 words; tier-1: u32 words)
-  // spill lists: per workgroup, one list per fold window of 2^win_shift bins starting at
-  // dense bin `spill_lo`; list (b, w) at spill + (b*nwin + w)*spill_cap
+  // spill lists: per workgroup, one list per fold window of 2^kFoldWindowShift bins
+  // starting at dense bin `spill_lo`; list (b, w) at spill + (b*nwin + w)*spill_cap;
+  // entries u32 = bin offset in the window | bytes << kFoldWindowShift (spill_entry)
   uint32_t spill_cap;
   uint32_t nwin, win_shift, spill_lo;
-  unsigned long long *spill;  // or null: bins >= lds_bins use global atomics
+  uint32_t *spill;  // or null: bins >= lds_bins use global atomics
   uint32_t *spill_count;      // [gridDim.x * nwin]
   // tier-1: LDS image of the IP table
   const uint8_t *ipl;
@@ -154,15 +155,23 @@ struct DenseSink {
   unsigned long long *lds;  // u64 bins (generic / dense_local kernels)
   uint32_t L;
   unsigned int *ctr;        // per-window spill counters (LDS)
-  unsigned long long *spill;
+  uint32_t *spill;
   uint32_t spill_cap, win_shift, spill_lo;
   DevDense d;
+  uint32_t wbits;           // bits of a window index (nwin <= 2^wbits)
 
-  __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> win_shift; }
+  __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> kFoldWindowShift; }
+  // 4-byte entry: the bin's offset in its window and the bytes; bytes that do not fit
+  // the field are added to the global counter here (rare) and the entry carries 0
+  __device__ __forceinline__ uint32_t entry(uint32_t bin, uint32_t nbytes) const {
+    const bool fits = nbytes < kSpillByteLimit;
+    if (!fits) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
+    return ((bin - spill_lo) & (kFoldWindowBins - 1)) | ((fits ? nbytes : 0u) << kFoldWindowShift);
+  }
   // store one reserved spill entry (pos from the window counter); full list -> global
   __device__ __forceinline__ void spill_put(uint32_t bin, uint32_t w, uint32_t pos, uint32_t nbytes) const {
-    if (pos < spill_cap) {
-      spill[mul_u24(w, spill_cap) + pos] = ((unsigned long long)bin << 32) | nbytes;
+    if (pos < spill_cap) {  // w < 32 and spill_cap < 2^24: 24-bit multiply
+      spill[mul_u24(w, spill_cap) + pos] = entry(bin, nbytes);
       return;
     }
     atomicAdd(&d.cnt[bin], 1ULL);
@@ -171,10 +180,10 @@ struct DenseSink {
 
   __device__ __forceinline__ void spill_add(uint32_t bin, uint32_t nbytes) const {
     if (spill) {
-      const uint32_t w = (bin - spill_lo) >> win_shift;
+      const uint32_t w = window(bin);
       const unsigned int pos = atomicAdd(&ctr[w], 1u);
-      if (pos < spill_cap) {  // w < 16 and spill_cap < 2^24: 24-bit multiply
-        spill[mul_u24(w, spill_cap) + pos] = ((unsigned long long)bin << 32) | nbytes;
+      if (pos < spill_cap) {
+        spill[mul_u24(w, spill_cap) + pos] = entry(bin, nbytes);
         return;
       }
     }
@@ -196,13 +205,34 @@ __device__ __forceinline__ DenseSink make_sink(const KArgs &a, unsigned long lon
                                                unsigned int *ctr) {
   return DenseSink{lds, L, ctr,
                    a.spill ? a.spill + (size_t)blockIdx.x * a.nwin * a.spill_cap : nullptr,
-                   a.spill_cap, a.win_shift, a.spill_lo, a.d};
+                   a.spill_cap, a.win_shift, a.spill_lo, a.d,
+                   a.nwin > 1 ? 32u - (uint32_t)__builtin_clz(a.nwin - 1) : 0u};
 }
 
 __device__ __forceinline__ void spill_counts_out(const KArgs &a, const unsigned int *ctr) {
   if (a.spill)
     for (uint32_t w = threadIdx.x; w < a.nwin; w += blockDim.x)
       a.spill_count[blockIdx.x * a.nwin + w] = ctr[w] < a.spill_cap ? ctr[w] : a.spill_cap;
+}
+
+// Positions in the per-window spill lists for the lanes with `ok`, reserved with ONE
+// LDS atomic per distinct window of the wave (lanes are grouped by wbits ballots of the
+// window bits; the group's lowest lane adds the group size and ds_bpermute hands the
+// base to the others).  Per-lane atomics on a few counters serialise in the LDS.
+// Must be called by the whole wave.
+__device__ __forceinline__ uint32_t wave_reserve(bool ok, uint32_t w, unsigned int *ctr, uint32_t wbits) {
+  uint64_t eq = __ballot(ok);
+  for (uint32_t b = 0; b < wbits; ++b) {
+    const bool bit = (w >> b) & 1u;
+    const uint64_t B = __ballot(bit);
+    eq &= bit ? B : ~B;
+  }
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(eq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)eq, 0u));
+  uint32_t base = 0;
+  if (ok && rank == 0) base = atomicAdd(&ctr[w], (uint32_t)__popcll(eq));
+  const uint32_t lead = eq ? (uint32_t)__builtin_ctzll(eq) : 0u;
+  base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)base);
+  return base + rank;
 }
 
 // Side tuple of a context (types.go:418-505): only the fields the options read.
@@ -725,8 +755,13 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       for (int k = 0; k < R; ++k) {
         wd[k] = ds.window(bd[k]);
         ws[k] = ds.window(bs[k]);
-        pd[k] = atomicAdd(vd[k] ? &ds.ctr[wd[k]] : &l4.bins[l4.dummy], 1u);
-        ps[k] = atomicAdd(vs[k] ? &ds.ctr[ws[k]] : &l4.bins[l4.dummy], 1u);
+        if (kMode == 2) {  // SpillQ flush: converged wave
+          pd[k] = wave_reserve(vd[k], wd[k], ds.ctr, ds.wbits);
+          ps[k] = wave_reserve(vs[k], ws[k], ds.ctr, ds.wbits);
+        } else {
+          pd[k] = atomicAdd(vd[k] ? &ds.ctr[wd[k]] : &l4.bins[l4.dummy], 1u);
+          ps[k] = atomicAdd(vs[k] ? &ds.ctr[ws[k]] : &l4.bins[l4.dummy], 1u);
+        }
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
@@ -876,7 +911,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
 // once.  Workgroups of one partition share blockIdx % 8 (one XCD under the observed
 // round-robin placement -- speed only).
 __global__ __launch_bounds__(1024) void spill_window_kernel(
-    const unsigned long long *spill, const uint32_t *spill_count, uint32_t n_lists,
+    const uint32_t *spill, const uint32_t *spill_count, uint32_t n_lists,
     uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d,
     unsigned long long *stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
@@ -888,40 +923,44 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
   __syncthreads();
-  // fewer than 2^20 entries into this window copy: no packed field can overflow, so
-  // plain (no-return) LDS atomics suffice; otherwise the exact carrying add
+  // fewer than 2^20 entries into this window copy: no packed field can overflow
+  // (entries carry < 2^18 bytes), so plain (no-return) LDS atomics suffice; otherwise
+  // the exact carrying add
   uint64_t total = 0;
   for (uint32_t l = part; l < n_lists; l += nparts) total += spill_count[(size_t)l * nwin + w];
   const bool fast = total < (1ULL << 20);
+  const uint32_t off_mask = kFoldWindowBins - 1;
+  auto add = [&](uint32_t x) {
+    const uint32_t off = x & off_mask, nb = x >> kFoldWindowShift;
+    if (fast) atomicAdd(&win[off], kLdsCountOne | nb);
+    else lds_add64_exact(&win[off], (uint32_t)lo + off, nb, d);
+  };
   for (uint32_t l = part; l < n_lists; l += nparts) {
     const uint32_t cnt = spill_count[(size_t)l * nwin + w];
-    const unsigned long long *e = spill + ((size_t)l * nwin + w) * spill_cap;
-    if (fast) {
-      uint32_t j = threadIdx.x;
-      for (; j + 3 * blockDim.x < cnt; j += 4 * blockDim.x) {
-        unsigned long long v[4];
+    const uint32_t *e = spill + ((size_t)l * nwin + w) * spill_cap;  // 16-byte aligned (cap % 4 == 0)
+    const uint4 *e4 = (const uint4 *)e;
+    const uint32_t n4 = cnt >> 2;
+    uint32_t j = threadIdx.x;
+    for (; j + 3 * blockDim.x < n4; j += 4 * blockDim.x) {  // 16 entries per lane in flight
+      uint4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = e[j + k * blockDim.x];
+      for (int k = 0; k < 4; ++k) v[k] = e4[j + k * blockDim.x];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t bin = (uint32_t)(v[k] >> 32), nb = (uint32_t)v[k];
-          atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
-          if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
-        }
-      }
-      for (; j < cnt; j += blockDim.x) {
-        const unsigned long long v = e[j];
-        const uint32_t bin = (uint32_t)(v >> 32), nb = (uint32_t)v;
-        atomicAdd(&win[bin - lo], kLdsCountOne | (nb < kLdsByteLimit ? nb : 0u));
-        if (nb >= kLdsByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
-      }
-    } else {
-      for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        const unsigned long long v = e[j];
-        const uint32_t bin = (uint32_t)(v >> 32);
-        lds_add64_exact(&win[bin - lo], bin, (uint32_t)v, d);
+      for (int k = 0; k < 4; ++k) {
+        add(v[k].x);
+        add(v[k].y);
+        add(v[k].z);
+        add(v[k].w);
       }
     }
+    for (; j < n4; j += blockDim.x) {
+      const uint4 v = e4[j];
+      add(v.x);
+      add(v.y);
+      add(v.z);
+      add(v.w);
+    }
+    for (uint32_t i = (n4 << 2) + threadIdx.x; i < cnt; i += blockDim.x) add(e[i]);
   }
   __syncthreads();
   if (stage) {  // staged: this window partial, whole, for stage_reduce_b_kernel
@@ -1041,7 +1080,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.s = dev_sparse(a.sparse);
   k.sk = DevSketch{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};
   k.lds_bins = a.lds_bins;
-  k.spill = (unsigned long long *)a.spill;
+  k.spill = a.spill;
   k.spill_cap = a.spill_cap;
   k.nwin = a.nwin;
   k.win_shift = a.win_shift;
@@ -1115,7 +1154,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (e != hipSuccess) return e;
   const uint32_t W = 1u << a.win_shift;
   hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
-                     (const unsigned long long *)a.spill, a.spill_count, a.blocks, a.spill_cap,
+                     (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
                      a.spill_lo, a.dense_len, W, a.nwin, k.d, (unsigned long long *)a.stage_b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (a.stage_b)

@@ -37,7 +37,7 @@ struct LaunchArgs {
   bool vec;             // every column 16-byte aligned: dwordx4 loads
   uint32_t lds_bins;    // dense bins [0, lds_bins) privatised in LDS
   uint64_t dense_len;
-  uint64_t *spill;      // per-workgroup spill lists, or null
+  uint32_t *spill;      // per-workgroup spill lists (u32 entries), or null
   uint32_t spill_cap;
   uint32_t *spill_count;
   uint32_t win_shift, nwin, win_blocks;  // fold windows of 2^win_shift bins

@@ -169,7 +169,7 @@ struct gpuagg_ctx {
   std::vector<std::array<hipEvent_t, 3>> pending_events;  // start, after aggregate, after fold
   uint32_t n_cu = 256;
   // dense spill lists (per workgroup) for bins beyond the LDS window
-  uint64_t *d_spill = nullptr;
+  uint32_t *d_spill = nullptr;
   size_t spill_alloc = 0;
   uint32_t *d_spill_count = nullptr;
   size_t spill_count_alloc = 0;
@@ -440,7 +440,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       // bins past the LDS window: per-workgroup spill lists bucketed by fold window
       const uint64_t rem = c->dense_len - a.lds_bins;
       const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
-      const uint64_t cap = 2 * a.chunk / nwin + 4096;  // overflow falls back to global atomics
+      // overflow falls back to global atomics; a multiple of 4 keeps lists 16-byte aligned
+      const uint64_t cap = ((2 * a.chunk / nwin + 4096) + 3) & ~3ULL;
       if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
         a.spill_cap = (uint32_t)cap;
         const size_t need = (size_t)a.blocks * nwin * a.spill_cap;

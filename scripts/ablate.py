@@ -29,7 +29,12 @@ FWD = W.LOCAL_FWD_DROP[:2]
 DROP = W.LOCAL_FWD_DROP[2:]
 
 
+ONLY = set(filter(None, os.environ.get("ABLATE_ONLY", "").split(",")))
+
+
 def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0):
+    if ONLY and name not in ONLY:
+        return
     g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
                max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags)
     g.reconcile(spec)
@@ -47,7 +52,7 @@ def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0):
     g.close()
     ms = st["kernel_ms"] / max(1, st["kernel_launches"])
     fold = st["fold_ms"] / max(1, st["kernel_launches"])
-    print(json.dumps({"variant": name, "records": n, "launch_ms": ms, "fold_ms": fold, "wall_ms": wall * 1e3,
+    print(json.dumps({"lib": os.path.basename(os.environ.get("GPUAGG_LIB", "")), "variant": name, "records": n, "launch_ms": ms, "fold_ms": fold, "wall_ms": wall * 1e3,
                       "grec_s": n / ms / 1e6, "hbm_frac_16B": 16 * n / (ms * 1e-3) / 8e12}), flush=True)
 
 
