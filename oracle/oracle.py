@@ -257,8 +257,22 @@ def decode_packet(raw: bytes) -> Flow:
     return f
 
 
-# struct packet of dropreason (drop_reason.c:39-54, Go kprobePacket): decoded by
-# dropReason.processRecord (dropreason_linux.go:345-386): obs forced to 2, DROPPED.
+# struct packet of dropreason (drop_reason.c:39-54, Go kprobePacket): 32 bytes
+# little-endian: src_ip, dst_ip, src_port, dst_port, skb_len, return_val, drop_type,
+# proto, in_filtermap, ts.
+DROP_STRUCT = struct.Struct("<IIHHIIHBBQ")
+assert DROP_STRUCT.size == 32
+
+
+def decode_drop(raw: bytes) -> Flow:
+    """dropReason.processRecord decode (dropreason_linux.go:345-386): HostToNetShort on
+    both ports, ToFlow(..., obs 2, DROPPED), AddDropReason(drop_type), AddPacketSize(skb_len)."""
+    src, dst, sport, dport, skb_len, _ret, drop_type, proto, _infm, _ts = DROP_STRUCT.unpack(raw)
+    return drop_flow(int2ip(src), int2ip(dst), host_to_net_short(sport), host_to_net_short(dport),
+                     proto, drop_type, skb_len)
+
+
+# dropReason.processRecord after the decode: obs forced to 2, DROPPED.
 def drop_flow(src_ip: str, dst_ip: str, sport: int, dport: int, proto: int,
               drop_type: int, skb_len: int) -> Flow:
     f = to_flow(src_ip, dst_ip, sport, dport, proto, 2, VERDICT_DROPPED)

@@ -142,10 +142,11 @@ constexpr uint32_t kLdsByteLimit = 1u << 24;
 constexpr uint64_t kLdsCountOne = 1ULL << kLdsCountShift;
 constexpr uint64_t kLdsBytesMask = kLdsCountOne - 1;
 constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^20, multiple of 4
-// fold windows: 2^14 u64 bins (128 KiB of LDS) so a spilled bin's window is a shift.
-// Spill entries are u32: the bin's offset in its window (14 bits) | bytes << 14; a
-// packet of >= 2^18 bytes adds its bytes with a global atomic and spills 0.
-constexpr uint32_t kFoldWindowShift = 14, kFoldWindowBins = 1u << kFoldWindowShift;
+// fold windows: 2^13 u64 bins (64 KiB of LDS, two fold workgroups per CU) so a spilled
+// bin's window is a shift.  Spill entries are u32: the bin's offset in its window
+// (13 bits) | bytes << 13; a packet of >= 2^19 bytes adds its bytes with a global
+// atomic and spills 0.
+constexpr uint32_t kFoldWindowShift = 13, kFoldWindowBins = 1u << kFoldWindowShift;
 constexpr uint32_t kSpillByteLimit = 1u << (32 - kFoldWindowShift);
 
 // ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------

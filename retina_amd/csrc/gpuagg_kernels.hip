@@ -564,6 +564,13 @@ struct L4Ctx {
   uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
   uint32_t dummy;  // this lane's dummy word: absorbs predicated-off updates
   DevDense d;
+  // Does the add of (count 1, bytes nb) that returned `old` need fix()?  Branch-free:
+  // callers OR this over all their adds and take the slow path once per wave.
+  static __device__ __forceinline__ bool fix_needed(bool valid, uint32_t old, uint32_t nb) {
+    const uint32_t b = nb < kL4ByteLimit ? nb : 0u;
+    return valid & (((old & kL4BytesMask) + b > kL4BytesMask) | (old >= 0xFFE00000u) |
+                    (nb >= kL4ByteLimit));
+  }
   // Exact correction after a packed add (count:12 | bytes:20) returned `old`: a carry
   // out of the bytes field, a wrap of the count field, or a packet too big for the
   // field is booked into the global counters.  Rare; the test is 3 VALU ops.
@@ -632,8 +639,8 @@ __device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t f
 // receives exactly one value.
 struct SpillQ {
   uint32_t e0, e1, e2;  // queued entries: slots (ss | sd << 16), bytes, meta
-  uint32_t r0, r1, r2;  // this push's permuted values (wrap-around part on overflow)
   uint32_t n;           // queued entries (wave-uniform), lanes [0, n)
+  uint32_t r0, r1, r2;  // this push's permuted values (wrap-around part on overflow)
   // push; returns true when the queue holds 64 entries (caller flushes, then next())
   __device__ __forceinline__ bool push(bool v, uint32_t lane, uint32_t a0, uint32_t a1, uint32_t a2) {
     const uint64_t m = __ballot(v);
@@ -652,12 +659,7 @@ struct SpillQ {
     return n >= 64;
   }
   // after flushing a full queue: the wrapped entries become the queue
-  __device__ __forceinline__ void next() {
-    e0 = r0;
-    e1 = r1;
-    e2 = r2;
-    n -= 64;
-  }
+  __device__ __forceinline__ void next() { e0 = r0; e1 = r1; e2 = r2; n -= 64; }
 };
 
 // R records of one thread through every group (tier-1).  Group-outer / record-inner:
@@ -721,8 +723,8 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
     for (int k = 0; k < R; ++k) {
       const bool hit = verdict[k] == want;
       const uint32_t sub = f == FAM_DROP ? reason[k] : 0u;
-      vd[k] = hit && sd[k] != kIplNoSlot;
-      vs[k] = hit && ss[k] != kIplNoSlot;
+      vd[k] = hit & (sd[k] != kIplNoSlot);  // '&': no short-circuit branches
+      vs[k] = hit & (ss[k] != kIplNoSlot);
       bd[k] = rd[k] + sub;
       bs[k] = rs[k] + sub;
     }
@@ -735,10 +737,16 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
           od[k] = atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], add);
           os[k] = atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], add);
         }
+        bool need = false;
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-          l4.fix(vd[k], od[k], nbytes[k], bd[k]);
-          l4.fix(vs[k], os[k], nbytes[k], bs[k]);
+        for (int k = 0; k < R; ++k)
+          need |= L4Ctx::fix_needed(vd[k], od[k], nbytes[k]) | L4Ctx::fix_needed(vs[k], os[k], nbytes[k]);
+        if (__builtin_expect(__ballot(need) != 0, 0)) {  // rare: a carry, a wrap or a jumbo size
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            l4.fix(vd[k], od[k], nbytes[k], bd[k]);
+            l4.fix(vs[k], os[k], nbytes[k], bs[k]);
+          }
         }
       } else {
 #pragma unroll
@@ -797,7 +805,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
   const DenseGroups<NG, SIG> G(a.p, L4);
   const uint32_t seed = a.ipl_seed;
-  SpillQ q{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  SpillQ q{};
   // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
   auto q_flush = [&](bool full) {
     const bool valid = full || lane < q.n;
@@ -835,7 +843,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
       uint32_t sl[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = act ? ipl_slot(vals, j[k]) : kIplNoSlot;
+      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
       const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
       const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
       if (!G.any_spilled) {
@@ -857,7 +865,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
 #pragma unroll
         for (int g = 0; g < NG; ++g)
           if (G.fam[g] != FAM_COUNT && !G.inl[g]) need |= fam_hit(G.fam[g], ver, fm);
-        need = need && x0 != 0xFFFFFFFFu;  // some side is a pod
+        need = need & (x0 != 0xFFFFFFFFu);  // some side is a pod
         if (q.push(need, lane, x0, y0, z0)) {
           q_flush(true);
           q.next();
@@ -908,16 +916,17 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
 
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.
 // List (A-workgroup l, window w) holds only window w's updates, so every entry is read
-// once.  Workgroups of one partition share blockIdx % 8 (one XCD under the observed
-// round-robin placement -- speed only).
+// once.  Workgroup b folds window b % nwin over partition b / nwin of the lists; with
+// W = 8192 bins (64 KB of LDS) two workgroups fit a CU, and the runtime sizes the grid
+// to 2 x CUs so the fold runs in a single wave of the chip.
 __global__ __launch_bounds__(1024) void spill_window_kernel(
     const uint32_t *spill, const uint32_t *spill_count, uint32_t n_lists,
     uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d,
     unsigned long long *stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
   const uint32_t b = blockIdx.x;
-  const uint32_t w = (b >> 3) % nwin;
-  const uint32_t part = (b & 7u) + 8u * (b / (8u * nwin));
+  const uint32_t w = b % nwin;
+  const uint32_t part = b / nwin;
   const uint32_t nparts = gridDim.x / nwin;
   const uint64_t lo = (uint64_t)lo0 + (uint64_t)w * W;
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
@@ -1011,7 +1020,7 @@ __global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long
   if (w >= nwin || lo0 + (uint64_t)off >= dense_len) return;
   unsigned long long cnt = 0, byt = 0;
   for (uint32_t part = 0; part < nparts; ++part) {
-    const uint32_t b = (part & 7u) + 8u * (w + nwin * (part >> 3));  // inverse of the fold map
+    const uint32_t b = part * nwin + w;  // inverse of the fold map
     const unsigned long long v = stage[(size_t)b * W + i];
     cnt += v >> kLdsCountShift;
     byt += v & kLdsBytesMask;

@@ -453,7 +453,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         a.nwin = nwin;
         a.spill_lo = a.lds_bins;
         a.win_shift = kFoldWindowShift;
-        a.win_blocks = nwin * 8u * std::max<uint32_t>(1u, (32u + nwin - 1) / nwin);
+        a.win_blocks = nwin * std::max<uint32_t>(1u, 2u * c->n_cu / nwin);  // one wave of 2 per CU
         // fold partials are stored (not atomically added) and summed by a reduce pass
         const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
         if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;

@@ -7,6 +7,7 @@ prints one JSON line per variant with the HIP-event time per launch:
   drop      drop_count/bytes    (dense, LDS window + spill lists + fold)
   c2        forward + drop      (the bench spec)
   c2-1kpods C2 spec with 1k pods (every dense bin in LDS, no spill)
+  c4-zipf   C2 spec on C4's Zipf(1.2) records (LDS atomic contention)
   *-hbm-ip-table  same with FLAG_NO_LDS_IP_TABLE (IP table in HBM, u64 LDS bins)
   remote    C1 remote spec (sparse table)
 """
@@ -71,6 +72,10 @@ def main():
     cols_s, _ = gen_device_records(n, small, 3, dev, {})
     run("c2-1kpods", W.LOCAL_FWD_DROP, small, cols_s, n)
     del cols_s
+    if not ONLY or "c4-zipf" in ONLY:  # C4: Zipf(1.2) source pods, heavy-hitter bins
+        cols_z, _ = gen_device_records(n, pods, 4, dev, dict(W.CONFIGS["c4"]["gen"]))
+        run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
+        del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
 
 
