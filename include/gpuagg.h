@@ -160,6 +160,42 @@ int gpuagg_submit(gpuagg_ctx *ctx, gpuagg_batch *batch, size_t n);
 /* Device-resident submit: the columns already live in this ctx's device memory. */
 int gpuagg_submit_device(gpuagg_ctx *ctx, const gpuagg_columns *dev_cols, size_t n);
 
+/* ------------------------------------------------------------------------------
+ * Raw perf records: the producers' eBPF output structs, decoded on
+ * the GPU into the columns above instead of by the Go workers' binary.Read + ToFlow.
+ *
+ *  GPUAGG_RAW_PACKET  struct packet of packetparser, 72 bytes little-endian
+ *                     (pkg/plugin/conntrack/_cprog/conntrack.c:34-49), decoded as
+ *                     packetParser.processRecord (packetparser_linux.go:571-631):
+ *                     verdict FORWARDED, TrafficDirection = traffic_direction,
+ *                     IsReply = is_reply != 0, TCP flags for proto 6 only, ports
+ *                     byte-swapped (utils.HostToNetShort, utils_linux.go:65-70).
+ *  GPUAGG_RAW_DROP    struct packet of dropreason, 32 bytes little-endian
+ *                     (pkg/plugin/dropreason/_cprog/drop_reason.c:39-54), decoded as
+ *                     dropReason.processRecord (dropreason_linux.go:345-386): verdict
+ *                     DROPPED, INGRESS (obs 2), DropReason = drop_type, Bytes = skb_len.
+ *
+ * Raw buffers are n back-to-back records (RawSample payloads), 16-byte aligned.
+ * A traffic_direction > 3 or drop_type > 7 does not fit the meta word (the eBPF
+ * programs emit 0..2 and 0..6): such a row gets verdict 255, which no metric consumes
+ * (the sketches still count its 5-tuple), and is counted in
+ * gpuagg_stats.decode_out_of_range (read at gpuagg_sync); a host re-renders it.
+ * ---------------------------------------------------------------------------- */
+#define GPUAGG_RAW_PACKET 1
+#define GPUAGG_RAW_DROP 2
+#define GPUAGG_RAW_PACKET_SIZE 72
+#define GPUAGG_RAW_DROP_SIZE 32
+
+/* Decode only: device raw records -> caller's device columns (ports / dns_id may be
+ * NULL; dns_id is filled with 0xFFFFFFFF).  Async on the ctx's stream. */
+int gpuagg_decode_device(gpuagg_ctx *ctx, int kind, const void *dev_raw, size_t n,
+                         const gpuagg_columns *dev_out);
+/* Decode device raw records into the ctx's own columns and aggregate them (async). */
+int gpuagg_submit_raw_device(gpuagg_ctx *ctx, int kind, const void *dev_raw, size_t n);
+/* Host-fed: copies n raw records (72 or 32 B each) to HBM, decodes and aggregates;
+ * returns once host_raw may be reused (the packetparser/dropreason reader's batch). */
+int gpuagg_submit_raw(gpuagg_ctx *ctx, int kind, const void *host_raw, size_t n);
+
 /* Wait for every submitted batch. */
 int gpuagg_sync(gpuagg_ctx *ctx);
 
@@ -227,6 +263,10 @@ typedef struct gpuagg_stats {
   double kernel_ms;          /* summed device time of the aggregation kernel (HIP events) */
   double fold_ms;            /* summed device time of the spill fold kernel          */
   uint32_t last_kernel;      /* kernel of the last launch: GPUAGG_KERNEL_*           */
+  uint64_t decoded;          /* raw records decoded on the GPU                       */
+  uint64_t decode_out_of_range; /* decoded rows with a field beyond the meta word (at sync) */
+  uint64_t decode_launches;  /* timed decode launches                                */
+  double decode_ms;          /* summed device time of the decode kernels (HIP events)   */
 } gpuagg_stats;
 
 #define GPUAGG_KERNEL_NONE 0u          /* nothing launched yet                        */

@@ -32,6 +32,18 @@ def pack_meta(proto: int, verdict: int, tdir: int = 0, reason: int = 0, flags: i
             | ((flags & 0x3F) << 21) | ((is_reply & 1) << 27) | ((dns_type & 3) << 28))
 
 
+def pack_meta_np(proto, verdict, tdir=0, reason=0, flags=0, is_reply=0, dns_type=0) -> np.ndarray:
+    """pack_meta over numpy arrays (fields masked to their widths)."""
+    u = np.uint32
+
+    def f(x, mask, shift):
+        return (np.asarray(x).astype(u) & u(mask)) << u(shift)
+    return (f(proto, 0xFF, META_PROTO_SHIFT) | f(verdict, 0xFF, META_VERDICT_SHIFT)
+            | f(tdir, 3, META_TDIR_SHIFT) | f(reason, 7, META_REASON_SHIFT)
+            | f(flags, 0x3F, META_FLAGS_SHIFT) | f(is_reply, 1, META_REPLY_SHIFT)
+            | f(dns_type, 3, META_DNSTYPE_SHIFT))
+
+
 @dataclass
 class DnsEntry:
     """One DNS label payload as the producer saw it (dns_linux.go:138)."""

@@ -58,7 +58,13 @@ class StateDesc(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("batches", C.c_uint64), ("sparse_entries", C.c_uint64),
                 ("sparse_dropped", C.c_uint64), ("kernel_launches", C.c_uint64),
-                ("kernel_ms", C.c_double), ("fold_ms", C.c_double), ("last_kernel", C.c_uint32)]
+                ("kernel_ms", C.c_double), ("fold_ms", C.c_double), ("last_kernel", C.c_uint32),
+                ("decoded", C.c_uint64), ("decode_out_of_range", C.c_uint64),
+                ("decode_launches", C.c_uint64), ("decode_ms", C.c_double)]
+
+
+RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
+RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32}
 
 
 KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel"}
@@ -79,6 +85,9 @@ SIGNATURES = [
     ("gpuagg_free_batch", None, [C.c_void_p, C.POINTER(Batch)]),
     ("gpuagg_submit", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_size_t]),
     ("gpuagg_submit_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t]),
+    ("gpuagg_decode_device", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.POINTER(Columns)]),
+    ("gpuagg_submit_raw_device", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    ("gpuagg_submit_raw", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     ("gpuagg_sync", C.c_int, [C.c_void_p]),
     ("gpuagg_reset", C.c_int, [C.c_void_p]),
     ("gpuagg_snapshot", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),

@@ -37,6 +37,8 @@ GA_HD uint32_t meta_dnstype(uint32_t m) { return (m >> 28) & 3u; }
 
 constexpr uint32_t kVerdictForwarded = 1, kVerdictDropped = 2, kVerdictRetrans = 15,
                    kVerdictDns = 16;
+// decoded raw row whose field does not fit the meta word: no metric consumes it
+constexpr uint32_t kVerdictUnencodable = 255;
 constexpr uint32_t kDnsQuery = 1, kDnsResponse = 2;
 // kernel flag bits (pkg/plugin/packetparser/types_linux.go:22-31)
 constexpr uint32_t kFin = 1, kSyn = 2, kRst = 4, kPsh = 8, kAck = 16, kUrg = 32;

@@ -53,6 +53,21 @@ struct LaunchArgs {
   uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
 };
 
+// Raw perf-record decode (gpuagg_decode.hip); kinds match GPUAGG_RAW_* of gpuagg.h.
+enum RawKind : int { kRawPacket = 1, kRawDrop = 2 };
+struct OutCols {
+  uint32_t *src_ip, *dst_ip, *bytes, *meta, *ports, *dns_id;  // ports / dns_id may be null
+};
+struct DecodeArgs {
+  int kind;
+  const void *raw;         // 16-byte aligned device pointer
+  size_t n;                // records
+  OutCols out;
+  uint64_t *out_of_range;  // device counter: fields that do not fit the meta word
+  uint32_t n_cu;
+};
+hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
+
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between);
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);

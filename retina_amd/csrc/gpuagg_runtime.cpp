@@ -178,6 +178,11 @@ struct gpuagg_ctx {
   size_t stage_a_alloc = 0;
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
+  // raw perf-record decode (gpuagg_decode.hip)
+  uint8_t *d_raw = nullptr;  // device copy of host-fed raw records
+  size_t raw_alloc = 0;
+  uint64_t *d_decode_oor = nullptr;  // out-of-range field counter
+  std::vector<std::array<hipEvent_t, 2>> pending_decode;  // decode start, end
 };
 
 // ------------------------------------------------------------------------------------
@@ -282,6 +287,7 @@ void ctx_values(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, 
 
 int ensure_staging(gpuagg_ctx *c, size_t cap) {
   if (cap <= c->staging_cap) return GPUAGG_OK;
+  if (c->staging_cap) hipStreamSynchronize(c->stream);  // in-flight launches may read the old columns
   for (auto &p : c->d_cols) dev_free(p);
   for (auto &p : c->d_cols) {
     int rc = dev_alloc(c, &p, cap);
@@ -338,7 +344,17 @@ void drain_timing(gpuagg_ctx *c) {
     for (hipEvent_t e : ev) hipEventDestroy(e);
   }
   c->pending_events.clear();
+  for (auto &ev : c->pending_decode) {
+    float ms = 0.f;
+    if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) {
+      c->stats.decode_ms += ms;
+      c->stats.decode_launches += 1;
+    }
+    for (hipEvent_t e : ev) hipEventDestroy(e);
+  }
+  c->pending_decode.clear();
 }
+
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
@@ -478,6 +494,43 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   return GPUAGG_OK;
 }
 
+// Decodes n raw records at dev_raw into `out` on the ctx's stream (timed when enabled).
+int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols &out) {
+  if (kind != kRawPacket && kind != kRawDrop) return fail(c, GPUAGG_EINVAL, "unknown raw record kind %d", kind);
+  if (n == 0) return GPUAGG_OK;
+  if (!dev_raw || ((uintptr_t)dev_raw & 15u)) return fail(c, GPUAGG_EINVAL, "raw records must be 16-byte aligned");
+  if (!out.src_ip || !out.dst_ip || !out.bytes || !out.meta) return fail(c, GPUAGG_EINVAL, "decode: null column");
+  if (!c->d_decode_oor) {
+    if (int rc = dev_alloc(c, &c->d_decode_oor, 1)) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_decode_oor, 0, 8, c->stream));
+  }
+  std::array<hipEvent_t, 2> ev{};
+  if (c->timing) {
+    for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+  }
+  DecodeArgs a{kind, dev_raw, n, out, c->d_decode_oor, c->n_cu};
+  HIPCHK(c, launch_decode(a, c->stream));
+  if (c->timing) {
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->pending_decode.push_back(ev);
+  }
+  c->stats.decoded += n;
+  return GPUAGG_OK;
+}
+
+// Decodes into the ctx's column staging and aggregates from there.
+int decode_and_launch(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n) {
+  int rc;
+  if ((rc = ensure_staging(c, n))) return rc;
+  const OutCols out{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3],
+                    (c->plan.need_ports || c->cms_len > 0) ? c->d_cols[4] : nullptr,
+                    c->plan.need_dns ? c->d_cols[5] : nullptr};
+  if ((rc = decode(c, kind, dev_raw, n, out))) return rc;
+  ColsView cv{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3], c->d_cols[4], c->d_cols[5]};
+  return launch(c, cv, n);
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -546,6 +599,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_spill_count);
   dev_free(c->d_stage_a);
   dev_free(c->d_stage_b);
+  dev_free(c->d_raw);
+  dev_free(c->d_decode_oor);
   for (auto &p : c->d_cols) dev_free(p);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -948,6 +1003,37 @@ int gpuagg_sync(gpuagg_ctx *c) {
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   drain_timing(c);
+  if (c->d_decode_oor)
+    HIPCHK(c, hipMemcpy(&c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
+  return GPUAGG_OK;
+}
+
+int gpuagg_decode_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const gpuagg_columns *d) {
+  if (!c || !d) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  return decode(c, kind, dev_raw, n, OutCols{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id});
+}
+
+int gpuagg_submit_raw_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n) {
+  if (!c) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  return decode_and_launch(c, kind, dev_raw, n);
+}
+
+int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
+  if (!c || (n && !host_raw)) return GPUAGG_EINVAL;
+  if (kind != kRawPacket && kind != kRawDrop) return fail(c, GPUAGG_EINVAL, "unknown raw record kind %d", kind);
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
+  const size_t rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
+  if ((rc = ensure_buf(c, &c->d_raw, &c->raw_alloc, n * rec))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_raw, host_raw, n * rec, hipMemcpyHostToDevice, c->stream));
+  if ((rc = decode_and_launch(c, kind, c->d_raw, n))) return rc;
+  // like gpuagg_submit: the raw staging is reused by the next call
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return GPUAGG_OK;
 }
 

@@ -228,6 +228,27 @@ class GpuAgg:
     def submit_device(self, cols: "_abi.Columns", n: int) -> None:
         self._check(self.lib.gpuagg_submit_device(self.h, C.byref(cols), n))
 
+    # -- raw perf records (gpuagg_decode.hip) ----------------------------------------
+    def decode_device(self, kind: int, raw_ptr: int, n: int, out: "_abi.Columns") -> None:
+        """Decode n raw records (device pointer) into device columns, async."""
+        self._check(self.lib.gpuagg_decode_device(self.h, kind, C.c_void_p(raw_ptr), n, C.byref(out)))
+
+    def submit_raw_device(self, kind: int, raw_ptr: int, n: int) -> None:
+        """Decode + aggregate n raw records already in this device's HBM, async."""
+        self._check(self.lib.gpuagg_submit_raw_device(self.h, kind, C.c_void_p(raw_ptr), n))
+
+    def submit_raw(self, kind: int, raw: np.ndarray, chunk: int = 1 << 22) -> None:
+        """Host-fed raw records (a uint8 buffer of n * record-size bytes)."""
+        size = _abi.RAW_SIZE[kind]
+        raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
+        if raw.size % size:
+            raise ValueError("raw buffer is not a whole number of %d-byte records" % size)
+        n = raw.size // size
+        for a in range(0, n, chunk):
+            m = min(chunk, n - a)
+            part = raw[a * size:(a + m) * size]
+            self._check(self.lib.gpuagg_submit_raw(self.h, kind, part.ctypes.data_as(C.c_void_p), m))
+
     def sync(self) -> None:
         self._check(self.lib.gpuagg_sync(self.h))
 

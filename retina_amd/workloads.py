@@ -182,6 +182,110 @@ def gen_records(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, drop_fr
                    payloads)
 
 
+# ---- raw perf records (GPUAGG_RAW_*) --------------------------------------
+# struct packet of packetparser (conntrack.c:34-49) and of dropreason (drop_reason.c:39-54)
+RAW_PACKET_DTYPE = np.dtype({
+    "names": ["t_nsec", "bytes", "src_ip", "dst_ip", "src_port", "dst_port", "seq", "ack_num",
+              "tsval", "tsecr", "obs", "tdir", "proto", "flags", "is_reply", "pad",
+              "bytes_fwd", "bytes_rep", "pkts_fwd", "pkts_rep"],
+    "formats": ["<u8", "<u4", "<u4", "<u4", "<u2", "<u2", "<u4", "<u4", "<u4", "<u4",
+                "u1", "u1", "u1", "u1", "u1", ("u1", 3), "<u8", "<u8", "<u4", "<u4"],
+    "offsets": [0, 8, 12, 16, 20, 22, 24, 28, 32, 36, 40, 41, 42, 43, 44, 45, 48, 56, 64, 68],
+    "itemsize": 72})
+RAW_DROP_DTYPE = np.dtype({
+    "names": ["src_ip", "dst_ip", "src_port", "dst_port", "skb_len", "return_val", "drop_type",
+              "proto", "in_filtermap", "ts"],
+    "formats": ["<u4", "<u4", "<u2", "<u2", "<u4", "<u4", "<u2", "u1", "u1", "<u8"],
+    "offsets": [0, 4, 8, 10, 12, 16, 20, 22, 23, 24],
+    "itemsize": 32})
+
+
+def gen_raw_packets(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, udp_frac: float = 0.10,
+                    other_proto_frac: float = 0.02, odd_frac: float = 0.0,
+                    out_of_range_frac: float = 0.0) -> np.ndarray:
+    """n packetparser perf records (72 B each) as a uint8 buffer.  Fields the decode
+    ignores (timestamps, TCP sequence/timestamp options, conntrack counters, padding)
+    are random.  odd_frac: raw flag bytes with ECE/CWR bits, is_reply bytes other than
+    0/1, observation points 4..255, traffic direction 0 or 3.  out_of_range_frac:
+    traffic direction 4..255 (beyond the meta word; the eBPF program never emits it)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    r = np.zeros(n, RAW_PACKET_DTYPE)
+    for f, hi in (("t_nsec", 1 << 62), ("seq", 1 << 32), ("ack_num", 1 << 32), ("tsval", 1 << 32),
+                  ("tsecr", 1 << 32), ("bytes_fwd", 1 << 40), ("bytes_rep", 1 << 40),
+                  ("pkts_fwd", 1 << 32), ("pkts_rep", 1 << 32)):
+        r[f] = rng.integers(0, hi, n, dtype=np.uint64)
+    r["pad"] = rng.integers(0, 256, (n, 3), dtype=np.uint8)
+    r["src_ip"] = _pick_ips(rng, n, pods, pod_frac, None)
+    r["dst_ip"] = _pick_ips(rng, n, pods, pod_frac, None)
+    r["bytes"] = rng.integers(64, 1501, n, dtype=np.uint32)
+    r["src_port"] = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    r["dst_port"] = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    pr = rng.random(n)
+    proto = np.full(n, PROTO_TCP, np.uint8)
+    proto[pr < udp_frac] = PROTO_UDP
+    proto[(pr >= udp_frac) & (pr < udp_frac + other_proto_frac)] = PROTO_ICMP
+    r["proto"] = proto
+    r["obs"] = rng.integers(0, 4, n, dtype=np.uint8)
+    r["tdir"] = rng.integers(1, 3, n, dtype=np.uint8)
+    flags = FLAG_COMBOS[rng.integers(0, len(FLAG_COMBOS), n)].astype(np.uint8)
+    r["flags"] = np.where(proto == PROTO_TCP, flags, np.uint8(1))  # UDP: always 1 (conntrack.c:46)
+    r["is_reply"] = rng.integers(0, 2, n, dtype=np.uint8)
+    if odd_frac:
+        o = rng.random(n) < odd_frac
+        k = rng.integers(0, 4, n)
+        r["flags"] = np.where(o & (k == 0), rng.integers(0, 256, n, dtype=np.uint8), r["flags"])
+        r["is_reply"] = np.where(o & (k == 1), rng.integers(2, 256, n, dtype=np.uint8), r["is_reply"])
+        r["obs"] = np.where(o & (k == 2), rng.integers(4, 256, n, dtype=np.uint8), r["obs"])
+        r["tdir"] = np.where(o & (k == 3), rng.choice(np.array([0, 3], np.uint8), n), r["tdir"])
+    if out_of_range_frac:
+        o = rng.random(n) < out_of_range_frac
+        r["tdir"] = np.where(o, rng.integers(4, 256, n, dtype=np.uint8), r["tdir"])
+    return r.view(np.uint8).reshape(-1)
+
+
+def gen_raw_drops(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, udp_frac: float = 0.2,
+                  out_of_range_frac: float = 0.0) -> np.ndarray:
+    """n dropreason perf records (32 B each) as a uint8 buffer; drop_type uniform over
+    the drop_reason.h enum 0..6, or 8..65535 for out_of_range_frac of the rows."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    r = np.zeros(n, RAW_DROP_DTYPE)
+    r["src_ip"] = _pick_ips(rng, n, pods, pod_frac, None)
+    r["dst_ip"] = _pick_ips(rng, n, pods, pod_frac, None)
+    r["src_port"] = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    r["dst_port"] = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    r["skb_len"] = rng.integers(40, 9001, n, dtype=np.uint32)
+    r["return_val"] = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    r["drop_type"] = rng.integers(0, 7, n, dtype=np.uint16)
+    r["proto"] = np.where(rng.random(n) < udp_frac, np.uint8(PROTO_UDP), np.uint8(PROTO_TCP))
+    r["in_filtermap"] = rng.integers(0, 2, n, dtype=np.uint8)
+    r["ts"] = rng.integers(0, 1 << 62, n, dtype=np.uint64)
+    if out_of_range_frac:
+        o = rng.random(n) < out_of_range_frac
+        r["drop_type"] = np.where(o, rng.integers(8, 1 << 16, n, dtype=np.uint16), r["drop_type"])
+    return r.view(np.uint8).reshape(-1)
+
+
+def raw_packets_torch(src, dst, nbytes, meta, ports):
+    """Device-side encoder for large batches: packetparser records whose decode yields
+    the given columns (verdict FORWARDED, is_reply from meta bit 27, TCP flags from meta).
+    Returns an int32 tensor [n, 18] (72-byte records) on the columns' device."""
+    import torch
+    n = src.shape[0]
+    w = torch.zeros((n, 18), dtype=torch.int32, device=src.device)
+    m = meta.to(torch.int64) & 0xFFFFFFFF
+    p = ports.to(torch.int64) & 0xFFFFFFFF
+    sp, dp = p & 0xFFFF, p >> 16
+    sw = lambda x: ((x & 0xFF) << 8) | (x >> 8)  # noqa: E731 -- HostToNetShort is an involution
+    proto, tdir, flags = m & 0xFF, (m >> 16) & 3, (m >> 21) & 0x3F
+    w[:, 2] = nbytes
+    w[:, 3] = src
+    w[:, 4] = dst
+    w[:, 5] = (sw(sp) | (sw(dp) << 16)).to(torch.int32)
+    w[:, 10] = (2 | (tdir << 8) | (proto << 16) | (flags << 24)).to(torch.int32)  # obs 2
+    w[:, 11] = ((m >> 27) & 1).to(torch.int32)
+    return w
+
+
 # ---- named configs ---------------------------------------------------------------------
 
 LOCAL_FWD_DROP = [

@@ -10,6 +10,8 @@ prints one JSON line per variant with the HIP-event time per launch:
   c4-zipf   C2 spec on C4's Zipf(1.2) records (LDS atomic contention)
   *-hbm-ip-table  same with FLAG_NO_LDS_IP_TABLE (IP table in HBM, u64 LDS bins)
   remote    C1 remote spec (sparse table)
+  raw-packet  decode of 72-byte packetparser records (C2 columns re-encoded) + C2 forward
+              aggregation; decode_ms is the decode kernel, 92 B/record of HBM traffic
 """
 
 import json
@@ -77,6 +79,32 @@ def main():
         run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
         del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+    if not ONLY or "raw-packet" in ONLY:
+        run_raw(pods, cols, n)
+
+
+def run_raw(pods, cols, n, steps=5):
+    from retina_amd import _abi
+    raw = W.raw_packets_torch(*cols[:5])
+    g = GpuAgg(device=0, max_slots=len(pods.endpoints) + 16, max_ips=2 * len(pods.endpoints) + 16)
+    g.reconcile(FWD)
+    g.load_endpoints(pods.endpoints)
+    g.submit_raw_device(_abi.RAW_PACKET, raw.data_ptr(), n)
+    g.sync()
+    g.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.submit_raw_device(_abi.RAW_PACKET, raw.data_ptr(), n)
+    g.sync()
+    wall = (time.perf_counter() - t0) / steps
+    st = g.stats()
+    g.close()
+    dec = st["decode_ms"] / max(1, st["decode_launches"])
+    agg = st["kernel_ms"] / max(1, st["kernel_launches"])
+    print(json.dumps({"variant": "raw-packet", "records": n, "decode_ms": dec, "launch_ms": agg,
+                      "wall_ms": wall * 1e3, "decode_grec_s": n / dec / 1e6,
+                      "decode_gbs": 92 * n / (dec * 1e-3) / 1e9,
+                      "decode_hbm_frac": 92 * n / (dec * 1e-3) / 8e12}), flush=True)
 
 
 if __name__ == "__main__":
