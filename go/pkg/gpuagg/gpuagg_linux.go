@@ -52,6 +52,22 @@ type Record struct {
 	SrcIP, DstIP, Bytes, Meta, Ports, DNSID uint32
 }
 
+// Raw perf-record kinds (GPUAGG_RAW_* of include/gpuagg.h): packetparser and
+// dropreason hand their perf.Record.RawSample bytes to WriteRaw and skip
+// binary.Read + utils.ToFlow (packetparser_linux.go:571-631, dropreason_linux.go:345-386);
+// the engine decodes them on the GPU.
+const (
+	RawPacket = int(C.GPUAGG_RAW_PACKET) // 72-byte struct packet, conntrack.c:34-49
+	RawDrop   = int(C.GPUAGG_RAW_DROP)   // 32-byte struct packet, drop_reason.c:39-54
+)
+
+var rawSize = map[int]int{RawPacket: int(C.GPUAGG_RAW_PACKET_SIZE), RawDrop: int(C.GPUAGG_RAW_DROP_SIZE)}
+
+type rawSample struct {
+	kind int
+	b    []byte
+}
+
 type gpuAgg struct {
 	cfg *kcfg.Config
 	l   *log.ZapLogger
@@ -61,6 +77,8 @@ type gpuAgg struct {
 	batch   *C.gpuagg_batch
 	n       int
 	records chan Record
+	raw     chan rawSample
+	rawBuf  map[int][]byte // per kind: back-to-back raw records awaiting submit
 	vecs    map[string]*prometheus.GaugeVec
 }
 
@@ -70,7 +88,8 @@ func init() {
 
 // New is the registry.PluginFunc (registry.go:37).
 func New(cfg *kcfg.Config) registry.Plugin {
-	return &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, 1<<16)}
+	return &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, 1<<16),
+		raw: make(chan rawSample, 1<<16), rawBuf: map[int][]byte{}}
 }
 
 func (g *gpuAgg) Name() string                           { return name }
@@ -146,6 +165,16 @@ func (g *gpuAgg) Reconcile(spec *api.MetricsSpec) error {
 // Write is what producers call per decoded record (Enricher.Write's replacement).
 func (g *gpuAgg) Write(r Record) { g.records <- r }
 
+// WriteRaw takes one perf RawSample of the given kind; a sample of the wrong size is
+// refused like binary.Read's size mismatch (dropreason_linux.go:347-352).
+func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
+	if sz, ok := rawSize[kind]; !ok || len(sample) != sz {
+		return fmt.Errorf("gpuagg: raw sample of %d bytes for kind %d", len(sample), kind)
+	}
+	g.raw <- rawSample{kind, sample}
+	return nil
+}
+
 // Start blocks until ctx is done (PluginManager runs it in an errgroup goroutine,
 // pluginmanager.go:166-169).
 func (g *gpuAgg) Start(ctx context.Context) error {
@@ -166,10 +195,32 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		g.n = 0
 		return err
 	}
+	submitRaw := func(kind int) error {
+		buf := g.rawBuf[kind]
+		if len(buf) == 0 {
+			return nil
+		}
+		g.mu.Lock()
+		defer g.mu.Unlock()
+		// gpuagg_submit_raw copies the records to HBM before it returns
+		err := check(g, C.gpuagg_submit_raw(g.ctx, C.int(kind), unsafe.Pointer(&buf[0]),
+			C.size_t(len(buf)/rawSize[kind])), "gpuagg_submit_raw")
+		g.rawBuf[kind] = buf[:0]
+		return err
+	}
+	submitAll := func() error {
+		err := submit()
+		for kind := range rawSize {
+			if e := submitRaw(kind); e != nil && err == nil {
+				err = e
+			}
+		}
+		return err
+	}
 	for {
 		select {
 		case <-ctx.Done():
-			return submit()
+			return submitAll()
 		case r := <-g.records:
 			src[g.n], dst[g.n], byt[g.n], meta[g.n], ports[g.n], dns[g.n] = r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID
 			g.n++
@@ -178,8 +229,15 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 					g.l.Error("submit failed", zap.Error(err))
 				}
 			}
+		case s := <-g.raw:
+			g.rawBuf[s.kind] = append(g.rawBuf[s.kind], s.b...)
+			if len(g.rawBuf[s.kind]) >= batchCapacity*rawSize[s.kind] {
+				if err := submitRaw(s.kind); err != nil {
+					g.l.Error("raw submit failed", zap.Error(err))
+				}
+			}
 		case <-flush.C:
-			if err := submit(); err != nil {
+			if err := submitAll(); err != nil {
 				g.l.Error("submit failed", zap.Error(err))
 			}
 		case <-epoch.C:
