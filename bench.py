@@ -9,6 +9,13 @@ the records already resident in HBM.  Weak scaling: every rank aggregates its ow
 all-reduce (the per-scrape-epoch merge).
 
     python bench.py [--gpus N --steps K --warmup W --config c2 --records R]
+
+Other BASELINE.json configs (parity-test cases; bench lines under profiles/):
+  --config c3   2^27 records per GPU (2^30 on 8 GPUs), C2 metrics + count-min
+                (d=4, w=2^20) over the 5-tuple + HLL p=14 of distinct dst per source pod;
+                counters, count-min (sum) and HLL registers (max) merged per timed region
+  --config c4   C2 with Zipf(1.2) source pods (atomic contention on heavy hitters)
+  --config c5   10M records, 100k pods: tcpflags + retransmits + DNS request/response
 """
 
 from __future__ import annotations
@@ -27,7 +34,24 @@ sys.path.insert(0, ROOT)
 
 METRIC = "flow records/sec aggregated (node, 1/2/4/8 GPU); % of HBM peak GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BYTES_PER_RECORD = 16  # src_ip, dst_ip, bytes, meta
+# Algorithmic bytes per record: the columns the enabled metrics read.
+BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c5": 24}
+
+
+def bench_spec(name: str):
+    """(metric spec, sketch kwargs, workload text) of a BASELINE.json config."""
+    from retina_amd import workloads as W
+    c2txt = "local context, per-pod forward count/bytes + drop-reason histogram [namespace, podname]"
+    if name == "c1":
+        return W.C1_LOCAL, {}, "C1 spec: local context [ip, namespace, podname, workload], forward + drop"
+    if name == "c3":
+        return W.LOCAL_FWD_DROP, dict(cms_depth=4, cms_width_log2=20, hll_precision=14), (
+            "C3: " + c2txt + " + count-min d=4 w=2^20 over the 5-tuple + HLL p=14 distinct dst per source pod")
+    if name == "c4":
+        return W.LOCAL_FWD_DROP, {}, "C4: Zipf(1.2) source pods, " + c2txt
+    if name == "c5":
+        return W.C5_SPEC, {}, "C5: tcpflags + tcp retransmission + DNS request/response, local context [namespace, podname]"
+    return W.LOCAL_FWD_DROP, {}, "C2: " + c2txt
 
 
 def log(*a):
@@ -104,18 +128,27 @@ def main():
 
     cfg = W.CONFIGS[args.config]
     n = args.records or cfg["records"]
+    if args.config == "c3" and not args.records:
+        n = cfg["records"] // 8  # 2^30 records over the 8 GPUs of a node; weak scaling per GPU
     gen_kw = dict(cfg["gen"])
-    spec = W.LOCAL_FWD_DROP
+    spec, sketch, workload = bench_spec(args.config)
+    bpr = BYTES_PER_RECORD[args.config]
     pods = W.make_pods(cfg["pods"], seed=cfg["seed"])
     t0 = time.time()
-    cols, _ = gen_device_records(n, pods, cfg["seed"] + 7919 * rank, device, gen_kw)
+    # DNS ids index one generated dictionary: C5 is generated as a single chunk
+    chunk = n if args.config == "c5" else 8_000_000
+    cols, last = gen_device_records(n, pods, cfg["seed"] + 7919 * rank, device, gen_kw, chunk=chunk)
     torch.cuda.synchronize()
     log("rank %d: %d records resident in HBM (%.1f s)" % (rank, n, time.time() - t0))
 
+    # C5's DNS series are sparse keys (one per query payload and side): a 2^24-slot table
     g = GpuAgg(device=local_rank, remote_context=False, max_slots=cfg["pods"] + 16,
-               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=16)
+               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=24 if args.config == "c5" else 16,
+               **sketch)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
+    for p in last.dns:
+        g.dns_intern(p.rcode, p.qtypes, p.query, p.ips, p.num_answers)
     dcols = GpuAgg.device_columns(*cols)
 
     for _ in range(args.warmup):
@@ -123,10 +156,14 @@ def main():
     g.sync()
 
     st = g.state()
-    dense_cnt = dense_byt = None
+    merge = []  # (tensor view of engine state, reduce op) merged once per timed region
     if world > 1:
-        dense_cnt = device_view(st.dense_count, st.dense_len, "<i8", device)
-        dense_byt = device_view(st.dense_bytes, st.dense_len, "<i8", device)
+        merge = [(device_view(st.dense_count, st.dense_len, "<i8", device), dist.ReduceOp.SUM),
+                 (device_view(st.dense_bytes, st.dense_len, "<i8", device), dist.ReduceOp.SUM)]
+        if st.cms_len:
+            merge.append((device_view(st.cms, st.cms_len, "<i4", device), dist.ReduceOp.SUM))
+        if st.hll_len:
+            merge.append((device_view(st.hll, st.hll_len, "|u1", device), dist.ReduceOp.MAX))
 
     # ---- timed region --------------------------------------------------------------
     if world > 1:
@@ -138,15 +175,16 @@ def main():
     for _ in range(args.steps):
         g.submit_device(dcols, n)
     g.sync()
-    if world > 1:  # per-epoch merge over RCCL/xGMI: sum of u64 counters
-        dist.all_reduce(dense_cnt)
-        dist.all_reduce(dense_byt)
+    for t_, op in merge:  # per-epoch merge over RCCL/xGMI: sum counters/count-min, max HLL
+        dist.all_reduce(t_, op=op)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     stats = g.stats()
     g.set_timing(False)
+    if stats["sparse_dropped"]:
+        raise RuntimeError("group-by table overflowed (%d updates lost)" % stats["sparse_dropped"])
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -154,7 +192,7 @@ def main():
 
     kernel_ms = stats["kernel_ms"] / max(1, stats["kernel_launches"])
     fold_ms = stats["fold_ms"] / max(1, stats["kernel_launches"])
-    achieved = BYTES_PER_RECORD * n / (kernel_ms * 1e-3) / 1e9
+    achieved = bpr * n / (kernel_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc):
@@ -177,13 +215,11 @@ def main():
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": "C2: %d-record batch per GPU, %d pods, local context, per-pod "
-                        "forward count/bytes + drop-reason histogram [namespace, podname]"
-                        % (n, cfg["pods"]),
+            "workload": "%s; %d-record batch per GPU, %d pods" % (workload, n, cfg["pods"]),
             "records_per_gpu": n,
             "pods": cfg["pods"],
             "metrics": [s["metric_name"] for s in spec],
-            "parallelism": "dp%d (records sharded, counters all-reduced once per timed region)" % world,
+            "parallelism": "dp%d (records sharded, state all-reduced once per timed region)" % world,
         },
         "roofline": {
             "bound": "hbm",
@@ -195,11 +231,14 @@ def main():
             "kernel": _abi.KERNEL_NAMES.get(int(stats["last_kernel"])),
             "kernel_ms": kernel_ms,
             "other_kernels_ms": fold_ms,
-            "bytes_per_record": BYTES_PER_RECORD,
+            "bytes_per_record": bpr,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, args.cpu_sample, cfg["seed"], gen_kw)
+        sample = min(args.cpu_sample, 2_000_000) if args.config == "c5" else args.cpu_sample
+        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, sample, cfg["seed"], gen_kw)
+        if sketch:
+            result["cpu_baseline"]["sample"] += " (metrics only: the sketches have no reference CPU path)"
     g.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

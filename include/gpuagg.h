@@ -258,7 +258,7 @@ typedef struct gpuagg_stats {
   uint64_t records;          /* rows submitted                                   */
   uint64_t batches;          /* batches submitted                                */
   uint64_t sparse_entries;   /* occupied group-by table entries (at last sync)   */
-  uint64_t sparse_dropped;   /* updates lost to a full group-by table            */
+  uint64_t sparse_dropped;   /* updates lost to a full group-by table (at sync)  */
   uint64_t kernel_launches;  /* timed aggregation launches                       */
   double kernel_ms;          /* summed device time of the aggregation kernel (HIP events) */
   double fold_ms;            /* summed device time of the spill fold kernel          */
@@ -267,6 +267,8 @@ typedef struct gpuagg_stats {
   uint64_t decode_out_of_range; /* decoded rows with a field beyond the meta word (at sync) */
   uint64_t decode_launches;  /* timed decode launches                                */
   double decode_ms;          /* summed device time of the decode kernels (HIP events)   */
+  uint64_t sketch_launches;  /* timed sketch passes (count-min scatter + fold, HLL)    */
+  double sketch_ms;          /* summed device time of the sketch passes              */
 } gpuagg_stats;
 
 #define GPUAGG_KERNEL_NONE 0u          /* nothing launched yet                        */

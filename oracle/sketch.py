@@ -63,3 +63,18 @@ def hll_estimate(reg: np.ndarray) -> float:
     if e <= 2.5 * m and zeros:
         e = m * np.log(m / zeros)
     return float(e)
+
+
+def cms_estimate(cms: np.ndarray, src, dst, ports, proto) -> np.ndarray:
+    """Count-min point queries (min over rows) for arrays of 5-tuples."""
+    depth, width = cms.shape
+    lo = np.asarray(src).astype(U64) | (np.asarray(dst).astype(U64) << U64(32))
+    hi = np.asarray(ports).astype(U64) | (np.asarray(proto).astype(U64) << U64(32))
+    base = fmix64(lo ^ fmix64(hi ^ CMS_SEED))
+    est = None
+    with np.errstate(over="ignore"):
+        for r in range(depth):
+            col = (fmix64(base + U64(r + 1) * CMS_STEP) & U64(width - 1)).astype(np.int64)
+            v = cms[r, col].astype(np.int64)
+            est = v if est is None else np.minimum(est, v)
+    return est

@@ -60,7 +60,8 @@ class Stats(C.Structure):
                 ("sparse_dropped", C.c_uint64), ("kernel_launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("fold_ms", C.c_double), ("last_kernel", C.c_uint32),
                 ("decoded", C.c_uint64), ("decode_out_of_range", C.c_uint64),
-                ("decode_launches", C.c_uint64), ("decode_ms", C.c_double)]
+                ("decode_launches", C.c_uint64), ("decode_ms", C.c_double),
+                ("sketch_launches", C.c_uint64), ("sketch_ms", C.c_double)]
 
 
 RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)

@@ -345,6 +345,26 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
   }
 }
 
+// HLL register max for (source pod slot, dst): register h >> (64 - p), rank
+// clz((h << p) | 2^(p-1)) + 1.  The register word is read first and the CAS loop runs
+// only when the rank is larger (rare once a pod's registers have warmed up).
+__device__ __forceinline__ void hll_update(uint32_t *hll, uint32_t p, int32_t slot, uint32_t dip) {
+  const uint64_t h = hll_hash(dip);
+  const uint32_t idx = (uint32_t)(h >> (64 - p));
+  const uint64_t w = (h << p) | (1ULL << (p - 1));
+  const uint32_t rho = (uint32_t)__builtin_clzll(w) + 1u;
+  const size_t byte = ((size_t)slot << p) + idx;
+  uint32_t *word = hll + (byte >> 2);
+  const uint32_t sh = (uint32_t)(byte & 3) * 8u;
+  uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (((old >> sh) & 0xFFu) < rho) {
+    const uint32_t nw = (old & ~(0xFFu << sh)) | (rho << sh);
+    const uint32_t prev = atomicCAS(word, old, nw);
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
 __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip, uint32_t dip,
                                               uint32_t ports, uint32_t proto, const Lk &ls) {
   if (sk.depth) {
@@ -353,22 +373,7 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
     for (uint32_t r = 0; r < sk.depth; ++r)
       atomicAdd(&sk.cms[((size_t)r << sk.wlog2) + cms_col(base, r, wmask)], 1u);
   }
-  if (sk.p && ls.slot >= 0) {
-    const uint64_t h = hll_hash(dip);
-    const uint32_t idx = (uint32_t)(h >> (64 - sk.p));
-    const uint64_t w = (h << sk.p) | (1ULL << (sk.p - 1));
-    const uint32_t rho = (uint32_t)__builtin_clzll(w) + 1u;
-    const size_t byte = ((size_t)ls.slot << sk.p) + idx;
-    uint32_t *word = sk.hll + (byte >> 2);
-    const uint32_t sh = (uint32_t)(byte & 3) * 8u;
-    uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (((old >> sh) & 0xFFu) < rho) {
-      const uint32_t nw = (old & ~(0xFFu << sh)) | (rho << sh);
-      const uint32_t prev = atomicCAS(word, old, nw);
-      if (prev == old) break;
-      old = prev;
-    }
-  }
+  if (sk.p && ls.slot >= 0) hll_update(sk.hll, sk.p, ls.slot, dip);
 }
 
 // ---- record streaming -------------------------------------------------------------
@@ -912,6 +917,127 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     }
   }
   spill_counts_out(a, bins + L4 + 64);
+}
+
+// ---- sketch pass (config C3): count-min by window partition, HLL direct -------------
+// Count-min updates are 4 random u32 adds per record into d x 2^w counters (16 MiB at
+// C3): as global atomics they run at the memory-side atomic rate (one 64-B request per
+// lane), ~40x slower than streaming.  Instead sketch_scatter_kernel appends each update's
+// column offset (u16) to a per-(workgroup, window) list -- a window is 2^15 columns of
+// one row -- with one LDS counter per window, and cms_fold_kernel adds one window's
+// lists into LDS and then into the row with coalesced 256-byte atomics.  Exact: an
+// update whose list is full falls back to its global atomic.
+struct SketchK {
+  const uint32_t *src, *dst, *ports, *meta;
+  uint64_t n, chunk;
+  DevIpTable t;
+  uint32_t *cms;
+  uint32_t depth, wlog2, wshift, nwin, cap;  // nwin = 0: every update is a global atomic
+  uint16_t *lists;   // [gridDim.x][nwin][cap]
+  uint32_t *counts;  // [gridDim.x][nwin]
+  uint32_t *hll;
+  uint32_t p;
+};
+
+__global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];  // [nwin] list fill counters
+  for (uint32_t i = threadIdx.x; i < k.nwin; i += blockDim.x) wcnt[i] = 0u;
+  __syncthreads();
+  const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
+  const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
+  const uint32_t wmask = (1u << k.wlog2) - 1u, hi_bits = k.wlog2 - k.wshift;
+  const uint32_t omask = (1u << k.wshift) - 1u;
+  uint16_t *mine = k.lists + (size_t)blockIdx.x * k.nwin * k.cap;
+  for (uint64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    const uint32_t s = k.src[i], d = k.dst[i];
+    if (k.depth) {
+      const uint64_t base = cms_base(s, d, k.ports[i], meta_proto(k.meta[i]));
+      for (uint32_t r = 0; r < k.depth; ++r) {
+        const uint32_t col = cms_col(base, r, wmask);
+        bool direct = k.nwin == 0;
+        if (!direct) {
+          const uint32_t w = (r << hi_bits) | (col >> k.wshift);
+          const uint32_t pos = atomicAdd(&wcnt[w], 1u);
+          direct = pos >= k.cap;
+          if (!direct) mine[(size_t)w * k.cap + pos] = (uint16_t)(col & omask);
+        }
+        if (direct) atomicAdd(&k.cms[((size_t)r << k.wlog2) + col], 1u);
+      }
+    }
+    if (k.p) {
+      const Lk ls = ip_lookup(k.t, s);
+      if (ls.slot >= 0) hll_update(k.hll, k.p, ls.slot, d);
+    }
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
+    k.counts[(size_t)blockIdx.x * k.nwin + w] = wcnt[w] < k.cap ? wcnt[w] : k.cap;
+}
+
+// Workgroup b folds window b % nwin over scatter workgroups [part*L/P, (part+1)*L/P).
+__global__ __launch_bounds__(1024) void cms_fold_kernel(SketchK k, uint32_t n_lists) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cwin[];  // [2^wshift]
+  const uint32_t W = 1u << k.wshift;
+  const uint32_t w = blockIdx.x % k.nwin, part = blockIdx.x / k.nwin, nparts = gridDim.x / k.nwin;
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) cwin[i] = 0u;
+  __syncthreads();
+  const uint32_t l0 = (uint32_t)((uint64_t)part * n_lists / nparts);
+  const uint32_t l1 = (uint32_t)((uint64_t)(part + 1) * n_lists / nparts);
+  for (uint32_t l = l0; l < l1; ++l) {
+    const uint32_t c = k.counts[(size_t)l * k.nwin + w];
+    const uint16_t *e = k.lists + ((size_t)l * k.nwin + w) * k.cap;  // 16-byte aligned (cap % 8 == 0)
+    const uint32_t n8 = c >> 3;
+    for (uint32_t j = threadIdx.x; j < n8; j += blockDim.x) {
+      const uint4 v = ((const uint4 *)e)[j];
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        atomicAdd(&cwin[x[q] & 0xFFFFu], 1u);
+        atomicAdd(&cwin[x[q] >> 16], 1u);
+      }
+    }
+    for (uint32_t j = (n8 << 3) + threadIdx.x; j < c; j += blockDim.x) atomicAdd(&cwin[e[j]], 1u);
+  }
+  __syncthreads();
+  const uint32_t hi_bits = k.wlog2 - k.wshift;
+  const uint32_t r = w >> hi_bits, colbase = (w & ((1u << hi_bits) - 1u)) << k.wshift;
+  uint32_t *row = k.cms + ((size_t)r << k.wlog2) + colbase;
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
+    const uint32_t v = cwin[i];
+    if (v) atomicAdd(&row[i], v);
+  }
+}
+
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  SketchK k{};
+  k.src = a.cols.src_ip;
+  k.dst = a.cols.dst_ip;
+  k.ports = a.cols.ports;
+  k.meta = a.cols.meta;
+  k.n = a.n;
+  k.chunk = a.chunk;
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed};
+  k.cms = a.cms;
+  k.depth = a.cms_depth;
+  k.wlog2 = a.cms_wlog2;
+  k.wshift = a.win_shift;
+  k.nwin = a.nwin;
+  k.cap = a.cap;
+  k.lists = a.lists;
+  k.counts = a.counts;
+  k.hll = (uint32_t *)a.hll;
+  k.p = a.hll_p;
+  hipLaunchKernelGGL(sketch_scatter_kernel, dim3(a.blocks), dim3(1024), (size_t)a.nwin * 4, st, k);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !a.nwin || !a.cms_depth) return e;
+  const size_t lds = (size_t)4 << a.win_shift;
+  if (lds > 64 * 1024 &&
+      (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
+  return hipGetLastError();
 }
 
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.

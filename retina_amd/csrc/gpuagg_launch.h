@@ -68,6 +68,25 @@ struct DecodeArgs {
 };
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
 
+// Sketch pass (count-min by window partition + HLL), after the metric kernels.
+struct SketchArgs {
+  ColsView cols;
+  size_t n;
+  uint64_t chunk;           // records per scatter workgroup
+  uint32_t blocks;          // scatter workgroups (= lists per window)
+  const uint64_t *ip_slots;
+  uint32_t ip_mask, ip_seed;
+  uint32_t *cms;
+  uint32_t cms_depth, cms_wlog2;
+  uint32_t win_shift, nwin, cap;  // windows of 2^win_shift columns; nwin 0: direct atomics
+  uint16_t *lists;
+  uint32_t *counts;
+  uint32_t fold_blocks;     // multiple of nwin
+  uint8_t *hll;
+  uint32_t hll_p;
+};
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
+
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between);
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);

@@ -183,6 +183,12 @@ struct gpuagg_ctx {
   size_t raw_alloc = 0;
   uint64_t *d_decode_oor = nullptr;  // out-of-range field counter
   std::vector<std::array<hipEvent_t, 2>> pending_decode;  // decode start, end
+  // sketch pass (count-min window lists)
+  uint16_t *d_sk_lists = nullptr;
+  size_t sk_lists_alloc = 0;
+  uint32_t *d_sk_counts = nullptr;
+  size_t sk_counts_alloc = 0;
+  std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch pass start, end
 };
 
 // ------------------------------------------------------------------------------------
@@ -353,6 +359,69 @@ void drain_timing(gpuagg_ctx *c) {
     for (hipEvent_t e : ev) hipEventDestroy(e);
   }
   c->pending_decode.clear();
+  for (auto &ev : c->pending_sketch) {
+    float ms = 0.f;
+    if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) {
+      c->stats.sketch_ms += ms;
+      c->stats.sketch_launches += 1;
+    }
+    for (hipEvent_t e : ev) hipEventDestroy(e);
+  }
+  c->pending_sketch.clear();
+}
+
+// Count-min windows: 2^15 columns (128 KiB of LDS in the fold); at most 4096 windows
+// (16 KiB of scatter counters), else every update is a direct global atomic.
+constexpr uint32_t kCmsWindowShift = 15, kCmsMaxWindows = 4096;
+
+// The sketch pass over n records: count-min scatter + fold, HLL direct (SketchArgs).
+int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
+  int rc;
+  SketchArgs s{};
+  s.ip_slots = c->d_ip;
+  s.ip_mask = (uint32_t)(c->ip_cap ? c->ip_cap - 1 : 0);
+  s.ip_seed = c->ip_seed;
+  s.cms = c->d_cms;
+  s.cms_depth = c->cms_len ? c->cfg.cms_depth : 0;
+  s.cms_wlog2 = c->cfg.cms_width_log2;
+  s.hll = c->d_hll;
+  s.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
+  s.blocks = c->n_cu;
+  s.win_shift = std::min<uint32_t>(kCmsWindowShift, s.cms_wlog2);
+  const uint64_t nwin = s.cms_depth ? ((uint64_t)s.cms_depth << (s.cms_wlog2 - s.win_shift)) : 0;
+  const uint64_t per_launch = (uint64_t)s.blocks << 20;  // <= 2^20 records per scatter workgroup
+  std::array<hipEvent_t, 2> ev{};
+  if (c->timing) {
+    for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+  }
+  for (uint64_t off = 0; off < n; off += per_launch) {
+    const uint64_t m = std::min<uint64_t>(per_launch, n - off);
+    s.cols = ColsView{cv.src_ip + off, cv.dst_ip + off, nullptr, cv.meta + off,
+                      cv.ports ? cv.ports + off : nullptr, nullptr};
+    s.n = m;
+    s.chunk = (m + s.blocks - 1) / s.blocks;
+    s.nwin = 0;
+    if (nwin && nwin <= kCmsMaxWindows) {
+      // expected entries per list = chunk * depth / nwin; +12.5 % + 2048 of headroom
+      // (overflow is exact but slow: it falls back to a global atomic)
+      const uint64_t mean = s.chunk * s.cms_depth / nwin;
+      const uint64_t cap = (mean + mean / 8 + 2048 + 7) & ~7ULL;
+      if ((rc = ensure_buf(c, &c->d_sk_lists, &c->sk_lists_alloc, (size_t)s.blocks * nwin * cap))) return rc;
+      if ((rc = ensure_buf(c, &c->d_sk_counts, &c->sk_counts_alloc, (size_t)s.blocks * nwin))) return rc;
+      s.nwin = (uint32_t)nwin;
+      s.cap = (uint32_t)cap;
+      s.lists = c->d_sk_lists;
+      s.counts = c->d_sk_counts;
+      s.fold_blocks = (uint32_t)nwin * std::max<uint32_t>(1u, c->n_cu / (uint32_t)nwin);
+    }
+    HIPCHK(c, launch_sketch(s, c->stream));
+  }
+  if (c->timing) {
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->pending_sketch.push_back(ev);
+  }
+  return GPUAGG_OK;
 }
 
 
@@ -377,6 +446,10 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.cms_wlog2 = c->cfg.cms_width_log2;
   a.hll = c->d_hll;
   a.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
+  // sketches run in their own pass (launch_sketches) so the metric groups keep the
+  // dense fast paths
+  a.cms_depth = 0;
+  a.hll_p = 0;
   // dense local-context fast path: every group dense, no sketches
   a.dense_ng = 0;
   if (c->plan.local && c->plan.ngroups > 0 && !a.cms_depth && !a.hll_p) {
@@ -431,7 +504,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.blocks = (a.lds_bins || a.tier1) ? c->n_cu : c->n_cu * 4;
   a.threads = (a.lds_bins || a.tier1) ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
-  for (uint64_t off = 0; off < n; off += per_launch) {
+  for (uint64_t off = 0; c->plan.ngroups > 0 && off < n; off += per_launch) {
     const uint64_t m = std::min<uint64_t>(per_launch, n - off);
     auto sh = [off](const uint32_t *p) { return p ? p + off : nullptr; };
     a.cols = ColsView{sh(cv.src_ip), sh(cv.dst_ip), sh(cv.bytes), sh(cv.meta), sh(cv.ports), sh(cv.dns_id)};
@@ -487,6 +560,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       c->pending_events.push_back(ev);
     }
   }
+  if ((c->cms_len || c->hll_len) && (rc = launch_sketches(c, cv, n))) return rc;
   c->stats.records += n;
   c->stats.batches += 1;
   c->stats.last_kernel = a.tier1 ? GPUAGG_KERNEL_DENSE_LDS_IP
@@ -600,6 +674,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_stage_a);
   dev_free(c->d_stage_b);
   dev_free(c->d_raw);
+  dev_free(c->d_sk_lists);
+  dev_free(c->d_sk_counts);
   dev_free(c->d_decode_oor);
   for (auto &p : c->d_cols) dev_free(p);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -1005,6 +1081,8 @@ int gpuagg_sync(gpuagg_ctx *c) {
   drain_timing(c);
   if (c->d_decode_oor)
     HIPCHK(c, hipMemcpy(&c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
+  if (c->sparse_slots)
+    HIPCHK(c, hipMemcpy(&c->stats.sparse_dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
 }
 

@@ -1,0 +1,96 @@
+"""Count-min and HyperLogLog on the GPU at the C3 sketch shape (d=4, w=2^20, p=14).
+
+* state bit-exact against the numpy restatement (oracle/sketch.py), through the
+  windowed count-min scatter/fold pass, including list overflow (Zipf-skewed 5-tuples
+  push single windows past their list capacity, which falls back to global atomics);
+* estimates within the stated bounds (BASELINE.json north_star): count-min never
+  under-counts and over-counts by more than eps*N = (e/w)*N for at most delta = e^-d of
+  the keys; HLL relative error per pod within 4 sigma, sigma = 1.04/sqrt(2^p).
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import sketch as S
+from retina_amd import workloads as W
+
+from .helpers import make_engine, to_device
+
+pytestmark = pytest.mark.gpu
+
+SPEC = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+
+
+def _run(recs, pods, gpu_device, d=4, w=20, p=14):
+    from retina_amd import GpuAgg
+    g = make_engine(pods, SPEC, False, gpu_device, cms_depth=d, cms_width_log2=w, hll_precision=p)
+    try:
+        g.submit_device(GpuAgg.device_columns(*to_device(recs, gpu_device)), len(recs))
+        g.sync()
+        return g.cms_array(), g.hll_array()
+    finally:
+        g.close()
+
+
+def _src_slots(pods, src):
+    ip_slot = {}
+    for s, ep in enumerate(pods.endpoints):
+        for ip in ep.ips:
+            ip_slot[int(ip)] = s
+    lut_ips = np.array(sorted(ip_slot), np.uint32)
+    lut_slot = np.array([ip_slot[int(x)] for x in lut_ips], np.int64)
+    pos = np.clip(np.searchsorted(lut_ips, src), 0, len(lut_ips) - 1)
+    return np.where(lut_ips[pos] == src, lut_slot[pos], -1)
+
+
+@pytest.mark.parametrize("zipf", [None, 1.2], ids=["uniform", "zipf"])
+def test_c3_shape_bit_exact(gpu_device, zipf):
+    pods = W.make_pods(200, seed=41)
+    recs = W.gen_records(3_000_000, pods, seed=42, udp_frac=0.2, zipf=zipf)
+    if zipf:  # heavy 5-tuples: repeat a few flows so some count-min windows overflow
+        hot = np.random.default_rng(1).integers(0, 64, len(recs)) == 0
+        recs.dst_ip[hot] = recs.dst_ip[0]
+        recs.src_ip[hot] = recs.src_ip[0]
+        recs.ports[hot] = recs.ports[0]
+    cms, hll = _run(recs, pods, gpu_device)
+    want = np.zeros((4, 1 << 20), np.uint32)
+    S.cms_update(want, recs.src_ip, recs.dst_ip, recs.ports, recs.meta & np.uint32(0xFF))
+    assert np.array_equal(cms, want)
+    want_h = np.zeros((len(pods.endpoints), 1 << 14), np.uint8)
+    S.hll_update(want_h, _src_slots(pods, recs.src_ip), recs.dst_ip, 14)
+    assert np.array_equal(hll[:len(pods.endpoints)], want_h)
+
+
+def test_count_min_bounds(gpu_device):
+    pods = W.make_pods(500, seed=43)
+    recs = W.gen_records(4_000_000, pods, seed=44, udp_frac=0.2, zipf=1.2)
+    cms, _ = _run(recs, pods, gpu_device)
+    key = np.stack([recs.src_ip, recs.dst_ip, recs.ports, recs.meta & np.uint32(0xFF)], 1)
+    uniq, true = np.unique(key, axis=0, return_counts=True)
+    est = S.cms_estimate(cms, uniq[:, 0], uniq[:, 1], uniq[:, 2], uniq[:, 3])
+    assert (est >= true).all()                      # count-min never under-counts
+    n, eps, delta = len(recs), math.e / (1 << 20), math.exp(-4)
+    frac_bad = float(np.mean(est - true > eps * n))
+    assert frac_bad <= delta, (frac_bad, delta)
+
+
+def test_hll_relative_error(gpu_device):
+    pods = W.make_pods(40, seed=45, secondary_frac=0.0)
+    n = 4_000_000
+    rng = np.random.default_rng(46)
+    recs = W.gen_records(n, pods, seed=46, pod_frac=1.0)
+    recs.dst_ip[:] = rng.integers(1, 1 << 32, n, dtype=np.uint64).astype(np.uint32)  # ~distinct dsts
+    _, hll = _run(recs, pods, gpu_device)
+    slot = _src_slots(pods, recs.src_ip)
+    sigma = 1.04 / math.sqrt(1 << 14)
+    errs = []
+    for s in range(len(pods.endpoints)):
+        true = len(np.unique(recs.dst_ip[slot == s]))
+        if true < 10_000:
+            continue
+        errs.append(abs(S.hll_estimate(hll[s]) - true) / true)
+    assert len(errs) >= 30
+    assert max(errs) <= 4 * sigma, max(errs)
+    assert float(np.mean(errs)) <= 1.5 * sigma
