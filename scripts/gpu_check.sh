@@ -14,7 +14,7 @@ python -c "import __graft_entry__ as g; g.build()" > "$OUT/${TAG}_build.log" 2>&
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -x > "$OUT/${TAG}_pytest.log" 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/${TAG}_pytest.log" 2>&1
       rc=$?; echo "pytest rc=$rc" >> "$OUT/${TAG}_pytest.log"
       [ $rc -gt 1 ] && exit $rc ;;
     smoke)
