@@ -88,10 +88,20 @@ def test_two_rank_merge_equals_single():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
+    # A fresh container can take minutes on each spawned rank's first `import torch`, so
+    # poll with a long overall deadline and fail fast only if a rank actually died.
+    import queue
+    import time
     res = {}
-    for _ in range(world):
-        rank, arrs, cms, hll, sparse = q.get(timeout=240)
-        res[rank] = (arrs, cms, hll, sparse)
+    deadline = time.monotonic() + 900
+    while len(res) < world:
+        try:
+            rank, arrs, cms, hll, sparse = q.get(timeout=10)
+            res[rank] = (arrs, cms, hll, sparse)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"gloo rank exited with {dead}"
+            assert time.monotonic() < deadline, "gloo ranks did not report within 900 s"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
