@@ -134,9 +134,11 @@ GA_HD uint32_t ip_h2(uint32_t ip, uint32_t seed) {
 // aggregates <= 2^20 records between flushes and an update carries < 2^24 bytes in
 // LDS (bigger packets add their bytes with a global atomic), so both fields are exact.
 // LDS layout: bins [0, L), 64 per-lane dummy words [L, L+64) that absorb predicated-
-// off updates, then 16 u32 spill-window counters.
+// off updates, then kMaxSpillWindows u32 spill-window counters.
 constexpr uint32_t kLdsBytes = 160 * 1024;
-constexpr uint32_t kMaxSpillWindows = 32;
+// 256 windows x 2^13 bins: dense spaces up to ~2M bins beyond the LDS prefix (C5's
+// 100k-pod tcpflags + retransmit groups) still fold in LDS instead of global atomics
+constexpr uint32_t kMaxSpillWindows = 256;
 constexpr uint32_t kLdsExtraWords = 64 + kMaxSpillWindows / 2;  // 64 dummies + u32 spill-window counters
 constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
 constexpr uint32_t kLdsCountShift = 44;
@@ -205,6 +207,9 @@ GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
 }
 
+// Sparse table slots are interleaved: k0 k1 k2 cnt byt + 3 pad words = one 64-byte
+// line per slot, so an insert's CAS / publish / adds touch one line, not five.
+constexpr uint32_t kSparseSlotWords = 8;
 // Sparse group-by key: k0 = occ | group<<59 | sub<<53 | s_slot1<<32 | s_ip
 //                      k1 = s_port17<<47 | d_port17<<30 | d_slot1<<9
 //                      k2 = d_ip<<32 | dns_id

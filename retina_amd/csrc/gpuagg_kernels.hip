@@ -107,22 +107,23 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
                                            uint64_t k2, uint64_t c, uint64_t b) {
   uint32_t h = (uint32_t)key_hash(k0, k1, k2) & s.mask;
   for (uint32_t probe = 0; probe < kSparseMaxProbe; ++probe) {
-    const unsigned long long cur = atomicCAS(&s.k0[h], 0ULL, (unsigned long long)k0);
+    const size_t o = (size_t)h * kSparseSlotWords;  // slot h's line (k1 = k0 + 1, ...)
+    const unsigned long long cur = atomicCAS(&s.k0[o], 0ULL, (unsigned long long)k0);
     if (cur == 0ULL) {
-      atomicExch(&s.k1[h], (unsigned long long)k1);
+      atomicExch(&s.k1[o], (unsigned long long)k1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      atomicExch(&s.k2[h], (unsigned long long)k2);  // publish
-      atomicAdd(&s.cnt[h], (unsigned long long)c);
-      if (b) atomicAdd(&s.byt[h], (unsigned long long)b);
+      atomicExch(&s.k2[o], (unsigned long long)k2);  // publish
+      atomicAdd(&s.cnt[o], (unsigned long long)c);
+      if (b) atomicAdd(&s.byt[o], (unsigned long long)b);
       return;
     }
     if (cur == k0) {
-      const unsigned long long c2 = atomicCAS(&s.k2[h], kKeyPending, kKeyPending);
+      const unsigned long long c2 = atomicCAS(&s.k2[o], kKeyPending, kKeyPending);
       if (c2 == k2) {
-        const unsigned long long c1 = atomicCAS(&s.k1[h], 0ULL, 0ULL);
+        const unsigned long long c1 = atomicCAS(&s.k1[o], 0ULL, 0ULL);
         if (c1 == k1) {
-          atomicAdd(&s.cnt[h], (unsigned long long)c);
-          if (b) atomicAdd(&s.byt[h], (unsigned long long)b);
+          atomicAdd(&s.cnt[o], (unsigned long long)c);
+          if (b) atomicAdd(&s.byt[o], (unsigned long long)b);
           return;
         }
       }
@@ -170,7 +171,7 @@ struct DenseSink {
   }
   // store one reserved spill entry (pos from the window counter); full list -> global
   __device__ __forceinline__ void spill_put(uint32_t bin, uint32_t w, uint32_t pos, uint32_t nbytes) const {
-    if (pos < spill_cap) {  // w < 32 and spill_cap < 2^24: 24-bit multiply
+    if (pos < spill_cap) {  // w < 256 and spill_cap < 2^24: 24-bit multiply
       spill[mul_u24(w, spill_cap) + pos] = entry(bin, nbytes);
       return;
     }
@@ -1070,6 +1071,27 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
     if (fast) atomicAdd(&win[off], kLdsCountOne | nb);
     else lds_add64_exact(&win[off], (uint32_t)lo + off, nb, d);
   };
+  // Short lists (many windows, e.g. C5's ~220: tens of entries per list) leave most of
+  // the workgroup idle and serialise on list latency, so each wave takes its own list;
+  // long lists (C2's drop windows: thousands of entries) keep the workgroup-wide loop.
+  const uint32_t lists_here = part < n_lists ? (n_lists - part + nparts - 1) / nparts : 0u;
+  if (total < (uint64_t)lists_here * 2048u) {
+    const uint32_t nwaves = blockDim.x >> 6, ln = threadIdx.x & 63u;
+    for (uint32_t l = part + (threadIdx.x >> 6) * nparts; l < n_lists; l += nwaves * nparts) {
+      const uint32_t cnt = spill_count[(size_t)l * nwin + w];
+      const uint32_t *e = spill + ((size_t)l * nwin + w) * spill_cap;
+      const uint4 *e4 = (const uint4 *)e;
+      const uint32_t n4 = cnt >> 2;
+      for (uint32_t j = ln; j < n4; j += 64) {
+        const uint4 v = e4[j];
+        add(v.x);
+        add(v.y);
+        add(v.z);
+        add(v.w);
+      }
+      for (uint32_t i = (n4 << 2) + ln; i < cnt; i += 64) add(e[i]);
+    }
+  } else {
   for (uint32_t l = part; l < n_lists; l += nparts) {
     const uint32_t cnt = spill_count[(size_t)l * nwin + w];
     const uint32_t *e = spill + ((size_t)l * nwin + w) * spill_cap;  // 16-byte aligned (cap % 4 == 0)
@@ -1097,6 +1119,7 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
     }
     for (uint32_t i = (n4 << 2) + threadIdx.x; i < cnt; i += blockDim.x) add(e[i]);
   }
+  }  // long lists
   __syncthreads();
   if (stage) {  // staged: this window partial, whole, for stage_reduce_b_kernel
     uint4 *dst = (uint4 *)(stage + ((size_t)b * W));
@@ -1158,23 +1181,24 @@ __global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long
 __global__ void sparse_init_kernel(unsigned long long *k2, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x)
-    k2[i] = kKeyPending;
+    k2[i * kSparseSlotWords] = kKeyPending;
 }
 
 __global__ void sparse_export_kernel(DevSparse s, size_t cap_slots, unsigned long long *out,
                                      size_t out_cap, unsigned long long *counter) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cap_slots;
        i += (size_t)gridDim.x * blockDim.x) {
-    const unsigned long long k0 = s.k0[i];
+    const size_t q = i * kSparseSlotWords;
+    const unsigned long long k0 = s.k0[q];
     if (!k0) continue;
     const unsigned long long pos = atomicAdd(counter, 1ULL);
     if (pos >= out_cap) continue;
     unsigned long long *o = out + pos * kSparseEntryWords;
     o[0] = k0;
-    o[1] = s.k1[i];
-    o[2] = s.k2[i];
-    o[3] = s.cnt[i];
-    o[4] = s.byt[i];
+    o[1] = s.k1[q];
+    o[2] = s.k2[q];
+    o[3] = s.cnt[q];
+    o[4] = s.byt[q];
   }
 }
 

@@ -309,10 +309,7 @@ int reset_state(gpuagg_ctx *c) {
     HIPCHK(c, hipMemsetAsync(c->d_dense_byt, 0, c->dense_len * 8, c->stream));
   }
   if (c->sparse_slots) {
-    HIPCHK(c, hipMemsetAsync(c->sv.k0, 0, c->sparse_slots * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->sv.k1, 0, c->sparse_slots * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->sv.cnt, 0, c->sparse_slots * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->sv.byt, 0, c->sparse_slots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->sv.k0, 0, c->sparse_slots * kSparseSlotWords * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->sv.dropped, 0, 8, c->stream));
     HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
   }
@@ -328,11 +325,14 @@ int ensure_sparse(gpuagg_ctx *c) {
   if (lg < 4 || lg > 30) return fail(c, GPUAGG_EINVAL, "sparse_capacity_log2 %u out of [4,30]", lg);
   const size_t n = (size_t)1 << lg;
   int rc;
-  if ((rc = dev_alloc(c, &c->sv.k0, n)) || (rc = dev_alloc(c, &c->sv.k1, n)) ||
-      (rc = dev_alloc(c, &c->sv.k2, n)) || (rc = dev_alloc(c, &c->sv.cnt, n)) ||
-      (rc = dev_alloc(c, &c->sv.byt, n)) || (rc = dev_alloc(c, &c->sv.dropped, 1)) ||
+  // one interleaved array: slot h = words [8h, 8h + 8) = k0 k1 k2 cnt byt pad (kSparseSlotWords)
+  if ((rc = dev_alloc(c, &c->sv.k0, n * kSparseSlotWords)) || (rc = dev_alloc(c, &c->sv.dropped, 1)) ||
       (rc = dev_alloc(c, &c->d_counter, 1)))
     return rc;
+  c->sv.k1 = c->sv.k0 + 1;
+  c->sv.k2 = c->sv.k0 + 2;
+  c->sv.cnt = c->sv.k0 + 3;
+  c->sv.byt = c->sv.k0 + 4;
   c->sv.mask = (uint32_t)(n - 1);
   c->sparse_slots = n;
   return GPUAGG_OK;
@@ -659,11 +659,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_ipl);
   dev_free(c->d_dense_cnt);
   dev_free(c->d_dense_byt);
-  dev_free(c->sv.k0);
-  dev_free(c->sv.k1);
-  dev_free(c->sv.k2);
-  dev_free(c->sv.cnt);
-  dev_free(c->sv.byt);
+  dev_free(c->sv.k0);  // k1, k2, cnt, byt point into the same array
   dev_free(c->sv.dropped);
   dev_free(c->d_counter);
   dev_free(c->d_export);
