@@ -1178,10 +1178,14 @@ __global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long
   if (byt) atomicAdd(&d.byt[lo0 + off], byt);
 }
 
-__global__ void sparse_init_kernel(unsigned long long *k2, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+// Writes every slot whole (k0 k1 = 0, k2 = pending, cnt byt pad = 0): four 16-byte
+// stores per 64-byte line, no separate memset.
+__global__ void sparse_init_kernel(unsigned long long *k0, size_t n) {
+  static_assert(kSparseSlotWords == 8, "one 64-byte line per slot");
+  ulonglong2 *v = (ulonglong2 *)k0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n * 4;
        i += (size_t)gridDim.x * blockDim.x)
-    k2[i * kSparseSlotWords] = kKeyPending;
+    v[i] = (i & 3) == 1 ? make_ulonglong2(kKeyPending, 0ULL) : make_ulonglong2(0ULL, 0ULL);
 }
 
 __global__ void sparse_export_kernel(DevSparse s, size_t cap_slots, unsigned long long *out,
@@ -1325,7 +1329,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
 
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st) {
   hipLaunchKernelGGL(sparse_init_kernel, dim3(2048), dim3(256), 0, st,
-                     (unsigned long long *)v.k2, slots);
+                     (unsigned long long *)v.k0, slots);
   return hipGetLastError();
 }
 

@@ -309,7 +309,6 @@ int reset_state(gpuagg_ctx *c) {
     HIPCHK(c, hipMemsetAsync(c->d_dense_byt, 0, c->dense_len * 8, c->stream));
   }
   if (c->sparse_slots) {
-    HIPCHK(c, hipMemsetAsync(c->sv.k0, 0, c->sparse_slots * kSparseSlotWords * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->sv.dropped, 0, 8, c->stream));
     HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
   }
@@ -501,8 +500,12 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.ipl_bytes = c->ipl_bytes;
     }
   }
-  a.blocks = (a.lds_bins || a.tier1) ? c->n_cu : c->n_cu * 4;
-  a.threads = (a.lds_bins || a.tier1) ? 1024 : 256;
+  // one 1024-thread workgroup per CU whenever LDS holds bins or spill counters: with
+  // dense bins but no LDS prefix (C5: 100k-pod groups) 4x fewer workgroups mean 4x
+  // fewer, longer spill lists for the fold (same 16 waves per CU)
+  const bool wide = a.lds_bins || a.tier1 || c->dense_len > 0;
+  a.blocks = wide ? c->n_cu : c->n_cu * 4;
+  a.threads = wide ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
   for (uint64_t off = 0; c->plan.ngroups > 0 && off < n; off += per_launch) {
     const uint64_t m = std::min<uint64_t>(per_launch, n - off);
