@@ -122,6 +122,10 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError("retina_amd: %s is missing; run __graft_entry__.build() "
                           "(there is no CPU fallback)" % path)
+    # One HIP runtime per process: PyTorch (device memory, streams, RCCL) must load its
+    # libamdhip64 before this library does, or torch's later HIP init finds no GPUs when
+    # the engine is created first (as smoke() does).
+    import torch  # noqa: F401
     lib = C.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
