@@ -1150,6 +1150,7 @@ __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *sta
   const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * blockIdx.y) / gridDim.y);
   const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (blockIdx.y + 1)) / gridDim.y);
   unsigned long long cnt = 0, byt = 0;
+#pragma unroll 8  // 8 independent copy loads in flight per lane
   for (uint32_t c = c0; c < c1; ++c) {
     const uint32_t w = stage[(size_t)c * stride + bin];
     cnt += packed ? (w >> kL4CountShift) : w;
@@ -1168,6 +1169,7 @@ __global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long
   const uint32_t w = off / W, i = off % W;
   if (w >= nwin || lo0 + (uint64_t)off >= dense_len) return;
   unsigned long long cnt = 0, byt = 0;
+#pragma unroll 8  // independent partial loads in flight per lane
   for (uint32_t part = 0; part < nparts; ++part) {
     const uint32_t b = part * nwin + w;  // inverse of the fold map
     const unsigned long long v = stage[(size_t)b * W + i];
