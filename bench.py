@@ -35,7 +35,10 @@ sys.path.insert(0, ROOT)
 METRIC = "flow records/sec aggregated (node, 1/2/4/8 GPU); % of HBM peak GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Algorithmic bytes per record: the columns the enabled metrics read.
-BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c5": 24}
+# C5's metrics (tcpflags, retransmits, DNS) count records only: src, dst, meta, dns_id.
+BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c5": 16}
+# the sketch pass reads src, dst, ports, meta (proto)
+SKETCH_BYTES_PER_RECORD = 16
 
 
 def bench_spec(name: str):
@@ -58,19 +61,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-class _CAI:
-    """__cuda_array_interface__ view of a raw device pointer (for RCCL merges)."""
-
-    def __init__(self, ptr, n, typestr):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
-                                         "version": 3, "strides": None}
-
-
-def device_view(ptr: int, n: int, typestr: str, device):
-    import torch
-    return torch.as_tensor(_CAI(ptr, n, typestr), device=device)
-
-
 def gen_device_records(n: int, pods, seed: int, device, gen_kw, chunk: int = 8_000_000):
     """Generates the workload on the host in chunks and keeps it resident in HBM."""
     import torch
@@ -87,19 +77,101 @@ def gen_device_records(n: int, pods, seed: int, device, gen_kw, chunk: int = 8_0
     return cols, r
 
 
-def cpu_baseline(cfg_name: str, pods, spec, sample: int, seed: int, gen_kw):
-    """The C port of the reference path (oracle/ref_cpu.c, go-shaped: dotted-string IPs,
-    string-keyed cache and label maps; enrich + every ProcessFlow per flow on one thread)
-    timed on a bounded sample of the same workload."""
+def _cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    # the GPU box grants a 16-CPU share of a larger machine (OMP_NUM_THREADS=16 there)
+    share = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
+    return model, os.cpu_count() or 1, max(1, min(avail, share))
+
+
+def cpu_baseline(cfg_name: str, pods, spec, seed: int, gen_kw, go_sample: int, tuned_sample: int,
+                 runs: int = 5):
+    """The C port of the reference path (oracle/ref_cpu.c) timed on this host, in the two
+    modes of SURVEY.md 8d / BASELINE.md, 1 warm-up + `runs` timed runs each, median:
+      go-shaped: dotted-string IPs, string-keyed cache and label maps, enrich + every
+                 ProcessFlow per flow on one thread (enricher.go:69-98,
+                 metrics_module.go:276-317);
+      tuned:     integer keys, every granted core, per-thread tables merged at the end.
+    `value` is the tuned median (the stronger CPU baseline)."""
     from oracle.ref_cpu import RefCPU
     from retina_amd import workloads as W
-    recs = W.gen_records(sample, pods, seed, **gen_kw)
-    r = RefCPU(spec, pods.endpoints, False, recs.dns)
-    dt = r.process(recs)
-    r.close()
-    return {"value": sample / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "%d records of config %s through oracle/ref_cpu.c (C port of enricher.go + "
-                      "metrics module, 1 thread), %.1f s" % (sample, cfg_name, dt)}
+    model, ncpu, threads = _cpu_info()
+    recs = W.gen_records(tuned_sample, pods, seed, **gen_kw)
+    go = W.Records(*(getattr(recs, k)[:go_sample] for k in ("src_ip", "dst_ip", "bytes", "meta",
+                                                              "ports", "dns_id")), recs.dns)
+
+    def timed(fn, n):
+        rates = []
+        for i in range(runs + 1):
+            r = RefCPU(spec, pods.endpoints, False, recs.dns)
+            dt = fn(r)
+            r.close()
+            if i:  # run 0 is the warm-up
+                rates.append(n / dt)
+        return float(np.median(rates)), rates
+
+    go_med, go_all = timed(lambda r: r.process(go), go_sample)
+    tu_med, tu_all = timed(lambda r: r.process_tuned(recs, threads), tuned_sample)
+    return {"value": tu_med, "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": "config %s through oracle/ref_cpu.c (C port of enricher.go + metrics module); "
+                      "tuned: %d records on %d threads; go-shaped: %d records on 1 thread; "
+                      "1 warm-up + %d timed runs each, median" % (cfg_name, tuned_sample, threads,
+                                                                 go_sample, runs),
+            "cpu_model": model, "nproc": ncpu,
+            "modes": {"tuned": {"value": tu_med, "threads": threads, "records": tuned_sample,
+                                "runs": tu_all},
+                      "go_shaped": {"value": go_med, "threads": 1, "records": go_sample,
+                                    "runs": go_all}}}
+
+
+def pmc_traffic(cfg_name: str, kernel: str):
+    """HBM bytes per launch from profiles/pmc_<config>.json, only if that file profiles
+    the kernel that ran (its `kernel` list holds rocprofv3 names containing `kernel`)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg_name)
+    if not os.path.exists(path):
+        return None, "no %s" % os.path.relpath(path, ROOT)
+    try:
+        pmc = json.load(open(path))
+    except ValueError:
+        return None, "unreadable %s" % os.path.relpath(path, ROOT)
+    names = pmc.get("kernel", [])
+    if not kernel or not any(kernel in k for k in names):
+        return None, "%s profiles %s, not %s: refused" % (os.path.relpath(path, ROOT), names, kernel)
+    return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
+
+
+def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = 1 << 22):
+    """Host-fed throughput: two pinned batches (pre-filled from the workload) submitted
+    alternately, gpuagg_submit's H2D copy of one overlapping the other's aggregation."""
+    import torch
+    n = min(batch, n_total)
+    hbs = [g.alloc_batch(n), g.alloc_batch(n)]
+    for k, hb in enumerate(hbs):
+        lo = (k * n) % max(1, n_total - n + 1)
+        for name, t in zip(("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"), cols):
+            getattr(hb, name)[:n] = t[lo:lo + n].cpu().numpy().view(np.uint32)
+    g.submit(hbs[0], n)
+    g.sync()
+    torch.cuda.synchronize()
+    reps = max(4, steps * 4)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        g.submit(hbs[k & 1], n)
+    g.sync()
+    dt = time.perf_counter() - t0
+    return {"value": reps * n / dt, "unit": "records/s", "batch_records": n, "batches": reps,
+            "note": "pinned host batches through gpuagg_submit (PCIe H2D included; not `value`)"}
 
 
 def main():
@@ -109,14 +181,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: config size)")
-    ap.add_argument("--cpu-sample", type=int, default=12_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=16_000_000,
+                    help="records in the tuned CPU baseline sample (go-shaped: 1/8 of it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-fed", action="store_true")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-    from retina_amd import GpuAgg, _abi
+    from retina_amd import GpuAgg
     from retina_amd import workloads as W
+    from retina_amd.dist import merge_engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -155,16 +230,6 @@ def main():
         g.submit_device(dcols, n)
     g.sync()
 
-    st = g.state()
-    merge = []  # (tensor view of engine state, reduce op) merged once per timed region
-    if world > 1:
-        merge = [(device_view(st.dense_count, st.dense_len, "<i8", device), dist.ReduceOp.SUM),
-                 (device_view(st.dense_bytes, st.dense_len, "<i8", device), dist.ReduceOp.SUM)]
-        if st.cms_len:
-            merge.append((device_view(st.cms, st.cms_len, "<i4", device), dist.ReduceOp.SUM))
-        if st.hll_len:
-            merge.append((device_view(st.hll, st.hll_len, "|u1", device), dist.ReduceOp.MAX))
-
     # ---- timed region --------------------------------------------------------------
     if world > 1:
         dist.barrier()
@@ -175,13 +240,14 @@ def main():
     for _ in range(args.steps):
         g.submit_device(dcols, n)
     g.sync()
-    for t_, op in merge:  # per-epoch merge over RCCL/xGMI: sum counters/count-min, max HLL
-        dist.all_reduce(t_, op=op)
+    if world > 1:  # per-epoch merge over RCCL/xGMI: dense + count-min sum, HLL max, sparse table
+        merge_engine(g)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     stats = g.stats()
+    kernel = g.kernel_name()
     g.set_timing(False)
     if stats["sparse_dropped"]:
         raise RuntimeError("group-by table overflowed (%d updates lost)" % stats["sparse_dropped"])
@@ -190,16 +256,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    kernel_ms = stats["kernel_ms"] / max(1, stats["kernel_launches"])
+    # roofline of the dominant kernel: the aggregation kernel, or (C3) the sketch pass
+    agg_ms = stats["kernel_ms"] / max(1, stats["kernel_launches"])
     fold_ms = stats["fold_ms"] / max(1, stats["kernel_launches"])
-    achieved = bpr * n / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch_corrected")
-        except Exception:
-            traffic = None
+    sk_ms = stats["sketch_ms"] / max(1, stats["sketch_launches"]) if stats["sketch_launches"] else 0.0
+    if sk_ms > agg_ms:
+        dom, dom_ms, dom_bpr = "sketch_scatter_kernel+cms_fold_kernel", sk_ms, SKETCH_BYTES_PER_RECORD
+        other_ms = agg_ms + fold_ms
+    else:
+        dom, dom_ms, dom_bpr = kernel, agg_ms, bpr
+        other_ms = fold_ms + sk_ms
+    achieved = dom_bpr * n / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.config, dom)
 
     result = {
         "metric": METRIC,
@@ -219,7 +287,7 @@ def main():
             "records_per_gpu": n,
             "pods": cfg["pods"],
             "metrics": [s["metric_name"] for s in spec],
-            "parallelism": "dp%d (records sharded, state all-reduced once per timed region)" % world,
+            "parallelism": "dp%d (records sharded, state merged once per timed region)" % world,
         },
         "roofline": {
             "bound": "hbm",
@@ -228,15 +296,19 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": _abi.KERNEL_NAMES.get(int(stats["last_kernel"])),
-            "kernel_ms": kernel_ms,
-            "other_kernels_ms": fold_ms,
-            "bytes_per_record": bpr,
+            "traffic_source": traffic_src,
+            "kernel": dom,
+            "kernel_ms": dom_ms,
+            "other_kernels_ms": other_ms,
+            "bytes_per_record": dom_bpr,
+            "step_bytes_per_record": bpr,
         },
     }
+    if rank == 0 and world == 1 and not args.no_host_fed:
+        result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample = min(args.cpu_sample, 2_000_000) if args.config == "c5" else args.cpu_sample
-        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, sample, cfg["seed"], gen_kw)
+        go_s, tu_s = (400_000, 4_000_000) if args.config == "c5" else (args.cpu_sample // 8, args.cpu_sample)
+        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s)
         if sketch:
             result["cpu_baseline"]["sample"] += " (metrics only: the sketches have no reference CPU path)"
     g.close()

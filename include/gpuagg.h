@@ -154,7 +154,9 @@ int gpuagg_alloc_batch(gpuagg_ctx *ctx, size_t capacity, gpuagg_batch **out);
 void gpuagg_free_batch(gpuagg_ctx *ctx, gpuagg_batch *batch);
 
 /* Host-fed submit: copies n rows to HBM and enqueues the aggregation.  Returns once
- * the batch's host buffers may be refilled; the aggregation itself runs async. */
+ * the batch's host buffers may be refilled (its H2D copies are complete); the
+ * aggregation itself runs async.  Two device staging buffers alternate, so the copy of
+ * the next batch (on a copy stream) overlaps the aggregation of this one. */
 int gpuagg_submit(gpuagg_ctx *ctx, gpuagg_batch *batch, size_t n);
 
 /* Device-resident submit: the columns already live in this ctx's device memory. */
@@ -242,6 +244,8 @@ typedef struct gpuagg_state_desc {
   uint32_t *cms;           size_t cms_len;      /* u32[cms_len]                */
   uint8_t *hll;            size_t hll_len;      /* u8[hll_len]                 */
   size_t sparse_entry_words;                    /* u64 words per exported entry */
+  size_t sparse_len;                            /* group-by table slots (0: none): an
+                                                   upper bound on exported entries */
 } gpuagg_state_desc;
 
 int gpuagg_state(gpuagg_ctx *ctx, gpuagg_state_desc *out);
@@ -269,6 +273,8 @@ typedef struct gpuagg_stats {
   double decode_ms;          /* summed device time of the decode kernels (HIP events)   */
   uint64_t sketch_launches;  /* timed sketch passes (count-min scatter + fold, HLL)    */
   double sketch_ms;          /* summed device time of the sketch passes              */
+  uint64_t async_returns;    /* host-fed submits that returned while their aggregation
+                                was still running (the double-buffered overlap)        */
 } gpuagg_stats;
 
 #define GPUAGG_KERNEL_NONE 0u          /* nothing launched yet                        */
@@ -281,6 +287,10 @@ int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
 int gpuagg_set_timing(gpuagg_ctx *ctx, int enabled);
 /* Returns the ctx's HIP stream (hipStream_t) as an opaque pointer. */
 void *gpuagg_stream(gpuagg_ctx *ctx);
+/* Signature of the aggregation kernel of the last launch, spelled as rocprofv3 names it
+ * (without "void gpuagg::" and the argument list), e.g. "dense_lds_kernel<2, true, 41u>";
+ * "" before the first launch.  Lets a profile be matched to the kernel that ran. */
+const char *gpuagg_kernel_name(const gpuagg_ctx *ctx);
 
 #ifdef __cplusplus
 }

@@ -112,6 +112,9 @@ typedef struct {
   smap_t ip_to_ep; /* dotted ip -> endpoint* */
   endpoint_t **eps;
   size_t neps;
+  /* tuned mode: integer IP -> endpoint index + 1 (last writer wins), open addressing */
+  uint32_t *ipk, *ipv;
+  size_t ipcap, nip;
   dns_t *dns;
   size_t ndns, dns_cap;
   metric_t m[32];
@@ -226,6 +229,45 @@ static void ip_str(uint32_t ip, char *b) {
   sprintf(b, "%u.%u.%u.%u", ip & 255u, (ip >> 8) & 255u, (ip >> 16) & 255u, ip >> 24);
 }
 
+/* tuned mode's integer IP index (value = endpoint index + 1; 0 = empty slot) */
+static uint32_t ip_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  return x ^ (x >> 16);
+}
+static void ip_put(ref_t *r, uint32_t ip, uint32_t v);
+static void ip_grow(ref_t *r) {
+  uint32_t *ok = r->ipk, *ov = r->ipv;
+  size_t oc = r->ipcap;
+  r->ipcap = oc ? 2 * oc : 1024;
+  r->ipk = calloc(r->ipcap, 4);
+  r->ipv = calloc(r->ipcap, 4);
+  r->nip = 0;
+  for (size_t i = 0; i < oc; ++i)
+    if (ov[i]) ip_put(r, ok[i], ov[i]);
+  free(ok);
+  free(ov);
+}
+static void ip_put(ref_t *r, uint32_t ip, uint32_t v) {
+  if (2 * (r->nip + 1) > r->ipcap) ip_grow(r);
+  size_t i = ip_mix(ip) & (r->ipcap - 1);
+  while (r->ipv[i] && r->ipk[i] != ip) i = (i + 1) & (r->ipcap - 1);
+  if (!r->ipv[i]) r->nip++;
+  r->ipk[i] = ip;
+  r->ipv[i] = v;
+}
+static uint32_t ip_get(const ref_t *r, uint32_t ip) {
+  if (!r->ipcap) return 0;
+  size_t i = ip_mix(ip) & (r->ipcap - 1);
+  while (r->ipv[i]) {
+    if (r->ipk[i] == ip) return r->ipv[i];
+    i = (i + 1) & (r->ipcap - 1);
+  }
+  return 0;
+}
+
 /* Cache.UpdateRetinaEndpoint restated for IP ownership: later writers own an IP. */
 int ref_add_endpoint(void *h, const char *ns, const char *pod, const char *wk_kind,
                      const char *wk_name, const uint32_t *ips, int nips) {
@@ -244,6 +286,7 @@ int ref_add_endpoint(void *h, const char *ns, const char *pod, const char *wk_ki
   for (int i = 0; i < nips; ++i) {
     ip_str(ips[i], b);
     smap_find(&r->ip_to_ep, b, 1)->val = e;
+    ip_put(r, ips[i], (uint32_t)r->neps); /* endpoint index + 1 */
   }
   return 0;
 }
@@ -465,6 +508,335 @@ int ref_process(void *h, const uint32_t *src, const uint32_t *dst, const uint32_
       if (r->m[k].active) process_metric(r, &r->m[k], &f);
   }
   return 0;
+}
+
+/* ---------------------------------------------------------------- tuned mode ----- *
+ * Same semantics as ref_process, with the per-flow work on integers: the IP cache is a
+ * u32-keyed table, every metric update is keyed by the integers its label values are a
+ * function of (endpoint index, IP, port, reason / flag / direction, DNS id), each thread
+ * accumulates its own range of records into its own table, and the tables are merged
+ * and rendered to label strings once at the end (the rendering mirrors process_metric).
+ */
+typedef struct {
+  /* w0 = metric | sub << 8 | tdir << 16 | dest << 18; w1..w3 source (ip, endpoint + 1,
+   * port | 0x10000); w4..w6 destination; w7 = dns id + 1 */
+  uint32_t w[8];
+} ikey_t;
+typedef struct {
+  ikey_t *k;
+  uint64_t *v; /* per key: count, bytes */
+  uint8_t *used;
+  size_t cap, n;
+} imap_t;
+
+static uint64_t ikey_hash(const ikey_t *k) {
+  uint64_t h = 0x9E3779B97F4A7C15ULL;
+  for (int i = 0; i < 8; i += 2) {
+    h ^= (uint64_t)k->w[i] | ((uint64_t)k->w[i + 1] << 32);
+    h *= 0xff51afd7ed558ccdULL;
+    h ^= h >> 29;
+  }
+  return h;
+}
+static void imap_add(imap_t *m, const ikey_t *k, uint64_t c, uint64_t b);
+static void imap_grow(imap_t *m) {
+  imap_t o = *m;
+  m->cap = o.cap ? 2 * o.cap : 4096;
+  m->n = 0;
+  m->k = malloc(m->cap * sizeof(ikey_t));
+  m->v = malloc(m->cap * 2 * sizeof(uint64_t));
+  m->used = calloc(m->cap, 1);
+  for (size_t i = 0; i < o.cap; ++i)
+    if (o.used[i]) imap_add(m, &o.k[i], o.v[2 * i], o.v[2 * i + 1]);
+  free(o.k);
+  free(o.v);
+  free(o.used);
+}
+static void imap_add(imap_t *m, const ikey_t *k, uint64_t c, uint64_t b) {
+  if (2 * (m->n + 1) > m->cap) imap_grow(m);
+  size_t i = ikey_hash(k) & (m->cap - 1);
+  for (;;) {
+    if (!m->used[i]) {
+      m->used[i] = 1;
+      m->k[i] = *k;
+      m->v[2 * i] = c;
+      m->v[2 * i + 1] = b;
+      m->n++;
+      return;
+    }
+    if (!memcmp(&m->k[i], k, sizeof *k)) {
+      m->v[2 * i] += c;
+      m->v[2 * i + 1] += b;
+      return;
+    }
+    i = (i + 1) & (m->cap - 1);
+  }
+}
+static void imap_free(imap_t *m) {
+  free(m->k);
+  free(m->v);
+  free(m->used);
+  memset(m, 0, sizeof *m);
+}
+
+static void side_key(uint32_t *w, int opts, uint32_t ip, uint32_t ep1, uint32_t port, uint32_t proto) {
+  w[0] = (opts & O_IP) ? ip : 0u;
+  w[1] = (opts & (O_NS | O_POD | O_WL)) ? ep1 : 0u;
+  w[2] = ((opts & O_PORT) && (proto == 6 || proto == 17)) ? (0x10000u | port) : 0u;
+}
+
+/* tcpflags.go:134-175 order: FIN, SYNACK | (SYN, ACK), RST, PSH, URG */
+static const char *FLAG_NAMES[7] = {"FIN", "SYNACK", "SYN", "ACK", "RST", "PSH", "URG"};
+static int flag_idx(uint32_t fl, int *out) {
+  int n = 0;
+  if (fl & 1) out[n++] = 0;
+  if ((fl & 2) && (fl & 16)) out[n++] = 1;
+  else {
+    if (fl & 2) out[n++] = 2;
+    if (fl & 16) out[n++] = 3;
+  }
+  if (fl & 4) out[n++] = 4;
+  if (fl & 8) out[n++] = 5;
+  if (fl & 32) out[n++] = 6;
+  return n;
+}
+
+typedef struct {
+  const ref_t *r;
+  const uint8_t *api; /* [endpoint index + 1]: the apiserver pseudo pod */
+  const uint8_t *lead; /* [metric]: first metric of its group (same key -> count and bytes) */
+  const uint32_t *src, *dst, *bytes, *meta, *ports, *dns_id;
+  size_t a, b;
+  imap_t map;
+  int bad;
+} tjob_t;
+
+static void tuned_flow(tjob_t *j, size_t i) {
+  const ref_t *r = j->r;
+  const uint32_t mt = j->meta[i], sip = j->src[i], dip = j->dst[i], nb = j->bytes[i];
+  const uint32_t proto = mt & 0xFF;
+  uint32_t verdict = (mt >> 8) & 0xFF;
+  if (verdict == 0) verdict = 1; /* ToFlow: 0 -> FORWARDED (flow_utils.go:94-96) */
+  const uint32_t tdir = (mt >> 16) & 3, reason = (mt >> 18) & 7, dnstype = (mt >> 28) & 3;
+  const uint32_t flags = (verdict == 1 || verdict == 15) && proto == 6 ? (mt >> 21) & 0x3F : 0;
+  const uint32_t sport = j->ports ? j->ports[i] & 0xFFFF : 0, dport = j->ports ? j->ports[i] >> 16 : 0;
+  const uint32_t dns = j->dns_id ? j->dns_id[i] : 0;
+  if (verdict == 16 && dns >= r->ndns) {
+    j->bad = 1;
+    return;
+  }
+  const uint32_t sep = ip_get(r, sip), dep = ip_get(r, dip); /* enricher.go:102-135 */
+  for (int k = 0; k < r->nm; ++k) {
+    const metric_t *m = &r->m[k];
+    if (!m->active || !j->lead[k]) continue;
+    int fi[8], nflags = 0;
+    if (m->family == F_FWD && verdict != 1) continue;
+    if (m->family == F_DROP && verdict != 2) continue;
+    if (m->family == F_RETRANS && verdict != 15) continue;
+    if (m->family == F_TCPFLAGS) {
+      if (verdict != 1 || proto != 6) continue;
+      if (!(nflags = flag_idx(flags, fi))) continue;
+    }
+    if (m->family == F_DNS) {
+      if (verdict != 16 || dnstype == 0) continue;
+      if (m->dns_kind == 1 && dnstype != 1) continue;
+      if (m->dns_kind == 2 && dnstype != 2) continue;
+    }
+    const uint64_t add = (m->family == F_FWD || m->family == F_DROP) ? nb : 0;
+    ikey_t key;
+    memset(&key, 0, sizeof key);
+    if (!r->remote) {
+      const int opts = m->src_opts;
+      const int ing = dep && !j->api[dep] && opts, egr = sep && !j->api[sep] && opts;
+      if (m->family == F_DNS) {
+        int dest;
+        if (ing && egr) dest = tdir == 1;
+        else if (ing) dest = 1;
+        else if (egr) dest = 0;
+        else continue;
+        key.w[0] = (uint32_t)k | ((uint32_t)dest << 18);
+        side_key(&key.w[1], opts, dest ? dip : sip, dest ? dep : sep, dest ? dport : sport, proto);
+        key.w[7] = dns + 1;
+        imap_add(&j->map, &key, 1, 0);
+        continue;
+      }
+      for (int side = 0; side < 2; ++side) {
+        const int dest = side == 0;
+        if (dest ? !ing : !egr) continue;
+        side_key(&key.w[1], opts, dest ? dip : sip, dest ? dep : sep, dest ? dport : sport, proto);
+        if (m->family == F_TCPFLAGS) {
+          for (int f = 0; f < nflags; ++f) {
+            key.w[0] = (uint32_t)k | ((uint32_t)fi[f] << 8) | ((uint32_t)dest << 18);
+            imap_add(&j->map, &key, 1, 0);
+          }
+          continue;
+        }
+        key.w[0] = (uint32_t)k | ((m->family == F_DROP ? reason : 0u) << 8) | ((uint32_t)dest << 18);
+        imap_add(&j->map, &key, 1, add);
+      }
+      continue;
+    }
+    const int with_ctx = m->family != F_FWD || m->adv;
+    if (with_ctx && m->has_src) side_key(&key.w[1], m->src_opts, sip, sep, sport, proto);
+    if (with_ctx && m->has_dst) side_key(&key.w[4], m->dst_opts, dip, dep, dport, proto);
+    if (m->family == F_TCPFLAGS) {
+      for (int f = 0; f < nflags; ++f) {
+        key.w[0] = (uint32_t)k | ((uint32_t)fi[f] << 8);
+        imap_add(&j->map, &key, 1, 0);
+      }
+      continue;
+    }
+    key.w[0] = (uint32_t)k | ((m->family == F_DROP ? reason : 0u) << 8) |
+               ((m->family == F_DNS ? 0u : tdir) << 16);
+    if (m->family == F_DNS) key.w[7] = dns + 1;
+    imap_add(&j->map, &key, 1, add);
+  }
+}
+
+#include <pthread.h>
+static void *tuned_worker(void *p) {
+  tjob_t *j = p;
+  for (size_t i = j->a; i < j->b; ++i) tuned_flow(j, i);
+  return NULL;
+}
+
+/* Renders one integer key to its label string exactly as process_metric builds it. */
+static void tuned_render(ref_t *r, int k, const ikey_t *key, uint64_t v) {
+  metric_t *m = &r->m[k];
+  const uint32_t sub = (key->w[0] >> 8) & 0xFF, tdir = (key->w[0] >> 16) & 3, dest = (key->w[0] >> 18) & 1;
+  flow_t f;
+  memset(&f, 0, sizeof f);
+  ip_str(key->w[1], f.sip);
+  ip_str(key->w[4], f.dip);
+  f.src = key->w[2] ? r->eps[key->w[2] - 1] : NULL;
+  f.dst = key->w[5] ? r->eps[key->w[5] - 1] : NULL;
+  f.sport = key->w[3] & 0xFFFF;
+  f.dport = key->w[6] & 0xFFFF;
+  f.proto = ((key->w[3] | key->w[6]) & 0x10000u) ? 6 : 0;
+  char lab[4096], payload[3072], tb[16], rb[16], nbuf[16];
+  char *p = lab;
+  payload[0] = 0;
+  if (m->family == F_DNS) {
+    const dns_t *d = &r->dns[key->w[7] - 1];
+    char *q = payload;
+    if (m->dns_kind == 1) {
+      q = put(q, d->qtypes);
+      q = put(q, d->query);
+    } else {
+      q = put(q, d->rcode < 6 ? RCODES[d->rcode] : "");
+      q = put(q, d->qtypes);
+      q = put(q, d->query);
+      q = put(q, d->ips);
+      sprintf(nbuf, "%u", d->nresp);
+      q = put(q, nbuf);
+    }
+    *q = 0;
+  }
+  if (!r->remote) {
+    /* local context: the side tuple sits in the source fields of the key */
+    f.dip[0] = 0;
+    flow_t g = f;
+    if (dest) {
+      memcpy(g.dip, f.sip, sizeof f.sip);
+      g.dst = f.src;
+      g.dport = f.sport;
+    }
+    if (m->family == F_DNS) p += sprintf(p, "%s", payload);
+    else if (m->family == F_TCPFLAGS) p = put(p, FLAG_NAMES[sub]);
+    else {
+      if (m->family == F_DROP) p = put(p, reason_name(sub, rb));
+      p = put(p, dest ? "ingress" : "egress");
+    }
+    p = side_values(p, m->src_opts, &g, (int)dest);
+    *p = 0;
+    update(m, lab, v);
+    return;
+  }
+  char ctx[2048];
+  char *c = ctx;
+  const int with_ctx = m->family != F_FWD || m->adv;
+  if (with_ctx && m->has_src) c = side_values(c, m->src_opts, &f, 0);
+  if (with_ctx && m->has_dst) c = side_values(c, m->dst_opts, &f, 1);
+  *c = 0;
+  if (m->family == F_TCPFLAGS) p = put(p, FLAG_NAMES[sub]);
+  if (m->family == F_DNS) p += sprintf(p, "%s", payload);
+  if (m->family == F_DROP) p = put(p, reason_name(sub, rb));
+  if (m->family == F_FWD || m->family == F_DROP || m->family == F_RETRANS) p = put(p, tdir_name(tdir, tb));
+  p += sprintf(p, "%s", ctx);
+  update(m, lab, v);
+}
+
+/* Tuned CPU path over nthreads threads; accumulates into the same series as ref_process. */
+int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const uint32_t *bytes,
+                      const uint32_t *meta, const uint32_t *ports, const uint32_t *dns_id, size_t n,
+                      int nthreads) {
+  ref_t *r = h;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  uint8_t *api = calloc(r->neps + 1, 1);
+  for (size_t e = 0; e < r->neps; ++e) api[e + 1] = (uint8_t)is_api(r->eps[e]);
+  /* metrics whose label tuples coincide (forward_count / forward_bytes with the same
+   * options, ...) share one key: the leader's table entry carries count and bytes */
+  uint8_t lead[32];
+  int leader[32];
+  for (int k = 0; k < r->nm; ++k) {
+    const metric_t *m = &r->m[k];
+    leader[k] = k;
+    for (int q = 0; q < k; ++q) {
+      const metric_t *o = &r->m[q];
+      if (o->active && o->family == m->family && o->src_opts == m->src_opts && o->dst_opts == m->dst_opts &&
+          o->has_src == m->has_src && o->has_dst == m->has_dst && o->adv == m->adv &&
+          o->dns_kind == m->dns_kind) {
+        leader[k] = leader[q];
+        break;
+      }
+    }
+    lead[k] = leader[k] == k;
+  }
+  tjob_t *jobs = calloc((size_t)nthreads, sizeof(tjob_t));
+  pthread_t *th = calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; ++t) {
+    tjob_t *j = &jobs[t];
+    j->r = r;
+    j->api = api;
+    j->lead = lead;
+    j->src = src;
+    j->dst = dst;
+    j->bytes = bytes;
+    j->meta = meta;
+    j->ports = ports;
+    j->dns_id = dns_id;
+    j->a = n * (size_t)t / (size_t)nthreads;
+    j->b = n * (size_t)(t + 1) / (size_t)nthreads;
+    if (t && pthread_create(&th[t], NULL, tuned_worker, j)) {
+      tuned_worker(j); /* no thread: run it here */
+      th[t] = 0;
+    }
+  }
+  tuned_worker(&jobs[0]);
+  int bad = jobs[0].bad;
+  for (int t = 1; t < nthreads; ++t) {
+    if (th[t]) pthread_join(th[t], NULL);
+    bad |= jobs[t].bad;
+    /* per-thread tables merged into thread 0's */
+    for (size_t i = 0; i < jobs[t].map.cap; ++i)
+      if (jobs[t].map.used[i])
+        imap_add(&jobs[0].map, &jobs[t].map.k[i], jobs[t].map.v[2 * i], jobs[t].map.v[2 * i + 1]);
+    imap_free(&jobs[t].map);
+  }
+  if (!bad)
+    for (size_t i = 0; i < jobs[0].map.cap; ++i)
+      if (jobs[0].map.used[i]) {
+        const int lk = (int)(jobs[0].map.k[i].w[0] & 0xFF);
+        for (int k = 0; k < r->nm; ++k)
+          if (r->m[k].active && leader[k] == lk)
+            tuned_render(r, k, &jobs[0].map.k[i], jobs[0].map.v[2 * i + (r->m[k].is_bytes ? 1 : 0)]);
+      }
+  imap_free(&jobs[0].map);
+  free(jobs);
+  free(th);
+  free(api);
+  return bad ? -1 : 0;
 }
 
 /* Flattens the series: labels are "\x1f"-separated values (label names are fixed per metric). */

@@ -17,7 +17,7 @@ LIB = os.path.join(HERE, "libref_cpu.so")
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-shared", "-fPIC", "-Wall",
+        subprocess.run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-shared", "-fPIC", "-Wall", "-pthread",
                         "-o", LIB + ".tmp", SRC], check=True)
         os.replace(LIB + ".tmp", LIB)
     return LIB
@@ -40,6 +40,7 @@ def lib():
         L.ref_add_dns.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32]
         u = C.POINTER(C.c_uint32)
         L.ref_process.argtypes = [C.c_void_p, u, u, u, u, u, u, C.c_size_t]
+        L.ref_process_tuned.argtypes = [C.c_void_p, u, u, u, u, u, u, C.c_size_t, C.c_int]
         L.ref_finish.restype = C.c_size_t
         L.ref_finish.argtypes = [C.c_void_p]
         L.ref_series.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
@@ -87,6 +88,18 @@ class RefCPU:
         dt = time.perf_counter() - t0
         if rc != 0:
             raise ValueError("ref_process failed")
+        return dt
+
+    def process_tuned(self, recs, threads: int) -> float:
+        """Tuned mode: integer keys, `threads` threads, per-thread tables merged at the end."""
+        u = C.POINTER(C.c_uint32)
+        cols = [np.ascontiguousarray(getattr(recs, k), np.uint32)
+                for k in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id")]
+        t0 = time.perf_counter()
+        rc = self.L.ref_process_tuned(self.h, *[c.ctypes.data_as(u) for c in cols], len(cols[0]), threads)
+        dt = time.perf_counter() - t0
+        if rc != 0:
+            raise ValueError("ref_process_tuned failed")
         return dt
 
     def series(self) -> Dict[Tuple[str, Tuple[str, ...]], int]:

@@ -52,7 +52,7 @@ class StateDesc(C.Structure):
                 ("dense_bytes", C.c_void_p),
                 ("cms", C.c_void_p), ("cms_len", C.c_size_t),
                 ("hll", C.c_void_p), ("hll_len", C.c_size_t),
-                ("sparse_entry_words", C.c_size_t)]
+                ("sparse_entry_words", C.c_size_t), ("sparse_len", C.c_size_t)]
 
 
 class Stats(C.Structure):
@@ -61,7 +61,8 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("fold_ms", C.c_double), ("last_kernel", C.c_uint32),
                 ("decoded", C.c_uint64), ("decode_out_of_range", C.c_uint64),
                 ("decode_launches", C.c_uint64), ("decode_ms", C.c_double),
-                ("sketch_launches", C.c_uint64), ("sketch_ms", C.c_double)]
+                ("sketch_launches", C.c_uint64), ("sketch_ms", C.c_double),
+                ("async_returns", C.c_uint64)]
 
 
 RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
@@ -109,6 +110,7 @@ SIGNATURES = [
     ("gpuagg_get_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     ("gpuagg_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("gpuagg_stream", C.c_void_p, [C.c_void_p]),
+    ("gpuagg_kernel_name", C.c_char_p, [C.c_void_p]),
 ]
 
 _lib = None
@@ -122,14 +124,38 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError("retina_amd: %s is missing; run __graft_entry__.build() "
                           "(there is no CPU fallback)" % path)
-    # One HIP runtime per process: PyTorch (device memory, streams, RCCL) must load its
-    # libamdhip64 before this library does, or torch's later HIP init finds no GPUs when
-    # the engine is created first (as smoke() does).
+    # One HIP runtime per process.  torch 2.10+rocm ships its own libamdhip64.so and
+    # libhsa-runtime64.so (torch/lib, SONAMEs libamdhip64.so.7 / libhsa-runtime64.so.1)
+    # and its libraries NEED them by the unversioned names.  libgpuagg.so NEEDs
+    # libamdhip64.so.7: loaded AFTER torch, the dynamic linker matches that SONAME to
+    # torch's copy and the process has one runtime; loaded BEFORE torch, it maps
+    # /opt/rocm/lib's copy, torch's NEEDED "libamdhip64.so" matches no loaded name and a
+    # second runtime is mapped -- whose HIP init then finds no GPU ("No HIP GPUs are
+    # available", round-1 smoke).  So torch is imported first, and the result is checked.
     import torch  # noqa: F401
     lib = C.CDLL(path)
+    runtimes = hip_runtimes_mapped()
+    if len(runtimes.get("libamdhip64", ())) > 1 or len(runtimes.get("libhsa-runtime64", ())) > 1:
+        raise ImportError("retina_amd: two HIP runtimes are mapped in this process: %r" % runtimes)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def hip_runtimes_mapped() -> dict:
+    """{"libamdhip64": {paths}, "libhsa-runtime64": {paths}} mapped in this process."""
+    out = {}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split()[-1] if len(line.split()) >= 6 else ""
+                base = os.path.basename(path)
+                for stem in ("libamdhip64", "libhsa-runtime64"):
+                    if base.startswith(stem + ".so"):
+                        out.setdefault(stem, set()).add(os.path.realpath(path))
+    except OSError:
+        pass
+    return out

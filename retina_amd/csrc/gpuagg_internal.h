@@ -90,6 +90,7 @@ struct Plan {
   int32_t ngroups;
   uint32_t need_ports;
   uint32_t need_dns;
+  uint32_t need_bytes;  // some group adds packet bytes (forward / drop)
   GroupPlan g[kMaxGroups];
 };
 

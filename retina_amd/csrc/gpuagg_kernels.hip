@@ -384,6 +384,7 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
 // (register rotation keeps one copy of the per-record code).
 template <bool kVec, class F>
 __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f) {
+  const bool need_bytes = a.p.need_bytes;  // no forward / drop group: the column is not read
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
   uint64_t tail = start;
@@ -394,7 +395,8 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
     const uint4 *p4 = (const uint4 *)a.c.ports, *q4 = (const uint4 *)a.c.dns;
     for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
       const uint64_t v = i >> 2;
-      const uint4 vs = s4[v], vd = d4[v], vb = b4[v], vm = m4[v];
+      const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
+      const uint4 vb = need_bytes ? b4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
@@ -424,8 +426,8 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
     const uint32_t sip = a.c.src[i], dip = a.c.dst[i];
-    f(sip, dip, a.c.bytes[i], a.c.meta[i], need_ports ? a.c.ports[i] : 0u, need_dns ? a.c.dns[i] : 0u,
-      ip_lookup(a.t, sip), ip_lookup(a.t, dip));
+    f(sip, dip, need_bytes ? a.c.bytes[i] : 0u, a.c.meta[i], need_ports ? a.c.ports[i] : 0u,
+      need_dns ? a.c.dns[i] : 0u, ip_lookup(a.t, sip), ip_lookup(a.t, dip));
   }
 }
 
@@ -1234,7 +1236,7 @@ static hipError_t launch_k(K kern, const KArgs &k, uint32_t blocks, uint32_t thr
   return hipGetLastError();
 }
 
-hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between) {
+hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between, const char **kernel) {
   if (a.n == 0) return hipSuccess;
   KArgs k{};
   k.c = DevCols{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
@@ -1274,6 +1276,17 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     fprintf(stderr, "gpuagg: launch variant=%d tier1=%d sig=0x%x ng=%u L=%u ipl_bytes=%u nwin=%u n=%llu\n",
             variant, (int)a.tier1, a.sig, a.dense_ng, a.lds_bins, a.ipl_bytes, a.nwin,
             (unsigned long long)a.n);
+  if (kernel) {
+    static thread_local char name[64];
+    if (a.tier1)
+      snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu>", variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng,
+               a.vec ? "true" : "false", variant >= 200 ? a.sig : 0u);
+    else if (a.dense_ng)
+      snprintf(name, sizeof name, "dense_local_kernel<%u, %s>", a.dense_ng, a.vec ? "true" : "false");
+    else
+      snprintf(name, sizeof name, "aggregate_kernel<%s, %s>", a.vec ? "true" : "false", sketch ? "true" : "false");
+    *kernel = name;
+  }
   switch (variant) {
     case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true, 0>, k, B, T, lds, st)
                         : launch_k(dense_lds_kernel<1, false, 0>, k, B, T, lds, st); break;

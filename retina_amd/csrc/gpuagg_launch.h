@@ -88,7 +88,10 @@ struct SketchArgs {
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
 
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
-hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between);
+// *kernel (may be null) receives the aggregation kernel's signature as rocprofv3 prints it
+// without "void gpuagg::" and the argument list, e.g. "dense_lds_kernel<2, true, 41u>".
+hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between,
+                            const char **kernel = nullptr);
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);
 hipError_t launch_sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t out_cap,
                                 uint64_t *counter, hipStream_t st);

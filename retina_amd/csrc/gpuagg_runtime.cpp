@@ -158,10 +158,21 @@ struct gpuagg_ctx {
   std::vector<uint32_t> h_cms;
   std::vector<uint8_t> h_hll;
 
-  // device staging for host-fed batches
-  uint32_t *d_cols[6] = {};
+  // Device staging for host-fed batches, double-buffered: batch k+1's H2D copy (on
+  // copy_stream) overlaps batch k's aggregation (on stream).  `copied` is recorded on
+  // copy_stream after the copy, `released` on stream after the last kernel reading it.
+  struct Staging {
+    uint32_t *cols[6] = {};
+    uint8_t *raw = nullptr;
+    size_t raw_alloc = 0;
+    hipEvent_t copied = nullptr, released = nullptr;
+    bool in_use = false;
+  } stg[2];
   size_t staging_cap = 0;
+  int next_stg = 0;
+  hipStream_t copy_stream = nullptr;
   std::vector<gpuagg_batch *> batches;
+  std::string kernel_name;  // aggregation kernel of the last launch (rocprofv3 spelling)
 
   // stats / timing
   gpuagg_stats stats{};
@@ -179,8 +190,6 @@ struct gpuagg_ctx {
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
   // raw perf-record decode (gpuagg_decode.hip)
-  uint8_t *d_raw = nullptr;  // device copy of host-fed raw records
-  size_t raw_alloc = 0;
   uint64_t *d_decode_oor = nullptr;  // out-of-range field counter
   std::vector<std::array<hipEvent_t, 2>> pending_decode;  // decode start, end
   // sketch pass (count-min window lists)
@@ -293,14 +302,44 @@ void ctx_values(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, 
 
 int ensure_staging(gpuagg_ctx *c, size_t cap) {
   if (cap <= c->staging_cap) return GPUAGG_OK;
-  if (c->staging_cap) hipStreamSynchronize(c->stream);  // in-flight launches may read the old columns
-  for (auto &p : c->d_cols) dev_free(p);
-  for (auto &p : c->d_cols) {
-    int rc = dev_alloc(c, &p, cap);
-    if (rc) return rc;
+  if (c->staging_cap) {  // in-flight copies / launches may use the old columns
+    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  c->staging_cap = 0;
+  for (auto &s : c->stg) {
+    for (auto &p : s.cols) dev_free(p);
+    for (auto &p : s.cols)
+      if (int rc = dev_alloc(c, &p, cap)) return rc;
   }
   c->staging_cap = cap;
   return GPUAGG_OK;
+}
+
+// The next staging buffer, once the kernels that read it last have finished.
+int acquire_staging(gpuagg_ctx *c, gpuagg_ctx::Staging **out) {
+  gpuagg_ctx::Staging &s = c->stg[c->next_stg];
+  c->next_stg ^= 1;
+  if (s.in_use) HIPCHK(c, hipEventSynchronize(s.released));
+  s.in_use = false;
+  *out = &s;
+  return GPUAGG_OK;
+}
+
+// After the H2D copies into s were enqueued on copy_stream: the aggregation stream waits
+// for them, `launch_fn` enqueues the kernels, s is released behind them, and the call
+// returns once the copies (not the kernels) are complete, so the caller's host buffer
+// may be refilled while the aggregation runs.
+template <class F>
+int run_staged(gpuagg_ctx *c, gpuagg_ctx::Staging &s, F &&launch_fn) {
+  HIPCHK(c, hipEventRecord(s.copied, c->copy_stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, s.copied, 0));
+  int rc = launch_fn();
+  HIPCHK(c, hipEventRecord(s.released, c->stream));
+  s.in_use = true;
+  HIPCHK(c, hipEventSynchronize(s.copied));
+  if (hipEventQuery(s.released) == hipErrorNotReady) c->stats.async_returns += 1;
+  return rc;
 }
 
 int reset_state(gpuagg_ctx *c) {
@@ -557,7 +596,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
       HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
-    HIPCHK(c, launch_aggregate(a, c->stream, c->timing ? ev[1] : nullptr));
+    const char *kname = nullptr;
+    HIPCHK(c, launch_aggregate(a, c->stream, c->timing ? ev[1] : nullptr, &kname));
+    if (kname) c->kernel_name = kname;
     if (c->timing) {
       HIPCHK(c, hipEventRecord(ev[2], c->stream));
       c->pending_events.push_back(ev);
@@ -596,15 +637,14 @@ int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols
   return GPUAGG_OK;
 }
 
-// Decodes into the ctx's column staging and aggregates from there.
-int decode_and_launch(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n) {
+// Decodes into staging buffer s's columns and aggregates from there.
+int decode_and_launch(gpuagg_ctx *c, gpuagg_ctx::Staging &s, int kind, const void *dev_raw, size_t n) {
   int rc;
-  if ((rc = ensure_staging(c, n))) return rc;
-  const OutCols out{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3],
-                    (c->plan.need_ports || c->cms_len > 0) ? c->d_cols[4] : nullptr,
-                    c->plan.need_dns ? c->d_cols[5] : nullptr};
+  uint32_t *const *d = s.cols;
+  const OutCols out{d[0], d[1], d[2], d[3], (c->plan.need_ports || c->cms_len > 0) ? d[4] : nullptr,
+                    c->plan.need_dns ? d[5] : nullptr};
   if ((rc = decode(c, kind, dev_raw, n, out))) return rc;
-  ColsView cv{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3], c->d_cols[4], c->d_cols[5]};
+  ColsView cv{d[0], d[1], d[2], d[3], d[4], d[5]};
   return launch(c, cv, n);
 }
 
@@ -632,17 +672,36 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
   if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return GPUAGG_EDEVICE;
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GPUAGG_EDEVICE;  // built for gfx950 only
   if (hipSetDevice(c->device) != hipSuccess) return GPUAGG_EDEVICE;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return GPUAGG_EDEVICE;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+    gpuagg_destroy(c.release());
+    return GPUAGG_EDEVICE;
+  }
+  for (auto &st : c->stg)
+    if (hipEventCreateWithFlags(&st.copied, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&st.released, hipEventDisableTiming) != hipSuccess) {
+      gpuagg_destroy(c.release());
+      return GPUAGG_EDEVICE;
+    }
   c->n_cu = (uint32_t)prop.multiProcessorCount;
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
-    if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) return GPUAGG_ENOMEM;
+    if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) {
+      gpuagg_destroy(c.release());
+      return GPUAGG_ENOMEM;
+    }
   }
   if (cfg->hll_precision) {
     c->hll_len = (size_t)cfg->max_slots << cfg->hll_precision;
-    if (dev_alloc(c.get(), &c->d_hll, c->hll_len)) return GPUAGG_ENOMEM;
+    if (dev_alloc(c.get(), &c->d_hll, c->hll_len)) {
+      gpuagg_destroy(c.release());
+      return GPUAGG_ENOMEM;
+    }
   }
-  if (reset_state(c.get())) return GPUAGG_EDEVICE;
+  if (reset_state(c.get())) {
+    gpuagg_destroy(c.release());
+    return GPUAGG_EDEVICE;
+  }
   *out = c.release();
   return GPUAGG_OK;
 }
@@ -650,6 +709,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
 void gpuagg_destroy(gpuagg_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   if (c->stream) hipStreamSynchronize(c->stream);
   drain_timing(c);
   for (auto *b : c->batches) {
@@ -672,11 +732,16 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_spill_count);
   dev_free(c->d_stage_a);
   dev_free(c->d_stage_b);
-  dev_free(c->d_raw);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
   dev_free(c->d_decode_oor);
-  for (auto &p : c->d_cols) dev_free(p);
+  for (auto &st : c->stg) {
+    for (auto &p : st.cols) dev_free(p);
+    dev_free(st.raw);
+    if (st.copied) hipEventDestroy(st.copied);
+    if (st.released) hipEventDestroy(st.released);
+  }
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -869,6 +934,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
     gp.nbins = groups[g].sparse ? 0u : (uint32_t)(groups[g].nkeys * 2 * groups[g].nsub);
     if ((gp.src_opts | gp.dst_opts) & OPT_PORT) p.need_ports = 1;
     if (gp.family == FAM_DNS_REQ || gp.family == FAM_DNS_RESP) p.need_dns = 1;
+    if (gp.family == FAM_FWD || gp.family == FAM_DROP) p.need_bytes = 1;
     any_sparse |= groups[g].sparse;
   }
 
@@ -1051,17 +1117,17 @@ int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
   if (!c || !b || n > b->capacity) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
   if ((rc = ensure_staging(c, b->capacity))) return rc;
+  gpuagg_ctx::Staging *s;
+  if ((rc = acquire_staging(c, &s))) return rc;
   uint32_t *src[6] = {b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports, b->cols.dns_id};
-  const bool need[6] = {true, true, true, true, c->plan.need_ports || c->cms_len > 0, (bool)c->plan.need_dns};
+  const bool need[6] = {true, true, (bool)c->plan.need_bytes, true, c->plan.need_ports || c->cms_len > 0,
+                        (bool)c->plan.need_dns};
   for (int i = 0; i < 6; ++i)
-    if (need[i] && n) HIPCHK(c, hipMemcpyAsync(c->d_cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->stream));
-  ColsView cv{c->d_cols[0], c->d_cols[1], c->d_cols[2], c->d_cols[3], c->d_cols[4], c->d_cols[5]};
-  if ((rc = launch(c, cv, n))) return rc;
-  // The single staging area is reused by the next submit, which is stream-ordered
-  // behind this kernel; the pinned batch is free once its copies have completed.
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return GPUAGG_OK;
+    if (need[i]) HIPCHK(c, hipMemcpyAsync(s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
+  ColsView cv{s->cols[0], s->cols[1], s->cols[2], s->cols[3], s->cols[4], s->cols[5]};
+  return run_staged(c, *s, [&] { return launch(c, cv, n); });
 }
 
 int gpuagg_submit_device(gpuagg_ctx *c, const gpuagg_columns *d, size_t n) {
@@ -1096,7 +1162,14 @@ int gpuagg_submit_raw_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_
   if (!c) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  return decode_and_launch(c, kind, dev_raw, n);
+  if (n == 0) return GPUAGG_OK;
+  if ((rc = ensure_staging(c, n))) return rc;
+  gpuagg_ctx::Staging *s;
+  if ((rc = acquire_staging(c, &s))) return rc;
+  rc = decode_and_launch(c, *s, kind, dev_raw, n);
+  HIPCHK(c, hipEventRecord(s->released, c->stream));
+  s->in_use = true;
+  return rc;
 }
 
 int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
@@ -1106,12 +1179,17 @@ int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
   if (rc) return rc;
   if (n == 0) return GPUAGG_OK;
   const size_t rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
-  if ((rc = ensure_buf(c, &c->d_raw, &c->raw_alloc, n * rec))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->d_raw, host_raw, n * rec, hipMemcpyHostToDevice, c->stream));
-  if ((rc = decode_and_launch(c, kind, c->d_raw, n))) return rc;
-  // like gpuagg_submit: the raw staging is reused by the next call
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return GPUAGG_OK;
+  if ((rc = ensure_staging(c, n))) return rc;
+  gpuagg_ctx::Staging *s;
+  if ((rc = acquire_staging(c, &s))) return rc;
+  if (n * rec > s->raw_alloc) {  // (acquire_staging waited for the kernels reading it)
+    dev_free(s->raw);
+    s->raw_alloc = 0;
+    if ((rc = dev_alloc(c, &s->raw, n * rec))) return rc;
+    s->raw_alloc = n * rec;
+  }
+  HIPCHK(c, hipMemcpyAsync(s->raw, host_raw, n * rec, hipMemcpyHostToDevice, c->copy_stream));
+  return run_staged(c, *s, [&] { return decode_and_launch(c, *s, kind, s->raw, n); });
 }
 
 int gpuagg_reset(gpuagg_ctx *c) {
@@ -1332,6 +1410,7 @@ int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   o->hll = c->d_hll;
   o->hll_len = c->hll_len;
   o->sparse_entry_words = kSparseEntryWords;
+  o->sparse_len = c->sparse_slots;
   return GPUAGG_OK;
 }
 
@@ -1380,5 +1459,7 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
 }
 
 void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }
 
 }  // extern "C"

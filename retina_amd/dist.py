@@ -112,33 +112,52 @@ def device_view(ptr: int, n: int, typestr: str, device):
     return torch.as_tensor(_CAI(ptr, n, typestr), device=device)
 
 
-def merge_engine(engine, group=None, dst: int = 0, export_cap: int = 1 << 22) -> None:
+def merge_engine(engine, group=None, dst: int = 0) -> None:
     """Per-epoch merge of a GpuAgg's state across ranks: rank `dst` ends with the node
     total, every other rank is reset (gpuagg_reset) so the next epoch counts only new
-    records."""
+    records.
+
+    Backend "nccl" (RCCL over xGMI) reduces the engine's device memory in place through
+    __cuda_array_interface__ views.  Backend "gloo" (CPU tests, and several ranks sharing
+    one GPU) stages each array through host memory: copy out, reduce, copy back."""
     import torch
     import torch.distributed as dist
     device = torch.device("cuda", engine.device)
+    on_host = dist.get_backend(group) == "gloo"
     engine.sync()
     st = engine.state()
-    if st.dense_len:
-        dist.reduce(device_view(st.dense_count, st.dense_len, "<i8", device), dst, group=group)
-        dist.reduce(device_view(st.dense_bytes, st.dense_len, "<i8", device), dst, group=group)
-    if st.cms_len:
-        dist.reduce(device_view(st.cms, st.cms_len, "<i4", device), dst, group=group)
-    if st.hll_len:
-        dist.reduce(device_view(st.hll, st.hll_len, "|u1", device), dst, op=dist.ReduceOp.MAX,
-                    group=group)
-    buf = torch.empty((export_cap, 5), dtype=torch.int64, device=device)
-    n = engine.sparse_export(buf.data_ptr(), export_cap)
-    torch.cuda.synchronize(device)
-    blocks = gather_entries(buf, n, dst, group)
     me = dist.get_rank(group)
+
+    def reduce(ptr, n, typestr, op):
+        view = device_view(ptr, n, typestr, device)
+        if not on_host:
+            dist.reduce(view, dst, op=op, group=group)
+            return
+        h = view.cpu()
+        dist.reduce(h, dst, op=op, group=group)
+        if me == dst:
+            view.copy_(h)
+
+    if st.dense_len:
+        reduce(st.dense_count, st.dense_len, "<i8", dist.ReduceOp.SUM)
+        reduce(st.dense_bytes, st.dense_len, "<i8", dist.ReduceOp.SUM)
+    if st.cms_len:
+        reduce(st.cms, st.cms_len, "<i4", dist.ReduceOp.SUM)
+    if st.hll_len:
+        reduce(st.hll, st.hll_len, "|u1", dist.ReduceOp.MAX)
+    # sparse table: every rank's compact entries gathered on dst and inserted-and-added
+    cap = int(st.sparse_len)
+    local = torch.zeros((max(cap, 1), 5), dtype=torch.int64, device=device)
+    n = engine.sparse_export(local.data_ptr(), cap) if cap else 0
+    torch.cuda.synchronize(device)
+    blocks = gather_entries(local.cpu() if on_host else local, n, dst, group)
     if blocks is not None:
         for r, b in enumerate(blocks):
             if r != me and b.shape[0]:
-                b = b.contiguous()
+                b = b.to(device).contiguous()
                 torch.cuda.synchronize(device)
                 engine.sparse_import(b.data_ptr(), int(b.shape[0]))
+    engine.sync()
+    torch.cuda.synchronize(device)
     if me != dst:
         engine.reset()

@@ -321,5 +321,9 @@ class GpuAgg:
         self._check(self.lib.gpuagg_get_stats(self.h, C.byref(s)))
         return {k: getattr(s, k) for k, _ in _abi.Stats._fields_}
 
+    def kernel_name(self) -> str:
+        """Signature of the last launch's aggregation kernel (rocprofv3 spelling)."""
+        return (self.lib.gpuagg_kernel_name(self.h) or b"").decode()
+
     def set_timing(self, enabled: bool) -> None:
         self._check(self.lib.gpuagg_set_timing(self.h, 1 if enabled else 0))

@@ -106,18 +106,56 @@ def _pick_ips(rng, n: int, pods: Pods, pod_frac: float, zipf: Optional[float]) -
     return np.where(is_pod, pods.ips[idx], ext).astype(np.uint32)
 
 
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        x += np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def flow_tuples(flow_id: np.ndarray, pods: Pods, n_dst: int, udp_frac: float = 0.0):
+    """The fixed 5-tuple of each flow id (C3, SURVEY.md 8d: flows with src in the pods and
+    dst among n_dst IPs, the first len(pods.ips) of them the pod IPs): a pure function of
+    the id, so a flow has the same 5-tuple in every chunk and on every rank."""
+    u = np.uint32
+    h1 = _splitmix64(flow_id)
+    h2 = _splitmix64(flow_id ^ np.uint64(0x5851F42D4C957F2D))
+    src = pods.ips[(h1 % np.uint64(len(pods.ips))).astype(np.int64)]
+    j = (h2 % np.uint64(n_dst)).astype(np.int64)
+    npi = len(pods.ips)
+    k = np.maximum(j - npi, 0).astype(u)
+    ext = (u(100) | ((u(64) + (k >> u(16))) << u(8)) | (((k >> u(8)) & u(255)) << u(16))
+           | ((k & u(255)) << u(24)))
+    dst = np.where(j < npi, pods.ips[np.minimum(j, npi - 1)], ext).astype(u)
+    h3 = (h1 >> np.uint64(32)).astype(u)
+    sport = u(32768) + (h3 % u(28232))
+    dport = np.array([80, 443, 53, 8080, 6443, 9090], u)[((h2 >> np.uint64(40)) % np.uint64(6)).astype(np.int64)]
+    udp = ((h2 >> np.uint64(8)) & np.uint64(0xFFFF)).astype(np.float64) < udp_frac * 65536.0
+    return src, dst, (sport | (dport << u(16))).astype(u), udp
+
+
 def gen_records(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, drop_frac: float = 0.10,
                 retrans_frac: float = 0.0, dns_frac: float = 0.0, udp_frac: float = 0.0,
                 other_proto_frac: float = 0.0, zipf: Optional[float] = None,
-                n_queries: int = 100_000, odd_frac: float = 0.0) -> Records:
+                n_queries: int = 100_000, odd_frac: float = 0.0, flows: Optional[int] = None,
+                n_dst: int = 1_000_000, flow_zipf: Optional[float] = None) -> Records:
     """Vectorised record generator (SURVEY.md 8d distributions).
 
     odd_frac adds edge rows: unknown / out-of-range traffic directions, verdicts no
-    metric consumes, drop reason 7, destination 255.255.255.255."""
+    metric consumes, drop reason 7, destination 255.255.255.255.
+    flows: draw each record's 5-tuple from `flows` fixed flows (flow_tuples; uniform, or
+    Zipf(flow_zipf) over flow ranks) instead of independently per record."""
     rng = np.random.Generator(np.random.PCG64(seed))
     u = np.uint32
-    src = _pick_ips(rng, n, pods, pod_frac, zipf)
-    dst = _pick_ips(rng, n, pods, pod_frac, None)
+    if flows:
+        fid = ((rng.zipf(flow_zipf, n) - 1) % flows) if flow_zipf else rng.integers(0, flows, n)
+        src, dst, ports_f, udp_f = flow_tuples(fid.astype(np.uint64), pods, n_dst, udp_frac)
+    else:
+        src = _pick_ips(rng, n, pods, pod_frac, zipf)
+        dst = _pick_ips(rng, n, pods, pod_frac, None)
     nbytes = rng.integers(64, 1501, n, dtype=u)
     r = rng.random(n)
     verdict = np.full(n, V_FWD, u)
@@ -129,6 +167,8 @@ def gen_records(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, drop_fr
     proto = np.full(n, PROTO_TCP, u)
     proto[pr < udp_frac] = PROTO_UDP
     proto[(pr >= udp_frac) & (pr < udp_frac + other_proto_frac)] = PROTO_ICMP
+    if flows:  # the flow fixes its protocol
+        proto = np.where(udp_f, u(PROTO_UDP), u(PROTO_TCP))
     proto[is_dns] = PROTO_UDP
     tdir = rng.integers(1, 3, n, dtype=u)
     tdir[verdict == V_DROP] = 1       # dropreason: obs 2 -> INGRESS (dropreason_linux.go:358-368)
@@ -178,8 +218,8 @@ def gen_records(n: int, pods: Pods, seed: int, *, pod_frac: float = 0.8, drop_fr
         reason = np.where(o & (kinds == 2) & (verdict == V_DROP), u(7), reason)
         dst = np.where(o & (kinds == 3), u(0xFFFFFFFF), dst)
     meta = pack_meta(proto, verdict, tdir, reason, flags, is_reply, dns_type)
-    return Records(src, dst, nbytes, meta.astype(u), (sport | (dport << u(16))).astype(u), dns_id,
-                   payloads)
+    ports = ports_f if flows else (sport | (dport << u(16))).astype(u)
+    return Records(src, dst, nbytes, meta.astype(u), ports, dns_id, payloads)
 
 
 # ---- raw perf records (GPUAGG_RAW_*) --------------------------------------
@@ -311,8 +351,12 @@ C5_SPEC = [
 CONFIGS = {
     "c1": dict(records=1_000_000, pods=10_000, seed=1, gen={}),
     "c2": dict(records=100_000_000, pods=10_000, seed=2, gen={}),
-    "c3": dict(records=1 << 30, pods=10_000, seed=3, gen={}),
+    # C3: 5-tuples from 10^7 flows, src in the 10k pods, dst among 10^6 IPs
+    "c3": dict(records=1 << 30, pods=10_000, seed=3, gen={"flows": 10_000_000, "n_dst": 1_000_000}),
+    # C4: Zipf(1.2) source pods and Zipf(1.2) 5-tuple (flow) ranks over 10^7 flows
     "c4": dict(records=100_000_000, pods=10_000, seed=4, gen={"zipf": 1.2}),
+    "c4-flows": dict(records=100_000_000, pods=10_000, seed=4,
+                     gen={"flows": 10_000_000, "flow_zipf": 1.2, "n_dst": 1_000_000}),
     "c5": dict(records=10_000_000, pods=100_000, seed=5,
                gen={"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
 }

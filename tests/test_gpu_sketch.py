@@ -94,3 +94,42 @@ def test_hll_relative_error(gpu_device):
     assert len(errs) >= 30
     assert max(errs) <= 4 * sigma, max(errs)
     assert float(np.mean(errs)) <= 1.5 * sigma
+
+
+def test_c3_full_shape_bit_exact(gpu_device):
+    """BASELINE.json config 3 at its benched per-GPU shape: 10k pods (HLL 10k x 16 KiB =
+    160 MiB), count-min d=4 w=2^20, 2^27 records drawn from SURVEY.md 8d's flow
+    distribution (10^7 flows, src in the pods, dst among 10^6 IPs), C2's metrics beside the
+    sketches.  Count-min rows, HLL registers and every series bit-exact against the numpy
+    restatements, accumulated chunk by chunk on the host."""
+    import torch
+    from oracle.vectorized import LocalDense
+    from retina_amd import GpuAgg
+    cfg = W.CONFIGS["c3"]
+    pods = W.make_pods(cfg["pods"], seed=cfg["seed"])
+    n, chunk = 1 << 27, 1 << 23
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, gpu_device, cms_depth=4, cms_width_log2=20,
+                    hll_precision=14)
+    dev = torch.device("cuda", gpu_device)
+    cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(6)]
+    want_c = np.zeros((4, 1 << 20), np.uint32)
+    want_h = np.zeros((len(pods.endpoints), 1 << 14), np.uint8)
+    v = LocalDense(W.LOCAL_FWD_DROP, pods.endpoints)
+    for k in range(n // chunk):
+        r = W.gen_records(chunk, pods, seed=3000 + k, **cfg["gen"])
+        for t, a in zip(cols, (r.src_ip, r.dst_ip, r.bytes, r.meta, r.ports, r.dns_id)):
+            t[k * chunk:(k + 1) * chunk].copy_(torch.from_numpy(a.view(np.int32)))
+        S.cms_update(want_c, r.src_ip, r.dst_ip, r.ports, r.meta & np.uint32(0xFF))
+        S.hll_update(want_h, _src_slots(pods, r.src_ip), r.dst_ip, 14)
+        v.add(r)
+    try:
+        g.submit_device(GpuAgg.device_columns(*cols), n)
+        got = g.snapshot()
+        cms, hll = g.cms_array(), g.hll_array()
+    finally:
+        g.close()
+    del cols
+    assert got == v.series()
+    assert np.array_equal(cms, want_c)
+    assert np.array_equal(hll[:len(pods.endpoints)], want_h)
+    assert int(cms[0].sum()) == n

@@ -30,6 +30,18 @@ def test_ref_cpu_matches_oracle(pods, cid, sp, remote, gen):
     assert got == want
 
 
+@pytest.mark.parametrize("cid,sp,remote,gen", CASES, ids=[c[0] for c in CASES])
+def test_ref_cpu_tuned_matches_oracle(pods, cid, sp, remote, gen):
+    """Tuned CPU baseline (integer keys, 4 threads, per-thread tables merged at the end)."""
+    recs = W.gen_records(12_000, pods, seed=zlib.crc32(cid.encode()) & 0xFFFF, **gen)
+    want = values_only(oracle_series(recs, pods, sp, remote))
+    r = RefCPU(sp, pods.endpoints, remote, recs.dns)
+    r.process_tuned(recs, 4)
+    got = r.series()
+    r.close()
+    assert got == want
+
+
 def test_ref_cpu_rejects_panicking_specs(pods):
     with pytest.raises(ValueError):
         RefCPU([{"metric_name": "dns_foo", "source_labels": ["podname"]}], pods.endpoints, False)
