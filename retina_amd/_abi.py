@@ -134,8 +134,10 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     # available", round-1 smoke).  So torch is imported first, and the result is checked.
     import torch  # noqa: F401
     lib = C.CDLL(path)
+    # (only libamdhip64 is enforced: under rocprofv3 the profiler's own tool library maps
+    # /opt/rocm's libhsa-runtime64 beside torch's, by design)
     runtimes = hip_runtimes_mapped()
-    if len(runtimes.get("libamdhip64", ())) > 1 or len(runtimes.get("libhsa-runtime64", ())) > 1:
+    if len(runtimes.get("libamdhip64", ())) > 1:
         raise ImportError("retina_amd: two HIP runtimes are mapped in this process: %r" % runtimes)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
