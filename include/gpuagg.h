@@ -43,6 +43,7 @@ extern "C" {
 #define GPUAGG_ESTATE (-5)     /* call not valid in the ctx's current state      */
 #define GPUAGG_EDUPLICATE (-6) /* two metrics would register the same family     */
 #define GPUAGG_ERANGE (-7)     /* value outside the encodable range              */
+#define GPUAGG_ENOTFOUND (-8)  /* no such object (cache.go's "not found in cache") */
 
 typedef struct gpuagg_ctx gpuagg_ctx;
 
@@ -67,6 +68,8 @@ typedef struct gpuagg_config {
 #define GPUAGG_FLAG_NO_LDS_IP_TABLE 1u /* keep the IP table in HBM/L2 only (diagnostics) */
 
 int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out);
+/* Number of gfx950 devices visible to this process (one ctx per device). */
+int gpuagg_device_count(int *n);
 void gpuagg_destroy(gpuagg_ctx *ctx);
 const char *gpuagg_last_error(const gpuagg_ctx *ctx);
 
@@ -75,7 +78,10 @@ const char *gpuagg_last_error(const gpuagg_ctx *ctx);
  * (crd/api/v1alpha1/metricsconfiguration_types.go:27-58).  A *_set flag of 0 means
  * the Go slice was nil (which changes behaviour, basemetricsobject.go:31-49).
  * Resets all accumulated state, like Clean() + ResetAdvancedMetricsRegistry()
- * (metrics_module.go:208-213).
+ * (metrics_module.go:208-213) -- unless the options equal the current ones under
+ * validations.MetricsContextOptionsCompare (same metric names, label lists equal as sets;
+ * validate_metricconfiguration.go:118-160, utils/common.go:58-84), in which case Module.Reconcile
+ * leaves the metrics alone (metrics_module.go:142-166) and so does this call.
  * ---------------------------------------------------------------------------- */
 typedef struct gpuagg_metric_options {
   const char *metric_name;
@@ -107,6 +113,36 @@ int gpuagg_slot_intern(gpuagg_ctx *ctx, const char *namespace_, const char *pod_
                        const char *workload_kind, const char *workload_name, int32_t *slot);
 int gpuagg_set_endpoints(gpuagg_ctx *ctx, const uint32_t *ipv4, const int32_t *slot, size_t n,
                          uint64_t version);
+
+/* ------------------------------------------------------------------------------
+ * The IP cache itself (pkg/controllers/cache/cache.go), kept natively so the IP -> pod
+ * map follows the reference's update/delete rules exactly: an update first deletes
+ * every object holding one of its IPs -- the WHOLE object, all its IPs (deleteByIP,
+ * cache.go:394-420; deleteEndpoint :315-337) -- and an IP no longer listed by an
+ * updated pod keeps pointing at it (updateEndpoint :204-233).  Services and nodes own
+ * IPs too (updateSvc :244-270, updateNode :282-305) and resolve to no endpoint.
+ * Endpoints are keyed "namespace/name" (BaseObject.Key, baseobject.go:19-21), nodes by
+ * name.  gpuagg_cache_commit installs the cache's current IP -> pod map (as
+ * gpuagg_set_endpoints does) for batches submitted after it.
+ * ---------------------------------------------------------------------------- */
+int gpuagg_cache_update_endpoint(gpuagg_ctx *ctx, const char *namespace_, const char *pod_name,
+                                 const char *workload_kind, const char *workload_name,
+                                 const uint32_t *ipv4, size_t n_ips);
+int gpuagg_cache_delete_endpoint(gpuagg_ctx *ctx, const char *namespace_, const char *pod_name);
+int gpuagg_cache_update_service(gpuagg_ctx *ctx, const char *namespace_, const char *name, uint32_t ipv4);
+int gpuagg_cache_delete_service(gpuagg_ctx *ctx, const char *namespace_, const char *name);
+int gpuagg_cache_update_node(gpuagg_ctx *ctx, const char *name, uint32_t ipv4);
+int gpuagg_cache_delete_node(gpuagg_ctx *ctx, const char *name);
+int gpuagg_cache_commit(gpuagg_ctx *ctx, uint64_t version);
+
+/* Slot lifecycle.  Dense counters and HLL registers are sized by the slots in use (grown
+ * when an endpoint table references a new slot, up to max_slots).  gpuagg_retire_slots
+ * frees every slot the installed IP table no longer references: its counters, HLL
+ * registers and group-by entries are cleared and the id is reused by a later
+ * gpuagg_slot_intern.  Call it at an epoch boundary, after the epoch's snapshot was
+ * published (the published series keep their last values, as the reference's gauges
+ * of a deleted pod do). */
+int gpuagg_retire_slots(gpuagg_ctx *ctx, size_t *n_retired);
 
 /* DNS label payload dictionary (utils.AddDNSInfo, flow_utils.go:186-220): interns
  * (rcode, qtypes joined with ",", query, ips joined with ",", num_answers) and
@@ -205,6 +241,14 @@ int gpuagg_sync(gpuagg_ctx *ctx);
  * metric plan, endpoints and dictionaries (used after a multi-GPU epoch merge). */
 int gpuagg_reset(gpuagg_ctx *ctx);
 
+/* Single-process multi-GPU merge (the Go agent drives every GPU of the node from one
+ * process): folds the state of ctxs[1..n) into ctxs[0] -- dense counters and count-min
+ * summed, HLL registers max-ed, group-by entries inserted-and-added -- over peer copies
+ * (xGMI between MI355X devices), then resets ctxs[1..n).  Every ctx must have the same
+ * metric plan and the same slot / DNS dictionaries (fed the same cache updates in the
+ * same order).  The one-process-per-GPU equivalent is retina_amd/dist.py (RCCL). */
+int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n);
+
 /* ------------------------------------------------------------------------------
  * Output: the Prometheus series the reference's GaugeVec/CounterVec would hold
  * (names under namespace "networkobservability", prometheusexporter.go:11,46-66).
@@ -217,6 +261,22 @@ size_t gpuagg_result_count(const gpuagg_result *r);
 int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric,
                          uint32_t *n_labels, const char *const **label_names,
                          const char *const **label_values, uint64_t *value);
+/* The series' Prometheus family: type "gauge" or "counter" and Help text, as the
+ * reference's Init creates the vector (forward.go:18-26,47-64, drops.go:18-23,42-60,
+ * tcpflags.go:18-24,43-51, tcpretrans.go:18-24,43-51 -- GaugeVec; dns.go:21-30,50-66 --
+ * CounterVec; exporter.CreatePrometheus{Gauge,Counter}VecForMetric,
+ * prometheusexporter.go:46-66). */
+int gpuagg_result_family(const gpuagg_result *r, size_t i, const char **type, const char **help);
+/* Group-by updates lost to a full table since the last reset (0 = every series exact).
+ * The snapshot still succeeds; series of the lost updates undercount. */
+uint64_t gpuagg_result_dropped(const gpuagg_result *r);
+/* Renders the series in the Prometheus text exposition format (0.0.4) exactly as
+ * client_golang's registry Gather + expfmt would for the AdvancedRegistry: families
+ * sorted by name with # HELP / # TYPE lines, label pairs sorted by name, series sorted by
+ * label values, values as Go strconv.FormatFloat(v, 'g', -1, 64).  *len receives the
+ * full length; buf (cap bytes, may be NULL) gets the text and a NUL when it fits,
+ * else GPUAGG_ECAPACITY. */
+int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len);
 void gpuagg_result_free(gpuagg_result *r);
 
 /* ------------------------------------------------------------------------------

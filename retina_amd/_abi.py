@@ -14,9 +14,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPUAGG_LIB") or os.path.join(HERE, "libgpuagg.so")
 
 ABI_VERSION = 1
-OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE = 0, -1, -2, -3, -4, -5, -6, -7
+OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE, ENOTFOUND = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ERR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", ECAPACITY: "ECAPACITY",
-             ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE"}
+             ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE", ENOTFOUND: "ENOTFOUND"}
 
 u32p = C.POINTER(C.c_uint32)
 
@@ -111,6 +111,20 @@ SIGNATURES = [
     ("gpuagg_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("gpuagg_stream", C.c_void_p, [C.c_void_p]),
     ("gpuagg_kernel_name", C.c_char_p, [C.c_void_p]),
+    ("gpuagg_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("gpuagg_cache_update_endpoint", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                               u32p, C.c_size_t]),
+    ("gpuagg_cache_delete_endpoint", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    ("gpuagg_cache_update_service", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]),
+    ("gpuagg_cache_delete_service", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    ("gpuagg_cache_update_node", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32]),
+    ("gpuagg_cache_delete_node", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("gpuagg_cache_commit", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("gpuagg_retire_slots", C.c_int, [C.c_void_p, C.POINTER(C.c_size_t)]),
+    ("gpuagg_merge", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    ("gpuagg_result_family", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
+    ("gpuagg_result_dropped", C.c_uint64, [C.c_void_p]),
+    ("gpuagg_result_render_text", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 ]
 
 _lib = None

@@ -1218,6 +1218,87 @@ __global__ void sparse_import_kernel(DevSparse s, const unsigned long long *in, 
   }
 }
 
+// ---- slot retirement and the single-process multi-GPU merge ----------------------------
+// Zeroes the dense bins of retired slots: workgroup b takes dead slot b, its lanes the
+// (group, side, sub) bins of that slot in every endpoint-keyed dense group.
+__global__ void zero_slots_kernel(unsigned long long *cnt, unsigned long long *byt, const uint32_t *dead,
+                                  Plan p) {
+  const uint32_t slot = dead[blockIdx.x];
+  for (int g = 0; g < p.ngroups; ++g) {
+    const GroupPlan gp = p.g[g];
+    if (gp.sparse || !gp.key_mode) continue;
+    const uint64_t lo = gp.dense_base + (uint64_t)slot * 2u * gp.nsub;
+    for (uint32_t i = threadIdx.x; i < 2u * gp.nsub; i += blockDim.x) {
+      cnt[lo + i] = 0ULL;
+      byt[lo + i] = 0ULL;
+    }
+  }
+}
+
+// Zeroes the 2^p HLL registers of each retired slot (16-byte stores).
+__global__ void zero_hll_rows_kernel(uint8_t *hll, const uint32_t *dead, uint32_t p) {
+  uint4 *row = (uint4 *)(hll + ((size_t)dead[blockIdx.x] << p));
+  for (uint32_t i = threadIdx.x; i < (1u << p) / 16u; i += blockDim.x) row[i] = make_uint4(0, 0, 0, 0);
+}
+
+// dst[i] op= src[i] for the merge (grid-stride, vectorised where the type allows).
+__global__ void add_u64_kernel(unsigned long long *dst, const unsigned long long *src, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+__global__ void add_u32_kernel(uint32_t *dst, const uint32_t *src, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+__global__ void max_u8_kernel(uint8_t *dst, const uint8_t *src, size_t n) {
+  // u8 registers, 4 per lane-word: byte-wise max on the whole words, tail bytewise
+  const size_t nw = n / 4;
+  uint32_t *dw = (uint32_t *)dst;
+  const uint32_t *sw = (const uint32_t *)src;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t a = dw[i], b = sw[i];
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = (a >> (8 * k)) & 0xFFu, y = (b >> (8 * k)) & 0xFFu;
+      r |= (x > y ? x : y) << (8 * k);
+    }
+    dw[i] = r;
+  }
+  for (size_t i = nw * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = dst[i] > src[i] ? dst[i] : src[i];
+}
+
+hipError_t launch_zero_slots(uint64_t *cnt, uint64_t *byt, uint8_t *hll, uint32_t hll_p, const uint32_t *dead,
+                             uint32_t ndead, const Plan &p, hipStream_t st) {
+  if (!ndead) return hipSuccess;
+  if (cnt) {
+    hipLaunchKernelGGL(zero_slots_kernel, dim3(ndead), dim3(64), 0, st, (unsigned long long *)cnt,
+                       (unsigned long long *)byt, dead, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (hll) hipLaunchKernelGGL(zero_hll_rows_kernel, dim3(ndead), dim3(256), 0, st, hll, dead, hll_p);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_add_u64(uint64_t *dst, const uint64_t *src, size_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(add_u64_kernel, dim3(2048), dim3(256), 0, st, (unsigned long long *)dst,
+                     (const unsigned long long *)src, n);
+  return hipGetLastError();
+}
+hipError_t launch_merge_add_u32(uint32_t *dst, const uint32_t *src, size_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(add_u32_kernel, dim3(2048), dim3(256), 0, st, dst, src, n);
+  return hipGetLastError();
+}
+hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(max_u8_kernel, dim3(2048), dim3(256), 0, st, dst, src, n);
+  return hipGetLastError();
+}
+
 // ---- launch wrappers called by the host runtime ---------------------------------------
 
 static DevSparse dev_sparse(const SparseView &v) {

@@ -93,6 +93,14 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between,
                             const char **kernel = nullptr);
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st);
+// Clears the dense bins (every endpoint-keyed dense group) and HLL rows (hll may be null)
+// of the ndead slots listed at dead (device u32 array).
+hipError_t launch_zero_slots(uint64_t *cnt, uint64_t *byt, uint8_t *hll, uint32_t hll_p, const uint32_t *dead,
+                             uint32_t ndead, const Plan &p, hipStream_t st);
+// Element-wise merge folds: dst += src (u64, u32) and dst = max(dst, src) (u8).
+hipError_t launch_merge_add_u64(uint64_t *dst, const uint64_t *src, size_t n, hipStream_t st);
+hipError_t launch_merge_add_u32(uint32_t *dst, const uint32_t *src, size_t n, hipStream_t st);
+hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipStream_t st);
 hipError_t launch_sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t out_cap,
                                 uint64_t *counter, hipStream_t st);
 hipError_t launch_sparse_import(const SparseView &v, const uint64_t *in, size_t n, hipStream_t st);

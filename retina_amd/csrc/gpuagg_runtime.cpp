@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -68,6 +69,7 @@ struct SlotAttr {
   std::string ns, pod, wk_kind, wk_name;
   bool has_owner = false;
   bool api = false;
+  bool in_use = true;  // false once retired (gpuagg_retire_slots); the id is then reusable
 };
 
 struct DnsAttr {
@@ -102,6 +104,31 @@ struct Series {
   std::string metric;
   std::vector<std::string> names, values;
   uint64_t value;
+  const char *type, *help;  // Prometheus family (static strings)
+};
+
+// A metric family's Prometheus type and Help text, as the reference's Init creates its
+// vector (forward.go:18-26,47-64; drops.go:18-23,42-60; tcpflags.go:18-24,43-51;
+// tcpretrans.go:18-24,43-51: GaugeVec; dns.go:21-30,50-66: CounterVec).
+struct FamilyInfo {
+  const char *type, *help;
+};
+FamilyInfo family_info(const std::string &vec) {
+  if (vec == "adv_forward_count") return {"gauge", "Total number of forwarded packets"};
+  if (vec == "adv_forward_bytes") return {"gauge", "Total number of forwarded bytes"};
+  if (vec == "adv_drop_count") return {"gauge", "Total number of dropped packets"};
+  if (vec == "adv_drop_bytes") return {"gauge", "Total number of dropped bytes"};
+  if (vec == "adv_tcpflags_count") return {"gauge", "Total number of packets by TCP flag"};
+  if (vec == "adv_tcpretrans_count") return {"gauge", "Total number of TCP retransmitted packets"};
+  if (vec == "adv_dns_request_count") return {"counter", "Total number of DNS query packets"};
+  if (vec == "adv_dns_response_count") return {"counter", "Total number of DNS response packets"};
+  return {"untyped", ""};
+}
+
+// Options of one MetricsContextOptions as last applied (the reconcile no-op comparison).
+struct OptCopy {
+  std::string name;
+  std::vector<std::string> src, dst;
 };
 
 }  // namespace
@@ -109,6 +136,7 @@ struct Series {
 struct gpuagg_result {
   std::vector<Series> series;
   std::vector<std::vector<const char *>> name_ptrs, value_ptrs;
+  uint64_t dropped = 0;
 };
 
 struct gpuagg_ctx {
@@ -126,6 +154,20 @@ struct gpuagg_ctx {
   // identity dictionaries
   std::map<std::tuple<std::string, std::string, std::string, std::string, int>, int32_t> slot_ids;
   std::vector<SlotAttr> slots;
+  std::vector<int32_t> free_slots;  // retired ids, reused first by gpuagg_slot_intern
+  uint32_t key_cap = 0;             // slots covered by the dense counters and HLL rows
+  std::vector<std::pair<uint32_t, int32_t>> installed;  // the installed IP -> slot map
+  std::vector<OptCopy> cur_opts;    // options of the last applied reconcile
+  bool have_opts = false;
+  // native IP cache (cache.go): endpoints "ns/name" -> (slot, IPs); services, nodes -> IP
+  struct CacheEp {
+    int32_t slot;
+    std::vector<uint32_t> ips;
+  };
+  std::unordered_map<std::string, CacheEp> ep_map;
+  std::unordered_map<uint32_t, std::string> ip_to_ep;
+  std::unordered_map<std::string, uint32_t> svc_map, node_map;
+  std::unordered_map<uint32_t, std::string> ip_to_svc, ip_to_node;
   std::unordered_map<std::string, uint32_t> dns_ids;
   std::vector<DnsAttr> dns;
 
@@ -373,6 +415,82 @@ int ensure_sparse(gpuagg_ctx *c) {
   c->sv.byt = c->sv.k0 + 4;
   c->sv.mask = (uint32_t)(n - 1);
   c->sparse_slots = n;
+  return GPUAGG_OK;
+}
+
+// Slots covered by the dense counters / HLL rows for n interned slots: whole 64-slot
+// steps (not powers of two, so the tier-1 kernel's LDS window keeps fitting C2's 10k
+// pods), never beyond max_slots.
+uint32_t key_cap_for(const gpuagg_ctx *c, size_t n) {
+  const size_t cap = std::max<size_t>(64, (n + 63) & ~(size_t)63);
+  return (uint32_t)std::min<size_t>(cap, c->cfg.max_slots);
+}
+
+// Lays the dense groups out for key_cap slots (hottest group first, see reconcile) and
+// sizes the HLL rows.  keep: the accumulated counters / registers move to the new layout
+// -- a group's bins are key-major, so its old bins are the prefix of its new ones -- else
+// the new state is zero.
+int layout_dense(gpuagg_ctx *c, uint32_t key_cap, bool keep) {
+  uint64_t total = 0;
+  std::vector<uint64_t> base(c->groups.size(), 0), old_base(c->groups.size(), 0), old_nbins(c->groups.size(), 0);
+  for (size_t g = 0; g < c->groups.size(); ++g) {
+    Group &gr = c->groups[g];
+    if (gr.sparse) continue;
+    old_base[g] = gr.dense_base;
+    old_nbins[g] = gr.nkeys * 2 * gr.nsub;
+    const uint64_t nkeys = gr.key_mode ? key_cap : 1;
+    base[g] = total;
+    total += nkeys * 2 * gr.nsub;
+  }
+  if (total >= (1ull << 32)) return fail(c, GPUAGG_ECAPACITY, "dense counter space >= 2^32 bins");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int rc;
+  uint64_t *cnt = nullptr, *byt = nullptr;
+  if ((rc = dev_alloc(c, &cnt, total)) || (rc = dev_alloc(c, &byt, total))) {
+    dev_free(cnt);
+    return rc;
+  }
+  if (total) {
+    HIPCHK(c, hipMemsetAsync(cnt, 0, total * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(byt, 0, total * 8, c->stream));
+  }
+  for (size_t g = 0; keep && c->dense_len && g < c->groups.size(); ++g) {
+    if (c->groups[g].sparse || !old_nbins[g]) continue;
+    const uint64_t nb = std::min<uint64_t>(old_nbins[g], total - base[g]);
+    HIPCHK(c, hipMemcpyAsync(cnt + base[g], c->d_dense_cnt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(byt + base[g], c->d_dense_byt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (c->cfg.hll_precision) {
+    const size_t len = (size_t)key_cap << c->cfg.hll_precision;
+    uint8_t *hll = nullptr;
+    if ((rc = dev_alloc(c, &hll, len))) {
+      dev_free(cnt);
+      dev_free(byt);
+      return rc;
+    }
+    HIPCHK(c, hipMemsetAsync(hll, 0, len, c->stream));
+    if (keep && c->hll_len)
+      HIPCHK(c, hipMemcpyAsync(hll, c->d_hll, std::min(len, c->hll_len), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dev_free(c->d_hll);
+    c->d_hll = hll;
+    c->hll_len = len;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dev_free(c->d_dense_cnt);
+  dev_free(c->d_dense_byt);
+  c->d_dense_cnt = cnt;
+  c->d_dense_byt = byt;
+  c->dense_len = total;
+  for (size_t g = 0; g < c->groups.size(); ++g) {
+    Group &gr = c->groups[g];
+    if (gr.sparse) continue;
+    gr.dense_base = base[g];
+    gr.nkeys = gr.key_mode ? key_cap : 1;
+    c->plan.g[g].dense_base = base[g];
+    c->plan.g[g].nbins = (uint32_t)(gr.nkeys * 2 * gr.nsub);
+  }
+  c->key_cap = key_cap;
   return GPUAGG_OK;
 }
 
@@ -691,14 +809,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
       return GPUAGG_ENOMEM;
     }
   }
-  if (cfg->hll_precision) {
-    c->hll_len = (size_t)cfg->max_slots << cfg->hll_precision;
-    if (dev_alloc(c.get(), &c->d_hll, c->hll_len)) {
-      gpuagg_destroy(c.release());
-      return GPUAGG_ENOMEM;
-    }
-  }
-  if (reset_state(c.get())) {
+  if (layout_dense(c.get(), key_cap_for(c.get(), 0), false) || reset_state(c.get())) {
     gpuagg_destroy(c.release());
     return GPUAGG_EDEVICE;
   }
@@ -748,10 +859,43 @@ void gpuagg_destroy(gpuagg_ctx *c) {
 
 const char *gpuagg_last_error(const gpuagg_ctx *c) { return c ? c->err.c_str() : "null ctx"; }
 
+// validations.MetricsContextOptionsCompare (validate_metricconfiguration.go:118-160):
+// same number of entries, same metric names (last entry of a name wins), source and
+// destination label lists equal as sets (utils.CompareStringSlice, common.go:58-84).
+bool same_options(const std::vector<OptCopy> &a, const std::vector<OptCopy> &b) {
+  if (a.size() != b.size()) return false;
+  std::map<std::string, const OptCopy *> ma, mb;
+  for (auto &o : a) ma[o.name] = &o;
+  for (auto &o : b) mb[o.name] = &o;
+  if (ma.size() != mb.size()) return false;
+  auto same_set = [](const std::vector<std::string> &x, const std::vector<std::string> &y) {
+    if (x.size() != y.size()) return false;
+    std::set<std::string> sx(x.begin(), x.end()), sy(y.begin(), y.end());
+    return sx == sy;
+  };
+  for (auto &kv : ma) {
+    auto it = mb.find(kv.first);
+    if (it == mb.end()) return false;
+    if (!same_set(kv.second->src, it->second->src) || !same_set(kv.second->dst, it->second->dst)) return false;
+  }
+  return true;
+}
+
 int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n) {
   if (!c || (n && !opts)) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  std::vector<OptCopy> new_opts(n);
+  for (size_t i = 0; i < n; ++i) {
+    new_opts[i].name = opts[i].metric_name ? opts[i].metric_name : "";
+    for (uint32_t k = 0; opts[i].source_labels && k < opts[i].n_source_labels; ++k)
+      new_opts[i].src.push_back(opts[i].source_labels[k] ? opts[i].source_labels[k] : "");
+    for (uint32_t k = 0; opts[i].destination_labels && k < opts[i].n_destination_labels; ++k)
+      new_opts[i].dst.push_back(opts[i].destination_labels[k] ? opts[i].destination_labels[k] : "");
+  }
+  // Module.Reconcile leaves the metrics alone when the context options compare equal
+  // (metrics_module.go:142-166): a resync or a namespace-only change keeps the counters
+  if (c->have_opts && same_options(c->cur_opts, new_opts)) return GPUAGG_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const bool local = !c->remote;
 
@@ -859,7 +1003,6 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
 
   // groups: one per (family, effective options)
   std::vector<Group> groups;
-  uint64_t dense_total = 0;
   for (auto &in : inst) {
     in.group = -1;
     if (!in.active) continue;
@@ -880,7 +1023,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
       g.sparse = !local || dns || (so & (OPT_IP | OPT_PORT));
       if (!g.sparse) {
         g.key_mode = (so & OPT_EP) ? 1 : 0;
-        g.nkeys = g.key_mode ? c->cfg.max_slots : 1;
+        g.nkeys = 0;  // laid out by layout_dense
         g.nsub = (in.family == FAM_DROP || in.family == FAM_TCPFLAGS) ? 8 : 1;
       }
       groups.push_back(g);
@@ -910,13 +1053,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
     groups.swap(sorted);
     for (auto &in : inst)
       if (in.group >= 0) in.group = new_index[in.group];
-    for (auto &g : groups) {
-      if (g.sparse) continue;
-      g.dense_base = dense_total;
-      dense_total += g.nkeys * 2 * g.nsub;
-    }
   }
-  if (dense_total >= (1ull << 32)) return fail(c, GPUAGG_ECAPACITY, "dense counter space >= 2^32 bins");
 
   Plan p{};
   p.local = local ? 1 : 0;
@@ -929,28 +1066,21 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
     gp.src_opts = groups[g].src_opts;
     gp.dst_opts = groups[g].dst_opts;
     gp.nsub = groups[g].nsub;
-    gp.dense_base = groups[g].dense_base;
     gp.key_mode = groups[g].key_mode;
-    gp.nbins = groups[g].sparse ? 0u : (uint32_t)(groups[g].nkeys * 2 * groups[g].nsub);
     if ((gp.src_opts | gp.dst_opts) & OPT_PORT) p.need_ports = 1;
     if (gp.family == FAM_DNS_REQ || gp.family == FAM_DNS_RESP) p.need_dns = 1;
     if (gp.family == FAM_FWD || gp.family == FAM_DROP) p.need_bytes = 1;
     any_sparse |= groups[g].sparse;
   }
 
-  // (re)allocate state
-  if (dense_total != c->dense_len) {
-    dev_free(c->d_dense_cnt);
-    dev_free(c->d_dense_byt);
-    c->dense_len = 0;
-    if ((rc = dev_alloc(c, &c->d_dense_cnt, dense_total)) || (rc = dev_alloc(c, &c->d_dense_byt, dense_total)))
-      return rc;
-    c->dense_len = dense_total;
-  }
+  // (re)allocate state: dense counters for the slots in use, zeroed
   if (any_sparse && (rc = ensure_sparse(c))) return rc;
   c->inst = inst;
   c->groups = groups;
   c->plan = p;
+  if ((rc = layout_dense(c, key_cap_for(c, c->slots.size()), false))) return rc;
+  c->cur_opts = new_opts;
+  c->have_opts = true;
   return reset_state(c);
 }
 
@@ -965,8 +1095,9 @@ int gpuagg_slot_intern(gpuagg_ctx *c, const char *ns, const char *pod, const cha
     *slot = it->second;
     return GPUAGG_OK;
   }
-  if (c->slots.size() >= c->cfg.max_slots)
-    return fail(c, GPUAGG_ECAPACITY, "more than max_slots=%u endpoint identities", c->cfg.max_slots);
+  if (c->free_slots.empty() && c->slots.size() >= c->cfg.max_slots)
+    return fail(c, GPUAGG_ECAPACITY, "more than max_slots=%u endpoint identities (retire unused ones "
+                "with gpuagg_retire_slots)", c->cfg.max_slots);
   SlotAttr a;
   a.ns = ns;
   a.pod = pod;
@@ -976,8 +1107,15 @@ int gpuagg_slot_intern(gpuagg_ctx *c, const char *ns, const char *pod, const cha
     a.wk_name = wk_name ? wk_name : "";
   }
   a.api = a.ns == kApiServer && a.pod == kApiServer;
-  const int32_t id = (int32_t)c->slots.size();
-  c->slots.push_back(a);
+  int32_t id;
+  if (!c->free_slots.empty()) {  // a retired id: its state was cleared when it retired
+    id = c->free_slots.back();
+    c->free_slots.pop_back();
+    c->slots[id] = a;
+  } else {
+    id = (int32_t)c->slots.size();
+    c->slots.push_back(a);
+  }
   c->slot_ids.emplace(key, id);
   *slot = id;
   return GPUAGG_OK;
@@ -993,7 +1131,7 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   std::unordered_map<uint32_t, uint64_t> last;
   last.reserve(n * 2 + 1);
   for (size_t i = 0; i < n; ++i) {
-    if (slot[i] < 0 || (size_t)slot[i] >= c->slots.size())
+    if (slot[i] < 0 || (size_t)slot[i] >= c->slots.size() || !c->slots[slot[i]].in_use)
       return fail(c, GPUAGG_EINVAL, "entry %zu: slot %d was not interned", i, slot[i]);
     if (ipv4[i] == 0xFFFFFFFFu) return fail(c, GPUAGG_ERANGE, "255.255.255.255 cannot be a pod IP");
     last[ipv4[i]] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
@@ -1029,6 +1167,9 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     if (cap > ((size_t)1 << 30)) return fail(c, GPUAGG_ECAPACITY, "IP table cannot be built");
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches use the old table
+  // dense counters / HLL rows cover every interned slot
+  if (c->slots.size() > c->key_cap && (rc = layout_dense(c, key_cap_for(c, c->slots.size()), true)))
+    return rc;
   if (cap != c->ip_cap) {
     dev_free(c->d_ip);
     c->ip_cap = 0;
@@ -1061,6 +1202,191 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   }
   c->ip_seed = seed;
   c->ip_version = version;
+  c->installed.clear();
+  for (const auto &kv : last) c->installed.emplace_back(kv.first, (int32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
+  return GPUAGG_OK;
+}
+
+// ---- the IP cache (cache.go), restated natively --------------------------------------
+namespace {
+
+int cache_delete_endpoint_key(gpuagg_ctx *c, const std::string &key) {  // deleteEndpoint (:315-337)
+  auto it = c->ep_map.find(key);
+  if (it == c->ep_map.end()) return GPUAGG_OK;  // "ignore the error if the endpoint is not found"
+  for (uint32_t ip : it->second.ips) c->ip_to_ep.erase(ip);
+  c->ep_map.erase(it);
+  return GPUAGG_OK;
+}
+int cache_delete_svc_key(gpuagg_ctx *c, const std::string &key) {  // deleteSvc (:348-368)
+  auto it = c->svc_map.find(key);
+  if (it == c->svc_map.end()) return fail(c, GPUAGG_ENOTFOUND, "service not found in cache: %s", key.c_str());
+  c->ip_to_svc.erase(it->second);
+  c->svc_map.erase(it);
+  return GPUAGG_OK;
+}
+int cache_delete_node_key(gpuagg_ctx *c, const std::string &name) {  // deleteNode (:379-392)
+  auto it = c->node_map.find(name);
+  if (it == c->node_map.end()) return fail(c, GPUAGG_ENOTFOUND, "node not found in cache: %s", name.c_str());
+  c->ip_to_node.erase(it->second);
+  c->node_map.erase(it);
+  return GPUAGG_OK;
+}
+// deleteByIP (:394-420): the object holding ip, unless it is `key` itself; services first,
+// then pods, then nodes
+int cache_delete_by_ip(gpuagg_ctx *c, uint32_t ip, const std::string &key) {
+  auto s = c->ip_to_svc.find(ip);
+  if (s != c->ip_to_svc.end()) return s->second == key ? GPUAGG_OK : cache_delete_svc_key(c, std::string(s->second));
+  auto e = c->ip_to_ep.find(ip);
+  if (e != c->ip_to_ep.end()) return e->second == key ? GPUAGG_OK : cache_delete_endpoint_key(c, std::string(e->second));
+  auto n = c->ip_to_node.find(ip);
+  if (n != c->ip_to_node.end()) return n->second == key ? GPUAGG_OK : cache_delete_node_key(c, std::string(n->second));
+  return GPUAGG_OK;
+}
+std::string ep_key(const char *ns, const char *name) { return std::string(ns) + "/" + name; }
+
+}  // namespace
+
+int gpuagg_cache_update_endpoint(gpuagg_ctx *c, const char *ns, const char *pod, const char *wk_kind,
+                                 const char *wk_name, const uint32_t *ipv4, size_t n_ips) {
+  if (!c || !ns || !pod || (n_ips && !ipv4)) return GPUAGG_EINVAL;
+  const std::string key = ep_key(ns, pod);
+  if (!n_ips) return fail(c, GPUAGG_EINVAL, "no IP found for endpoint %s", key.c_str());  // ep.IPs() error
+  int32_t slot;
+  int rc = gpuagg_slot_intern(c, ns, pod, wk_kind, wk_name, &slot);
+  if (rc) return rc;
+  for (size_t i = 0; i < n_ips; ++i)  // updateEndpoint (:204-233)
+    if ((rc = cache_delete_by_ip(c, ipv4[i], key))) return rc;
+  gpuagg_ctx::CacheEp &e = c->ep_map[key];
+  e.slot = slot;
+  e.ips.assign(ipv4, ipv4 + n_ips);
+  for (size_t i = 0; i < n_ips; ++i) c->ip_to_ep[ipv4[i]] = key;
+  return GPUAGG_OK;
+}
+
+int gpuagg_cache_delete_endpoint(gpuagg_ctx *c, const char *ns, const char *pod) {
+  if (!c || !ns || !pod) return GPUAGG_EINVAL;
+  return cache_delete_endpoint_key(c, ep_key(ns, pod));
+}
+
+int gpuagg_cache_update_service(gpuagg_ctx *c, const char *ns, const char *name, uint32_t ipv4) {
+  if (!c || !ns || !name) return GPUAGG_EINVAL;
+  const std::string key = ep_key(ns, name);
+  int rc = cache_delete_by_ip(c, ipv4, key);  // updateSvc (:244-270)
+  if (rc) return rc;
+  c->ip_to_svc[ipv4] = key;
+  c->svc_map[key] = ipv4;
+  return GPUAGG_OK;
+}
+
+int gpuagg_cache_delete_service(gpuagg_ctx *c, const char *ns, const char *name) {
+  if (!c || !ns || !name) return GPUAGG_EINVAL;
+  return cache_delete_svc_key(c, ep_key(ns, name));
+}
+
+int gpuagg_cache_update_node(gpuagg_ctx *c, const char *name, uint32_t ipv4) {
+  if (!c || !name) return GPUAGG_EINVAL;
+  int rc = cache_delete_by_ip(c, ipv4, name);  // updateNode (:282-305)
+  if (rc) return rc;
+  c->node_map[name] = ipv4;
+  c->ip_to_node[ipv4] = name;
+  return GPUAGG_OK;
+}
+
+int gpuagg_cache_delete_node(gpuagg_ctx *c, const char *name) {
+  if (!c || !name) return GPUAGG_EINVAL;
+  return cache_delete_node_key(c, name);
+}
+
+int gpuagg_cache_commit(gpuagg_ctx *c, uint64_t version) {
+  if (!c) return GPUAGG_EINVAL;
+  // GetObjByIP (cache.go:154-169): an IP resolves to a pod when ipToEpKey names an
+  // endpoint still in epMap (an IP an updated pod no longer lists keeps pointing at it)
+  std::vector<uint32_t> ips;
+  std::vector<int32_t> slots;
+  ips.reserve(c->ip_to_ep.size());
+  slots.reserve(c->ip_to_ep.size());
+  for (const auto &kv : c->ip_to_ep) {
+    auto e = c->ep_map.find(kv.second);
+    if (e == c->ep_map.end()) continue;
+    ips.push_back(kv.first);
+    slots.push_back(e->second.slot);
+  }
+  return gpuagg_set_endpoints(c, ips.data(), slots.data(), ips.size(), version);
+}
+
+int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
+  if (!c) return GPUAGG_EINVAL;
+  if (n_retired) *n_retired = 0;
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<char> live(c->slots.size(), 0);
+  for (const auto &e : c->installed) live[e.second] = 1;
+  std::vector<uint32_t> dead;
+  for (size_t s = 0; s < c->slots.size(); ++s)
+    if (c->slots[s].in_use && !live[s]) dead.push_back((uint32_t)s);
+  if (dead.empty()) return GPUAGG_OK;
+  // dense bins and HLL rows of the dead slots (slots < key_cap: set_endpoints grew it)
+  std::vector<uint32_t> dead_dev;
+  for (uint32_t s : dead)
+    if (s < c->key_cap) dead_dev.push_back(s);
+  if (!dead_dev.empty() && (c->dense_len || c->hll_len)) {
+    uint32_t *d = nullptr;
+    if ((rc = dev_alloc(c, &d, dead_dev.size()))) return rc;
+    hipError_t e = hipMemcpyAsync(d, dead_dev.data(), dead_dev.size() * 4, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+      e = launch_zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
+                            c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dev_free(d);
+    if (e != hipSuccess) return fail(c, GPUAGG_EDEVICE, "retire: %s", hipGetErrorString(e));
+  }
+  // group-by entries keyed by a dead slot (as source or destination): the table is
+  // rebuilt without them (export, filter on the host, re-insert)
+  if (c->sparse_slots) {
+    std::vector<char> is_dead(c->slots.size() + 1, 0);  // indexed by slot + 1
+    for (uint32_t s : dead) is_dead[s + 1] = 1;
+    if (c->export_cap < c->sparse_slots) {
+      dev_free(c->d_export);
+      c->export_cap = 0;
+      if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
+      c->export_cap = c->sparse_slots;
+    }
+    size_t nent = 0;
+    if ((rc = gpuagg_sparse_export(c, c->d_export, c->export_cap, &nent))) return rc;
+    std::vector<uint64_t> ent(nent * kSparseEntryWords);
+    if (nent) HIPCHK(c, hipMemcpy(ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
+    size_t keep = 0;
+    for (size_t i = 0; i < nent; ++i) {
+      const uint64_t *w = &ent[i * kSparseEntryWords];
+      const uint32_t s1 = key_s_slot1(w[0]), d1 = key_d_slot1(w[1]);
+      if ((s1 < is_dead.size() && is_dead[s1]) || (d1 < is_dead.size() && is_dead[d1])) continue;
+      memmove(&ent[keep * kSparseEntryWords], w, kSparseEntryWords * 8);
+      ++keep;
+    }
+    if (keep != nent) {
+      uint64_t dropped = 0;
+      HIPCHK(c, hipMemcpy(&dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+      if (keep) {
+        HIPCHK(c, hipMemcpyAsync(c->d_export, ent.data(), keep * kSparseEntryWords * 8, hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, launch_sparse_import(c->sv, c->d_export, keep, c->stream));
+      }
+      HIPCHK(c, hipMemcpyAsync(c->sv.dropped, &dropped, 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+  }
+  // the dictionary: ids become reusable
+  for (uint32_t s : dead) {
+    SlotAttr &a = c->slots[s];
+    c->slot_ids.erase(std::make_tuple(a.ns, a.pod, a.wk_kind, a.wk_name, a.has_owner ? 1 : 0));
+    a = SlotAttr();
+    a.in_use = false;
+    c->free_slots.push_back((int32_t)s);
+  }
+  std::sort(c->free_slots.begin(), c->free_slots.end(), std::greater<int32_t>());  // lowest id first
+  if (n_retired) *n_retired = dead.size();
   return GPUAGG_OK;
 }
 
@@ -1218,10 +1544,7 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
   if (c->sparse_slots) {
     uint64_t dropped = 0;
     HIPCHK(c, hipMemcpy(&dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
-    c->stats.sparse_dropped = dropped;
-    if (dropped)
-      return fail(c, GPUAGG_ECAPACITY, "group-by table full: %llu updates lost (raise sparse_capacity_log2)",
-                  (unsigned long long)dropped);
+    c->stats.sparse_dropped = dropped;  // reported with the result (gpuagg_result_dropped)
     if (c->export_cap < c->sparse_slots) {
       dev_free(c->d_export);
       if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
@@ -1300,8 +1623,13 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
   }
 
   auto *r = new gpuagg_result();
-  for (size_t ii = 0; ii < c->inst.size(); ++ii)
-    for (auto &kv : acc[ii]) r->series.push_back(Series{c->inst[ii].vec_name, c->inst[ii].label_names, kv.first, kv.second});
+  r->dropped = c->stats.sparse_dropped;
+  const size_t ns_len = strlen("networkobservability_");
+  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
+    const FamilyInfo fi = family_info(c->inst[ii].vec_name.substr(ns_len));
+    for (auto &kv : acc[ii])
+      r->series.push_back(Series{c->inst[ii].vec_name, c->inst[ii].label_names, kv.first, kv.second, fi.type, fi.help});
+  }
   r->name_ptrs.resize(r->series.size());
   r->value_ptrs.resize(r->series.size());
   for (size_t i = 0; i < r->series.size(); ++i) {
@@ -1319,6 +1647,125 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
 }
 
 size_t gpuagg_result_count(const gpuagg_result *r) { return r ? r->series.size() : 0; }
+
+int gpuagg_result_family(const gpuagg_result *r, size_t i, const char **type, const char **help) {
+  if (!r || i >= r->series.size()) return GPUAGG_EINVAL;
+  if (type) *type = r->series[i].type;
+  if (help) *help = r->series[i].help;
+  return GPUAGG_OK;
+}
+
+uint64_t gpuagg_result_dropped(const gpuagg_result *r) { return r ? r->dropped : 0; }
+
+namespace {
+// Go strconv.FormatFloat(v, 'g', -1, 64), as expfmt writes a sample value: the shortest
+// decimal digits d1.d2..dn x 10^x that round-trip, in %e form (exponent of at least two
+// digits) when x < -4 or x >= 6 -- Go's fmtG uses precision 6 for that choice when the
+// digits are the shortest (strconv/ftoa.go) -- else in %f form.
+std::string go_float_g(double v) {
+  if (v == 0) return "0";
+  char buf[64];
+  // shortest round-trip digits via %.17g probing
+  int prec = 1;
+  for (; prec <= 17; ++prec) {
+    snprintf(buf, sizeof buf, "%.*e", prec - 1, v);
+    if (strtod(buf, nullptr) == v) break;
+  }
+  // buf = d.ddde[+-]XX
+  std::string m(buf);
+  const size_t epos = m.find('e');
+  const int x = atoi(m.c_str() + epos + 1);
+  std::string digits;
+  for (size_t k = 0; k < epos; ++k)
+    if (isdigit((unsigned char)m[k])) digits += m[k];
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  const bool neg = v < 0;
+  // Go: shortest => eprec = 6; "%e is used if the exponent from the conversion is less
+  // than -4 or greater than or equal to the precision"; if eprec > digits and digits >=
+  // decimal point position, eprec = digits ... with shortest it is 6 (ftoa.go)
+  int eprec = 6;
+  std::string out = neg ? "-" : "";
+  if (x < -4 || x >= eprec) {
+    out += digits[0];
+    if (digits.size() > 1) {
+      out += '.';
+      out += digits.substr(1);
+    }
+    char e[16];
+    snprintf(e, sizeof e, "e%c%02d", x < 0 ? '-' : '+', x < 0 ? -x : x);
+    out += e;
+    return out;
+  }
+  if (x >= 0) {  // integer part digits[0..x], fraction the rest
+    std::string ip = digits.substr(0, std::min<size_t>(digits.size(), (size_t)x + 1));
+    while ((int)ip.size() < x + 1) ip += '0';
+    out += ip;
+    if (digits.size() > (size_t)x + 1) out += "." + digits.substr(x + 1);
+  } else {
+    out += "0." + std::string((size_t)(-x - 1), '0') + digits;
+  }
+  return out;
+}
+
+void escape_into(std::string &out, const std::string &s, bool quote) {  // expfmt escaping
+  for (char ch : s) {
+    if (ch == '\\') out += "\\\\";
+    else if (ch == '\n') out += "\\n";
+    else if (quote && ch == '"') out += "\\\"";
+    else out += ch;
+  }
+}
+}  // namespace
+
+int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
+  if (!r || !len) return GPUAGG_EINVAL;
+  // family name -> series indices; label pairs sorted by name (client_golang keeps a
+  // metric's label pairs sorted), series sorted by those values (MetricSorter)
+  std::map<std::string, std::vector<size_t>> fam;
+  for (size_t i = 0; i < r->series.size(); ++i) fam[r->series[i].metric].push_back(i);
+  std::vector<std::vector<std::pair<std::string, std::string>>> pairs(r->series.size());
+  for (size_t i = 0; i < r->series.size(); ++i) {
+    const Series &se = r->series[i];
+    for (size_t k = 0; k < se.names.size(); ++k) pairs[i].emplace_back(se.names[k], se.values[k]);
+    std::stable_sort(pairs[i].begin(), pairs[i].end(),
+                     [](const auto &a, const auto &b) { return a.first < b.first; });
+  }
+  std::string out;
+  for (auto &kv : fam) {
+    auto &idx = kv.second;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+      const auto &pa = pairs[a], &pb = pairs[b];
+      for (size_t k = 0; k < pa.size() && k < pb.size(); ++k)
+        if (pa[k].second != pb[k].second) return pa[k].second < pb[k].second;
+      return false;
+    });
+    const Series &first = r->series[idx[0]];
+    out += "# HELP " + kv.first + " ";
+    escape_into(out, first.help, false);
+    out += "\n# TYPE " + kv.first + " " + first.type + "\n";
+    for (size_t i : idx) {
+      out += kv.first;
+      if (!pairs[i].empty()) {
+        out += '{';
+        for (size_t k = 0; k < pairs[i].size(); ++k) {
+          if (k) out += ',';
+          out += pairs[i][k].first + "=\"";
+          escape_into(out, pairs[i][k].second, true);
+          out += '"';
+        }
+        out += '}';
+      }
+      out += ' ';
+      out += go_float_g((double)r->series[i].value);
+      out += '\n';
+    }
+  }
+  *len = out.size();
+  if (!buf) return GPUAGG_OK;
+  if (cap < out.size() + 1) return GPUAGG_ECAPACITY;
+  memcpy(buf, out.c_str(), out.size() + 1);
+  return GPUAGG_OK;
+}
 
 int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, uint32_t *n_labels,
                          const char *const **names, const char *const **values, uint64_t *value) {
@@ -1363,7 +1810,7 @@ int gpuagg_cms_estimate(gpuagg_ctx *c, uint32_t src, uint32_t dst, uint32_t port
 int gpuagg_hll_estimate(gpuagg_ctx *c, int32_t slot, double *est) {
   if (!c || !est) return GPUAGG_EINVAL;
   if (!c->hll_len || c->h_hll.size() != c->hll_len) return fail(c, GPUAGG_ESTATE, "no HLL snapshot");
-  if (slot < 0 || (uint32_t)slot >= c->cfg.max_slots) return GPUAGG_EINVAL;
+  if (slot < 0 || (uint32_t)slot >= c->key_cap) return GPUAGG_EINVAL;
   const uint32_t p = c->cfg.hll_precision;
   const size_t m = (size_t)1 << p;
   const uint8_t *reg = &c->h_hll[(size_t)slot << p];
@@ -1438,6 +1885,121 @@ int gpuagg_sparse_import(gpuagg_ctx *c, const uint64_t *dev_in, size_t n) {
   if ((rc = ensure_sparse(c))) return rc;
   HIPCHK(c, launch_sparse_import(c->sv, dev_in, n, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPUAGG_OK;
+}
+
+int gpuagg_device_count(int *n) {
+  if (!n) return GPUAGG_EINVAL;
+  *n = 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) return GPUAGG_EDEVICE;
+  for (int d = 0; d < ndev; ++d) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++*n;
+  }
+  return GPUAGG_OK;
+}
+
+int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
+  if (!ctxs || !n || !ctxs[0]) return GPUAGG_EINVAL;
+  gpuagg_ctx *c0 = ctxs[0];
+  int rc;
+  // compatibility: one metric plan and one slot / DNS dictionary on every ctx
+  size_t cap = c0->key_cap;
+  for (size_t i = 1; i < n; ++i) {
+    const gpuagg_ctx *ci = ctxs[i];
+    if (!ci || ci == c0) return fail(c0, GPUAGG_EINVAL, "merge: ctx %zu is null or the target", i);
+    bool same = ci->remote == c0->remote && ci->groups.size() == c0->groups.size() &&
+                ci->cms_len == c0->cms_len && ci->cfg.hll_precision == c0->cfg.hll_precision &&
+                (ci->sparse_slots != 0) == (c0->sparse_slots != 0) && ci->slots.size() == c0->slots.size() &&
+                ci->dns.size() == c0->dns.size();
+    for (size_t g = 0; same && g < c0->groups.size(); ++g)
+      same = ci->groups[g].family == c0->groups[g].family && ci->groups[g].sparse == c0->groups[g].sparse &&
+             ci->groups[g].src_opts == c0->groups[g].src_opts && ci->groups[g].dst_opts == c0->groups[g].dst_opts;
+    for (size_t k = 0; same && k < c0->slots.size(); ++k)
+      same = ci->slots[k].ns == c0->slots[k].ns && ci->slots[k].pod == c0->slots[k].pod &&
+             ci->slots[k].wk_kind == c0->slots[k].wk_kind && ci->slots[k].wk_name == c0->slots[k].wk_name &&
+             ci->slots[k].has_owner == c0->slots[k].has_owner && ci->slots[k].in_use == c0->slots[k].in_use;
+    for (size_t k = 0; same && k < c0->dns.size(); ++k)
+      same = ci->dns[k].rcode == c0->dns[k].rcode && ci->dns[k].nresp == c0->dns[k].nresp &&
+             ci->dns[k].qtypes == c0->dns[k].qtypes && ci->dns[k].query == c0->dns[k].query &&
+             ci->dns[k].ips == c0->dns[k].ips;
+    if (!same)
+      return fail(c0, GPUAGG_EINVAL, "merge: ctx %zu has another metric plan or slot/DNS dictionary", i);
+    cap = std::max<size_t>(cap, ci->key_cap);
+  }
+  // one layout everywhere (the largest slot coverage), then every stream idle
+  for (size_t i = 0; i < n; ++i) {
+    gpuagg_ctx *ci = ctxs[i];
+    if ((rc = bind(ci))) return rc;
+    if (ci->key_cap < cap && (rc = layout_dense(ci, (uint32_t)cap, true))) return rc;
+    HIPCHK(ci, hipStreamSynchronize(ci->stream));
+    HIPCHK(ci, hipStreamSynchronize(ci->copy_stream));
+  }
+  if ((rc = bind(c0))) return rc;
+  const size_t tmp_bytes = std::max({c0->dense_len * 8, c0->cms_len * 4, c0->hll_len, (size_t)8});
+  uint8_t *tmp = nullptr;
+  if ((rc = dev_alloc(c0, &tmp, tmp_bytes))) return rc;
+  uint64_t *ent = nullptr;
+  size_t ent_cap = 0;
+  auto cleanup = [&] {
+    dev_free(tmp);
+    dev_free(ent);
+  };
+  auto peer = [&](void *dst, const void *src, int src_dev, size_t bytes) {
+    return hipMemcpyPeerAsync(dst, c0->device, src, src_dev, bytes, c0->stream);
+  };
+  for (size_t i = 1; i < n; ++i) {
+    gpuagg_ctx *ci = ctxs[i];
+    hipError_t e = hipSuccess;
+    if (c0->dense_len) {
+      if ((e = peer(tmp, ci->d_dense_cnt, ci->device, c0->dense_len * 8)) == hipSuccess)
+        e = launch_merge_add_u64(c0->d_dense_cnt, (const uint64_t *)tmp, c0->dense_len, c0->stream);
+      if (e == hipSuccess && (e = peer(tmp, ci->d_dense_byt, ci->device, c0->dense_len * 8)) == hipSuccess)
+        e = launch_merge_add_u64(c0->d_dense_byt, (const uint64_t *)tmp, c0->dense_len, c0->stream);
+    }
+    if (e == hipSuccess && c0->cms_len && (e = peer(tmp, ci->d_cms, ci->device, c0->cms_len * 4)) == hipSuccess)
+      e = launch_merge_add_u32(c0->d_cms, (const uint32_t *)tmp, c0->cms_len, c0->stream);
+    if (e == hipSuccess && c0->hll_len && (e = peer(tmp, ci->d_hll, ci->device, c0->hll_len)) == hipSuccess)
+      e = launch_merge_max_u8(c0->d_hll, tmp, c0->hll_len, c0->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return fail(c0, GPUAGG_EDEVICE, "merge of ctx %zu: %s", i, hipGetErrorString(e));
+    }
+    if (ci->sparse_slots) {  // group-by entries: exported on ci, inserted-and-added on c0
+      if ((rc = bind(ci))) break;
+      if (ci->export_cap < ci->sparse_slots) {
+        dev_free(ci->d_export);
+        ci->export_cap = 0;
+        if ((rc = dev_alloc(ci, &ci->d_export, ci->sparse_slots * kSparseEntryWords))) break;
+        ci->export_cap = ci->sparse_slots;
+      }
+      size_t m = 0;
+      if ((rc = gpuagg_sparse_export(ci, ci->d_export, ci->export_cap, &m))) break;
+      if ((rc = bind(c0))) break;
+      if (m > ent_cap) {
+        dev_free(ent);
+        ent_cap = 0;
+        if ((rc = dev_alloc(c0, &ent, m * kSparseEntryWords))) break;
+        ent_cap = m;
+      }
+      if (m) {
+        if ((e = peer(ent, ci->d_export, ci->device, m * kSparseEntryWords * 8)) == hipSuccess)
+          e = hipStreamSynchronize(c0->stream);
+        if (e != hipSuccess) {
+          rc = fail(c0, GPUAGG_EDEVICE, "merge: %s", hipGetErrorString(e));
+          break;
+        }
+        if ((rc = gpuagg_sparse_import(c0, ent, m))) break;
+      }
+    }
+    if ((rc = gpuagg_reset(ci))) break;
+    if ((rc = bind(c0))) break;
+  }
+  cleanup();
+  if (rc) return rc;
+  HIPCHK(c0, hipStreamSynchronize(c0->stream));
   return GPUAGG_OK;
 }
 

@@ -165,21 +165,53 @@ class GpuAgg:
             self.h, ips.ctypes.data_as(_abi.u32p), slots.ctypes.data_as(C.POINTER(C.c_int32)),
             len(ips), version))
 
-    def load_endpoints(self, endpoints: Sequence[Endpoint], version: int = 0) -> Dict[int, int]:
-        """Interns every endpoint identity and installs the IP -> slot table.
-
-        Later endpoints win an IP held by an earlier one (cache.go:204-233)."""
-        ip_to_slot: Dict[int, int] = {}
+    def load_endpoints(self, endpoints: Sequence[Endpoint], version: int = 0) -> None:
+        """Cache.UpdateRetinaEndpoint for every endpoint in order, then installs the
+        cache's IP -> pod map (cache.go:196-233: a later endpoint that takes an IP of an
+        earlier one deletes that whole earlier endpoint)."""
         for ep in endpoints:
-            owner = ep.owner_refs[0] if ep.owner_refs else None
-            slot = self.slot_intern(ep.namespace, ep.name, owner[0] if owner else None,
-                                    owner[1] if owner else None)
-            for ip in ep.ips:
-                ip_to_slot[int(ip)] = slot
-        ips = np.fromiter(ip_to_slot.keys(), dtype=np.uint32, count=len(ip_to_slot))
-        sl = np.fromiter(ip_to_slot.values(), dtype=np.int32, count=len(ip_to_slot))
-        self.set_endpoints(ips, sl, version)
-        return ip_to_slot
+            self.cache_update_endpoint(ep)
+        self.cache_commit(version)
+
+    # -- the IP cache (cache.go), natively in the engine ---------------------------------
+    def cache_update_endpoint(self, ep: Endpoint) -> None:
+        owner = ep.owner_refs[0] if ep.owner_refs else None
+        ips = np.ascontiguousarray(np.asarray(list(ep.ips), dtype=np.uint32))
+        self._check(self.lib.gpuagg_cache_update_endpoint(
+            self.h, ep.namespace.encode(), ep.name.encode(),
+            None if owner is None else owner[0].encode(),
+            None if owner is None else (owner[1] or "").encode(),
+            ips.ctypes.data_as(_abi.u32p), len(ips)))
+
+    def cache_delete_endpoint(self, namespace: str, name: str) -> None:
+        self._check(self.lib.gpuagg_cache_delete_endpoint(self.h, namespace.encode(), name.encode()))
+
+    def cache_update_service(self, namespace: str, name: str, ip: int) -> None:
+        self._check(self.lib.gpuagg_cache_update_service(self.h, namespace.encode(), name.encode(), ip))
+
+    def cache_delete_service(self, namespace: str, name: str) -> None:
+        self._check(self.lib.gpuagg_cache_delete_service(self.h, namespace.encode(), name.encode()))
+
+    def cache_update_node(self, name: str, ip: int) -> None:
+        self._check(self.lib.gpuagg_cache_update_node(self.h, name.encode(), ip))
+
+    def cache_delete_node(self, name: str) -> None:
+        self._check(self.lib.gpuagg_cache_delete_node(self.h, name.encode()))
+
+    def cache_commit(self, version: int = 0) -> None:
+        self._check(self.lib.gpuagg_cache_commit(self.h, version))
+
+    def retire_slots(self) -> int:
+        """Frees the slots the installed IP table no longer references (epoch boundary)."""
+        n = C.c_size_t()
+        self._check(self.lib.gpuagg_retire_slots(self.h, C.byref(n)))
+        return n.value
+
+    def merge_from(self, others: Sequence["GpuAgg"]) -> None:
+        """gpuagg_merge: fold the state of `others` (any devices) into this engine and
+        reset them -- the single-process multi-GPU epoch merge."""
+        arr = (C.c_void_p * (1 + len(others)))(self.h, *[o.h for o in others])
+        self._check(self.lib.gpuagg_merge(arr, len(arr)))
 
     def dns_intern(self, rcode: int, qtypes: Sequence[str], query: str, ips: Sequence[str],
                    num_answers: int) -> int:
@@ -256,11 +288,41 @@ class GpuAgg:
         self._check(self.lib.gpuagg_reset(self.h))
 
     # -- output ------------------------------------------------------------------------
+    def snapshot_text(self) -> str:
+        """The snapshot in the Prometheus text exposition format (gpuagg_result_render_text)."""
+        r = C.c_void_p()
+        self._check(self.lib.gpuagg_snapshot(self.h, C.byref(r)))
+        try:
+            n = C.c_size_t()
+            self._check(self.lib.gpuagg_result_render_text(r, None, 0, C.byref(n)))
+            buf = C.create_string_buffer(n.value + 1)
+            self._check(self.lib.gpuagg_result_render_text(r, buf, n.value + 1, C.byref(n)))
+            return buf.value.decode()
+        finally:
+            self.lib.gpuagg_result_free(r)
+
+    def snapshot_families(self) -> Dict[str, Tuple[str, str]]:
+        """{metric: (prometheus type, help)} of the snapshot's series."""
+        r = C.c_void_p()
+        self._check(self.lib.gpuagg_snapshot(self.h, C.byref(r)))
+        out = {}
+        try:
+            metric, t, h = C.c_char_p(), C.c_char_p(), C.c_char_p()
+            for i in range(self.lib.gpuagg_result_count(r)):
+                self._check(self.lib.gpuagg_result_series(r, i, C.byref(metric), None, None, None, None))
+                self._check(self.lib.gpuagg_result_family(r, i, C.byref(t), C.byref(h)))
+                out[metric.value.decode()] = (t.value.decode(), h.value.decode())
+        finally:
+            self.lib.gpuagg_result_free(r)
+        return out
+
     def snapshot(self) -> Dict[SeriesKey, int]:
         r = C.c_void_p()
         self._check(self.lib.gpuagg_snapshot(self.h, C.byref(r)))
         out: Dict[SeriesKey, int] = {}
+        self.last_dropped = 0
         try:
+            self.last_dropped = int(self.lib.gpuagg_result_dropped(r))
             n = self.lib.gpuagg_result_count(r)
             metric = C.c_char_p()
             nl = C.c_uint32()
@@ -297,10 +359,11 @@ class GpuAgg:
         return a.reshape(self.cfg.cms_depth, -1) if a.size else a
 
     def hll_array(self) -> np.ndarray:
+        """HLL registers [slots covered, 2^p] (rows grow with the slots in use)."""
         d = self.state()
         a = np.zeros(d.hll_len, np.uint8)
         self._check(self.lib.gpuagg_hll_copy(self.h, a.ctypes.data_as(C.POINTER(C.c_uint8)), a.size))
-        return a.reshape(self.cfg.max_slots, -1) if a.size else a
+        return a.reshape(-1, 1 << self.cfg.hll_precision) if a.size else a
 
     # -- merge / introspection -----------------------------------------------------------
     def state(self) -> "_abi.StateDesc":

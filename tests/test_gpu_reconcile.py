@@ -70,7 +70,10 @@ def test_reconcile_resets_counters(gpu_device, data):
     g = make_engine(pods, sp, False, gpu_device, recs)
     g.submit_numpy(recs)
     assert g.snapshot()
-    g.reconcile(sp)
+    g.reconcile(sp)  # equal options: Module.Reconcile does nothing (metrics_module.go:142-166)
+    assert g.snapshot()
+    g.reconcile(sp[:2])  # a change re-creates the metrics ...
+    g.reconcile(sp)      # ... and so does changing back
     assert g.snapshot() == {}
     g.submit_numpy(recs)
     assert g.snapshot() == oracle_series(recs, pods, sp, False)
