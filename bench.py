@@ -36,7 +36,7 @@ METRIC = "flow records/sec aggregated (node, 1/2/4/8 GPU); % of HBM peak GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Algorithmic bytes per record: the columns the enabled metrics read.
 # C5's metrics (tcpflags, retransmits, DNS) count records only: src, dst, meta, dns_id.
-BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c5": 16}
+BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c4-src": 16, "c5": 16}
 # the sketch pass reads src, dst, ports, meta (proto)
 SKETCH_BYTES_PER_RECORD = 16
 
@@ -51,7 +51,9 @@ def bench_spec(name: str):
         return W.LOCAL_FWD_DROP, dict(cms_depth=4, cms_width_log2=20, hll_precision=14), (
             "C3: " + c2txt + " + count-min d=4 w=2^20 over the 5-tuple + HLL p=14 distinct dst per source pod")
     if name == "c4":
-        return W.LOCAL_FWD_DROP, {}, "C4: Zipf(1.2) source pods, " + c2txt
+        return W.LOCAL_FWD_DROP, {}, "C4: Zipf(1.2) 5-tuple ranks over 10^7 flows, " + c2txt
+    if name == "c4-src":
+        return W.LOCAL_FWD_DROP, {}, "C4 (round-1 form): Zipf(1.2) source pods, " + c2txt
     if name == "c5":
         return W.C5_SPEC, {}, "C5: tcpflags + tcp retransmission + DNS request/response, local context [namespace, podname]"
     return W.LOCAL_FWD_DROP, {}, "C2: " + c2txt

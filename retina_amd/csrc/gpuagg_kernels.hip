@@ -73,6 +73,7 @@ struct KArgs {
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
+  unsigned long long *l4_ovf;  // tier-1: [2 * lds_bins] exact-correction pairs
   Plan p;
 };
 
@@ -548,25 +549,29 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   dense_flush(a, ds);
 }
 
-// ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
-// Probe of the LDS cuckoo image: two 8-byte bucket reads and 4 compares give the index
-// of the matching key (or ~0u); the u16 slot id is read separately so all key reads of
-// a thread's records can be in flight together.
+// ---- tier-1: IP keys and 32-bit bins in LDS, bins indexed by IP-table position -------
+// LDS holds only the KEYS of the bucketized-cuckoo IP image (u32[2nb]); a probe yields
+// the position j of the matching key, or P = 2nb (not a pod, or the apiserver pseudo
+// pod, which local context treats alike, types.go:407-413).  Endpoint-keyed groups whose
+// bins fit LDS count per (position, side, sub) instead of (slot, side, sub), so no probe
+// reads a slot id.  stage_reduce_a_kernel maps positions to slots through the image's
+// u16 value array in HBM when it folds the workgroups' copies: a pod's secondary IPs are
+// other positions that add into the same slot bins there.  Groups whose bins do not fit
+// (C2: the 10 % drops into 10k x 2 x 8 bins) stay slot-keyed in HBM: their records are
+// queued in a per-wave LDS ring and spilled 64 at a time, reading their slots from the
+// value array once per queued record.
 __device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32_t nb, uint32_t seed,
                                                     uint32_t ip) {
   uint32_t b1, b2;
   ipl_buckets(ip, seed, nb, b1, b2);
   const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
-  uint32_t j = nb * 2;  // sentinel entry: kIplNoSlot
+  uint32_t j = nb * 2;  // P: not found
   j = k1.x == ip ? b1 * 2 : j;
   j = k1.y == ip ? b1 * 2 + 1 : j;
   j = k2.x == ip ? b2 * 2 : j;
   j = k2.y == ip ? b2 * 2 + 1 : j;
   return j;
 }
-
-// slot id, or kIplNoSlot (not a pod, or the apiserver pseudo pod)
-__device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
 
 struct L4Ctx {
   uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
@@ -579,37 +584,78 @@ struct L4Ctx {
     return valid & (((old & kL4BytesMask) + b > kL4BytesMask) | (old >= 0xFFE00000u) |
                     (nb >= kL4ByteLimit));
   }
-  // Exact correction after a packed add (count:12 | bytes:20) returned `old`: a carry
-  // out of the bytes field, a wrap of the count field, or a packet too big for the
-  // field is booked into the global counters.  Rare; the test is 3 VALU ops.
-  __device__ __forceinline__ void fix(bool valid, uint32_t old, uint32_t nb, uint32_t bin) const {
+  // Exact correction after a packed add (count:12 | bytes:20) into LDS bin `lbin` returned
+  // `old`: a carry out of the bytes field, a wrap of the count field, or a packet too big
+  // for the field.  The difference goes into a per-bin overflow pair in HBM (`ovf`,
+  // indexed like the LDS bins, folded by stage_reduce_a_kernel) -- LDS bins are keyed
+  // by position, so the slot-keyed dense counters cannot take it here.  Rare; the test
+  // is 3 VALU ops.
+  unsigned long long *ovf;  // [2 * L4]: count, bytes per LDS bin
+  __device__ __forceinline__ void fix(bool valid, uint32_t old, uint32_t nb, uint32_t lbin) const {
     const uint32_t b = nb < kL4ByteLimit ? nb : 0u;
-    if (!(valid && ((old & kL4BytesMask) + b > kL4BytesMask || old >= 0xFFE00000u ||
-                    nb >= kL4ByteLimit)))
+    if (!(valid && ((old & kL4BytesMask) + b > kL4BytesMask || old >= 0xFFE00000u || nb >= kL4ByteLimit)))
       return;
-    if (nb >= kL4ByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
+    unsigned long long *o = ovf + 2ull * lbin;
+    if (nb >= kL4ByteLimit) atomicAdd(&o[1], (unsigned long long)nb);
     const uint32_t carry = ((old & kL4BytesMask) + b) >> kL4CountShift;
     const uint32_t wrap = ((old >> kL4CountShift) + 1u + carry) >> (32 - kL4CountShift);
     if (carry) {
-      atomicAdd(&d.byt[bin], (unsigned long long)kL4ByteLimit);
-      atomicAdd(&d.cnt[bin], ~0ULL);  // the carry also bumped the count field
+      atomicAdd(&o[1], (unsigned long long)kL4ByteLimit);
+      atomicAdd(&o[0], ~0ULL);  // the carry also bumped the count field
     }
-    if (wrap) atomicAdd(&d.cnt[bin], 1ULL << (32 - kL4CountShift));
+    if (wrap) atomicAdd(&o[0], 1ULL << (32 - kL4CountShift));
   }
 };
 static_assert(kL4CountShift == 20, "fix() thresholds assume count:12 | bytes:20");
 
+// A record's fields as the tier-1 group updates read them.
+struct Rec {
+  uint32_t nbytes, verdict, reason, flagmask;
+};
+__device__ __forceinline__ Rec rec_of(uint32_t nbytes, uint32_t meta, bool any_flags) {
+  Rec r;
+  r.nbytes = nbytes;
+  r.verdict = meta_verdict(meta);
+  r.reason = meta_reason(meta);
+  r.flagmask = (any_flags && r.verdict == kVerdictForwarded && meta_proto(meta) == 6)
+                   ? flag_label_mask(meta_flags(meta)) : 0u;
+  return r;
+}
+// Ring entry word 1: bytes:20 | verdict class:2 | reason:3 | flag mask:7 (records whose
+// bytes do not fit take the direct path).
+constexpr uint32_t kRingByteLimit = 1u << 20;
+__device__ __forceinline__ uint32_t rec_pack(const Rec &r) {
+  const uint32_t cls = r.verdict == kVerdictForwarded ? 1u : r.verdict == kVerdictDropped ? 2u
+                       : r.verdict == kVerdictRetrans ? 3u : 0u;
+  return (r.nbytes & (kRingByteLimit - 1)) | (cls << 20) | (r.reason << 22) | (r.flagmask << 25);
+}
+__device__ __forceinline__ Rec rec_unpack(uint32_t w) {
+  const uint32_t cls = (w >> 20) & 3u;
+  Rec r;
+  r.nbytes = w & (kRingByteLimit - 1);
+  r.verdict = cls == 1u ? kVerdictForwarded : cls == 2u ? kVerdictDropped : cls == 3u ? kVerdictRetrans : 0u;
+  r.reason = (w >> 22) & 7u;
+  r.flagmask = w >> 25;
+  return r;
+}
+
+// Does a record update group f (tier-1 families only: fwd / drop / tcpflags / retrans)?
+__device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t flagmask) {
+  if (f == FAM_TCPFLAGS) return flagmask != 0;
+  return verdict == (f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans);
+}
+
 // Group descriptors of the dense local-context plan, compile-time indexed (SGPRs).
 // SIG != 0 also fixes every group's family and LDS residency at compile time (4 bits per
-// group: family + 1, bit 3 = in LDS; see tier1_signature), so the per-record family
-// dispatch folds away; SIG == 0 reads them from the plan.
+// group: family + 1, bit 3 = in LDS; see sig_group), so the per-record family dispatch
+// folds away; SIG == 0 reads them from the plan.
 template <int NG, uint32_t SIG>
 struct DenseGroups {
-  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  uint32_t fam[NG], base[NG], lbase[NG], nsub[NG], keyed[NG];
   bool inl[NG];
   bool any_flags;
   bool any_spilled;  // some group's bins are outside LDS
-  __device__ __forceinline__ DenseGroups(const Plan &p, uint32_t L) {
+  __device__ __forceinline__ DenseGroups(const Plan &p) {
     any_flags = false;
     any_spilled = false;
 #pragma unroll
@@ -620,91 +666,55 @@ struct DenseGroups {
         inl[g] = (SIG >> (4 * g + 3)) & 1u;
       } else {
         fam[g] = g < p.ngroups ? p.g[g].family : (uint32_t)FAM_COUNT;
-        inl[g] = p.g[g].dense_base + p.g[g].nbins <= L;
+        inl[g] = p.g[g].lds_nbins != 0;
       }
       base[g] = (uint32_t)p.g[g].dense_base;
+      lbase[g] = p.g[g].lds_base;
       nsub[g] = p.g[g].nsub;
       keyed[g] = p.g[g].key_mode;
       any_flags |= fam[g] == FAM_TCPFLAGS;
       any_spilled |= fam[g] != FAM_COUNT && !inl[g];
     }
   }
-};
-
-// Does a record update group f (tier-1 families only: fwd / drop / tcpflags / retrans)?
-__device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t flagmask) {
-  if (f == FAM_TCPFLAGS) return flagmask != 0;
-  return verdict == (f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans);
-}
-
-// Wave-level compaction queue for the records that update a spilled group (one whose
-// bins are not in LDS).  Such records are rare (C2: the 10 % drops), so updating them
-// in place would issue every spill instruction for ~5 active lanes of 64.  Instead each
-// step pushes them into three queue registers (one entry per lane) with ds_permute --
-// LDS crossbar, no LDS memory -- and the spill code runs once per 64 queued records
-// with every lane busy.  Push = ballot + mbcnt + a bijective lane permutation: hits go
-// to queue positions [n, n + hits), misses to the remaining ones, so every lane
-// receives exactly one value.
-struct SpillQ {
-  uint32_t e0, e1, e2;  // queued entries: slots (ss | sd << 16), bytes, meta
-  uint32_t n;           // queued entries (wave-uniform), lanes [0, n)
-  uint32_t r0, r1, r2;  // this push's permuted values (wrap-around part on overflow)
-  // push; returns true when the queue holds 64 entries (caller flushes, then next())
-  __device__ __forceinline__ bool push(bool v, uint32_t lane, uint32_t a0, uint32_t a1, uint32_t a2) {
-    const uint64_t m = __ballot(v);
-    const uint32_t cnt = (uint32_t)__popcll(m);
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    const uint32_t pos = v ? n + below : n + cnt + (lane - below);
-    const int addr = (int)((pos & 63u) << 2);
-    r0 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a0);
-    r1 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a1);
-    r2 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a2);
-    const bool got = lane >= n && lane < n + cnt;
-    e0 = got ? r0 : e0;
-    e1 = got ? r1 : e1;
-    e2 = got ? r2 : e2;
-    n += cnt;
-    return n >= 64;
-  }
-  // after flushing a full queue: the wrapped entries become the queue
-  __device__ __forceinline__ void next() { e0 = r0; e1 = r1; e2 = r2; n -= 64; }
-};
-
-// R records of one thread through every group (tier-1).  Group-outer / record-inner:
-// a group's 2R returning LDS adds are all issued before any result is inspected, so
-// their latency overlaps.  ss/sd: source / destination slot or kIplNoSlot.
-// kMode: 0 every group; 1 LDS groups only (spilled ones go through SpillQ); 2 spilled
-// groups only (the SpillQ flush).
-template <int NG, uint32_t SIG, int R, int kMode = 0>
-__device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const L4Ctx &l4,
-                                           const DenseSink &ds, const uint32_t (&nbytes)[R],
-                                           const uint32_t (&meta)[R], const uint32_t (&ss)[R],
-                                           const uint32_t (&sd)[R]) {
-  uint32_t verdict[R], reason[R], flagmask[R];
+  // does record r update some spilled group?
+  __device__ __forceinline__ bool hits_spilled(const Rec &r) const {
+    bool h = false;
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    verdict[k] = meta_verdict(meta[k]);
-    reason[k] = meta_reason(meta[k]);
-    flagmask[k] = (G.any_flags && verdict[k] == kVerdictForwarded && meta_proto(meta[k]) == 6)
-                      ? flag_label_mask(meta_flags(meta[k])) : 0u;
+    for (int g = 0; g < NG; ++g)
+      if (fam[g] != FAM_COUNT && !inl[g]) h |= fam_hit(fam[g], r.verdict, r.flagmask);
+    return h;
   }
+};
+
+// R records of one thread through the groups (tier-1).  Group-outer / record-inner: a
+// group's 2R returning LDS adds are all issued before any result is inspected, so their
+// latency overlaps.  ks / kd: source / destination key, `none` when the side is no pod.
+// kMode 0: every group, keys are IP positions (only when no group is spilled)
+//       1: LDS groups only, keys are IP positions
+//       2: spilled groups only, keys are slots, whole wave converged (ring flush)
+//       3: spilled groups only, keys are slots, any lanes (per-lane reservation)
+template <int NG, uint32_t SIG, int R, int kMode>
+__device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const L4Ctx &l4,
+                                           const DenseSink &ds, const Rec (&rec)[R],
+                                           const uint32_t (&ks)[R], const uint32_t (&kd)[R], uint32_t none) {
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const uint32_t f = G.fam[g];
     if (f == FAM_COUNT) continue;
-    if ((kMode == 1 && !G.inl[g]) || (kMode == 2 && G.inl[g])) continue;
+    if ((kMode == 1 && !G.inl[g]) || (kMode >= 2 && G.inl[g])) continue;
+    const uint32_t b0 = G.inl[g] ? G.lbase[g] : G.base[g];
     uint32_t rd[R], rs[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {  // slots < 2^16, nsub <= 64: 24-bit multiplies
-      const uint32_t kd = G.keyed[g] ? sd[k] : 0u, ks = G.keyed[g] ? ss[k] : 0u;
-      rd[k] = G.base[g] + mul_u24(kd * 2u, G.nsub[g]);       // side 0: ingress (dst)
-      rs[k] = G.base[g] + mul_u24(ks * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
+    for (int k = 0; k < R; ++k) {  // keys < 2^16, nsub <= 64: 24-bit multiplies
+      const uint32_t xd = G.keyed[g] ? kd[k] : 0u, xs = G.keyed[g] ? ks[k] : 0u;
+      rd[k] = b0 + mul_u24(xd * 2u, G.nsub[g]);       // side 0: ingress (dst)
+      rs[k] = b0 + mul_u24(xs * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
     }
     if (f == FAM_TCPFLAGS) {
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        uint32_t m = flagmask[k];
-        const bool d_ok = sd[k] != kIplNoSlot, s_ok = ss[k] != kIplNoSlot;
+        uint32_t m = rec[k].flagmask;
+        const bool d_ok = kd[k] != none, s_ok = ks[k] != none;
         if (G.inl[g]) {
           while (__ballot(m != 0)) {
             const bool v = m != 0;
@@ -723,16 +733,15 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       }
       continue;
     }
-    const uint32_t want = f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped
-                                                                          : kVerdictRetrans;
+    const uint32_t want = f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans;
     bool vd[R], vs[R];
     uint32_t bd[R], bs[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      const bool hit = verdict[k] == want;
-      const uint32_t sub = f == FAM_DROP ? reason[k] : 0u;
-      vd[k] = hit & (sd[k] != kIplNoSlot);  // '&': no short-circuit branches
-      vs[k] = hit & (ss[k] != kIplNoSlot);
+      const bool hit = rec[k].verdict == want;
+      const uint32_t sub = f == FAM_DROP ? rec[k].reason : 0u;
+      vd[k] = hit & (kd[k] != none);  // '&': no short-circuit branches
+      vs[k] = hit & (ks[k] != none);
       bd[k] = rd[k] + sub;
       bs[k] = rs[k] + sub;
     }
@@ -741,19 +750,22 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
         uint32_t od[R], os[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-          const uint32_t add = (1u << kL4CountShift) | (nbytes[k] < kL4ByteLimit ? nbytes[k] : 0u);
+          const uint32_t add = (1u << kL4CountShift) | (rec[k].nbytes < kL4ByteLimit ? rec[k].nbytes : 0u);
           od[k] = atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], add);
           os[k] = atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], add);
         }
         bool need = false;
 #pragma unroll
         for (int k = 0; k < R; ++k)
-          need |= L4Ctx::fix_needed(vd[k], od[k], nbytes[k]) | L4Ctx::fix_needed(vs[k], os[k], nbytes[k]);
+        {
+          need |= L4Ctx::fix_needed(vd[k], od[k], rec[k].nbytes);
+          need |= L4Ctx::fix_needed(vs[k], os[k], rec[k].nbytes);
+        }
         if (__builtin_expect(__ballot(need) != 0, 0)) {  // rare: a carry, a wrap or a jumbo size
 #pragma unroll
           for (int k = 0; k < R; ++k) {
-            l4.fix(vd[k], od[k], nbytes[k], bd[k]);
-            l4.fix(vs[k], os[k], nbytes[k], bs[k]);
+            l4.fix(vd[k], od[k], rec[k].nbytes, bd[k]);
+            l4.fix(vs[k], os[k], rec[k].nbytes, bs[k]);
           }
         }
       } else {
@@ -771,7 +783,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       for (int k = 0; k < R; ++k) {
         wd[k] = ds.window(bd[k]);
         ws[k] = ds.window(bs[k]);
-        if (kMode == 2) {  // SpillQ flush: converged wave
+        if (kMode == 2) {  // ring flush: converged wave
           pd[k] = wave_reserve(vd[k], wd[k], ds.ctr, ds.wbits);
           ps[k] = wave_reserve(vs[k], ws[k], ds.ctr, ds.wbits);
         } else {
@@ -781,14 +793,14 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
+        const uint32_t add_b = f <= FAM_DROP ? rec[k].nbytes : 0u;
         if (vd[k]) ds.spill_put(bd[k], wd[k], pd[k], add_b);
         if (vs[k]) ds.spill_put(bs[k], ws[k], ps[k], add_b);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
+        const uint32_t add_b = f <= FAM_DROP ? rec[k].nbytes : 0u;
         if (vd[k]) ds.spill_add(bd[k], add_b);
         if (vs[k]) ds.spill_add(bs[k], add_b);
       }
@@ -796,31 +808,39 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
   }
 }
 
+constexpr uint32_t kRing = 128;  // ring entries per wave (uint2: positions, packed record)
+
 template <int NG, bool kVec, uint32_t SIG>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t nb = a.ipl_nb;
+  const uint32_t nb = a.ipl_nb, P = 2u * nb;
   const uint32_t *keys = (const uint32_t *)smem;
-  const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
-  uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
-  const uint32_t L4 = a.lds_bins;
-  for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
-    ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
+  const uint32_t kbytes = ipl_vals_offset(nb);  // the key array, 16-byte padded
+  const uint16_t *gvals = (const uint16_t *)(a.ipl + kbytes);  // HBM: position -> slot
+  uint32_t *bins = (uint32_t *)(smem + kbytes);
+  const uint32_t L4 = a.lds_bins;  // even (host)
+  unsigned int *ctr = bins + L4 + 64;
+  for (uint32_t i = threadIdx.x; i < kbytes / 16; i += blockDim.x) ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
   for (uint32_t i = threadIdx.x; i < L4 + 64 + kMaxSpillWindows; i += blockDim.x) bins[i] = 0u;
   __syncthreads();
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const L4Ctx l4{bins, L4 + lane, a.d};
-  const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
-  const DenseGroups<NG, SIG> G(a.p, L4);
+  const L4Ctx l4{bins, L4 + lane, a.d, a.l4_ovf};
+  const DenseSink ds = make_sink(a, nullptr, 0, ctr);
+  const DenseGroups<NG, SIG> G(a.p);
   const uint32_t seed = a.ipl_seed;
-  SpillQ q{};
-  // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
-  auto q_flush = [&](bool full) {
-    const bool valid = full || lane < q.n;
-    const uint32_t s1[1] = {valid ? (q.e0 & 0xFFFFu) : kIplNoSlot};
-    const uint32_t d1[1] = {valid ? (q.e0 >> 16) : kIplNoSlot};
-    const uint32_t b1[1] = {q.e1}, m1[1] = {q.e2};
-    l4_records<NG, SIG, 1, 2>(G, l4, ds, b1, m1, s1, d1);
+  uint2 *ring = (uint2 *)(ctr + kMaxSpillWindows) + (threadIdx.x >> 6) * kRing;
+  uint32_t head = 0, nq = 0;  // wave-uniform ring state
+  // spill updates of `cnt` queued records from the ring head (lanes >= cnt hold none)
+  auto ring_flush = [&](uint32_t cnt) {
+    const uint2 e = ring[(head + lane) & (kRing - 1)];
+    const bool valid = lane < cnt;
+    const uint32_t ps = e.x & 0xFFFFu, pd = e.x >> 16;
+    const uint32_t ss[1] = {valid && ps != P ? (uint32_t)gvals[ps] : kIplNoSlot};
+    const uint32_t sd[1] = {valid && pd != P ? (uint32_t)gvals[pd] : kIplNoSlot};
+    const Rec r1[1] = {rec_unpack(e.y)};
+    l4_records<NG, SIG, 1, 2>(G, l4, ds, r1, ss, sd, kIplNoSlot);
+    head = (head + cnt) & (kRing - 1);
+    nq -= cnt;
   };
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -831,8 +851,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t v0 = start >> 2, vn = (end - start) >> 2, vend = v0 + vn;
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
-    // the loop is wave-uniform (SpillQ's cross-lane pushes need every lane present):
-    // lanes past the end load a clamped vector and update nothing
+    // the loop is wave-uniform (the ring's ballots need every lane present): lanes past
+    // the end load a clamped vector and update nothing
     const uint64_t vwave = v0 + (threadIdx.x & ~63u);
     const uint64_t vlast = vend - 1;  // vn >= 1
     uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
@@ -848,78 +868,75 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t j[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
-      uint32_t sl[8];
+      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);  // every lane: no branch
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
-      const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
-      const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
+      for (int k = 0; k < 8; ++k) j[k] = act ? j[k] : P;
+      const uint32_t js[4] = {j[0], j[1], j[2], j[3]}, jd[4] = {j[4], j[5], j[6], j[7]};
+      const Rec rec[4] = {rec_of(vb.x, vm.x, G.any_flags), rec_of(vb.y, vm.y, G.any_flags),
+                          rec_of(vb.z, vm.z, G.any_flags), rec_of(vb.w, vm.w, G.any_flags)};
       if (!G.any_spilled) {
-        l4_records<NG, SIG, 4, 0>(G, l4, ds, by, me, ss, sd);
+        l4_records<NG, SIG, 4, 0>(G, l4, ds, rec, js, jd, P);
         continue;
       }
-      l4_records<NG, SIG, 4, 1>(G, l4, ds, by, me, ss, sd);
-      // records that update a spilled group -> SpillQ (rolled: one copy of the flush)
-      uint32_t x0 = ss[0] | sd[0] << 16, x1 = ss[1] | sd[1] << 16, x2 = ss[2] | sd[2] << 16,
-               x3 = ss[3] | sd[3] << 16;
-      uint32_t y0 = by[0], y1 = by[1], y2 = by[2], y3 = by[3];
-      uint32_t z0 = me[0], z1 = me[1], z2 = me[2], z3 = me[3];
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t ver = meta_verdict(z0);
-        const uint32_t fm = (G.any_flags && ver == kVerdictForwarded && meta_proto(z0) == 6)
-                                ? flag_label_mask(meta_flags(z0)) : 0u;
-        bool need = false;
+      l4_records<NG, SIG, 4, 1>(G, l4, ds, rec, js, jd, P);
+      // records that update a spilled group -> this wave's LDS ring
+      uint64_t bal[4];
+      uint32_t T = 0;
+      bool big = false;
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
-          if (G.fam[g] != FAM_COUNT && !G.inl[g]) need |= fam_hit(G.fam[g], ver, fm);
-        need = need & (x0 != 0xFFFFFFFFu);  // some side is a pod
-        if (q.push(need, lane, x0, y0, z0)) {
-          q_flush(true);
-          q.next();
-        }
-        x0 = x1; x1 = x2; x2 = x3;
-        y0 = y1; y1 = y2; y2 = y3;
-        z0 = z1; z1 = z2; z2 = z3;
+      for (int k = 0; k < 4; ++k) {
+        const bool need = G.hits_spilled(rec[k]) & ((js[k] != P) | (jd[k] != P));
+        bal[k] = __ballot(need);
+        T += (uint32_t)__popcll(bal[k]);
+        big |= need & (rec[k].nbytes >= kRingByteLimit);
       }
+      if (__builtin_expect(__ballot(big) != 0 || nq + T > kRing, 0)) {
+        // rare: a packet too big for the ring word, or a step that would overflow the
+        // ring: these 4 records' spilled updates directly, slots read from HBM
+        uint32_t ss[4], sd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool need = (bal[k] >> lane) & 1u;
+          ss[k] = need && js[k] != P ? (uint32_t)gvals[js[k]] : kIplNoSlot;
+          sd[k] = need && jd[k] != P ? (uint32_t)gvals[jd[k]] : kIplNoSlot;
+        }
+        l4_records<NG, SIG, 4, 2>(G, l4, ds, rec, ss, sd, kIplNoSlot);
+        continue;
+      }
+      uint32_t pos = head + nq;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
+        if ((bal[k] >> lane) & 1u) ring[(pos + rank) & (kRing - 1)] = make_uint2(js[k] | (jd[k] << 16), rec_pack(rec[k]));
+        pos += (uint32_t)__popcll(bal[k]);
+      }
+      nq += T;
+      while (nq >= 64) ring_flush(64);
     }
     tail = start + (vn << 2);
   }
-  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
-    const uint32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
-    const uint32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
-    const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
-    l4_records<NG, SIG, 1>(G, l4, ds, by, me, ss, sd);
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {  // < 4 records per workgroup
+    const uint32_t js[1] = {ipl_probe_index(keys, nb, seed, a.c.src[i])};
+    const uint32_t jd[1] = {ipl_probe_index(keys, nb, seed, a.c.dst[i])};
+    const Rec rec[1] = {rec_of(a.c.bytes[i], a.c.meta[i], G.any_flags)};
+    if (!G.any_spilled) {
+      l4_records<NG, SIG, 1, 0>(G, l4, ds, rec, js, jd, P);
+      continue;
+    }
+    l4_records<NG, SIG, 1, 1>(G, l4, ds, rec, js, jd, P);
+    const uint32_t ss[1] = {js[0] != P ? (uint32_t)gvals[js[0]] : kIplNoSlot};
+    const uint32_t sd[1] = {jd[0] != P ? (uint32_t)gvals[jd[0]] : kIplNoSlot};
+    l4_records<NG, SIG, 1, 3>(G, l4, ds, rec, ss, sd, kIplNoSlot);
   }
-  if (G.any_spilled && q.n) q_flush(false);
+  if (G.any_spilled && nq) ring_flush(nq);  // wave-uniform
 
   __syncthreads();
-  if (a.stage_a) {
-    // staged flush: plain 16-byte stores of this workgroup's bins; stage_reduce_kernel
-    // sums the copies (a global atomic per bin per workgroup costs more)
-    uint4 *dst = (uint4 *)(a.stage_a + (size_t)blockIdx.x * a.stage_a_stride);
-    for (uint32_t i = threadIdx.x; i < a.stage_a_stride / 4; i += blockDim.x) dst[i] = ((const uint4 *)bins)[i];
-  } else {
-    // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (G.fam[g] == FAM_COUNT || !G.inl[g]) continue;
-      const bool with_bytes = G.fam[g] <= FAM_DROP;
-      const uint32_t hi = G.base[g] + a.p.g[g].nbins;
-      for (uint32_t i = G.base[g] + threadIdx.x; i < hi; i += blockDim.x) {
-        const uint32_t w = bins[i];
-        if (!w) continue;
-        if (with_bytes) {
-          atomicAdd(&a.d.cnt[i], (unsigned long long)(w >> kL4CountShift));
-          const uint32_t by = w & kL4BytesMask;
-          if (by) atomicAdd(&a.d.byt[i], (unsigned long long)by);
-        } else {
-          atomicAdd(&a.d.cnt[i], (unsigned long long)w);
-        }
-      }
-    }
-  }
-  spill_counts_out(a, bins + L4 + 64);
+  // staged flush: plain 16-byte stores of this workgroup's bins; stage_reduce_a_kernel
+  // maps positions to slots and sums the copies
+  uint4 *dst = (uint4 *)(a.stage_a + (size_t)blockIdx.x * a.stage_a_stride);
+  for (uint32_t i = threadIdx.x; i < a.stage_a_stride / 4; i += blockDim.x) dst[i] = ((const uint4 *)bins)[i];
+  spill_counts_out(a, ctr);
 }
 
 // ---- sketch pass (config C3): count-min by window partition, HLL direct -------------
@@ -1138,17 +1155,29 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
 }
 
-// Sums the tier-1 workgroups' staged u32 bins: blockIdx.y takes 1/gridDim.y of the
-// copies, so each bin gets gridDim.y global atomics instead of one per workgroup.
+// Folds the tier-1 workgroups' staged u32 bins (keyed by IP position) into the slot-keyed
+// dense counters: bin -> (group, position, side, sub) -> slot through the image's value
+// array.  blockIdx.y takes 1/gridDim.y of the copies, so each bin gets gridDim.y global
+// atomics instead of one per workgroup; y == 0 also takes the bin's overflow pair.
 __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *stage, uint32_t ncopies,
                                                              uint32_t stride, uint32_t L4, Plan p,
-                                                             DevDense d) {
+                                                             DevDense d, const uint16_t *gvals,
+                                                             unsigned long long *ovf) {
   const uint32_t bin = blockIdx.x * blockDim.x + threadIdx.x;
   if (bin >= L4) return;
-  bool packed = false;
+  int gi = -1;
   for (int g = 0; g < p.ngroups; ++g)
-    if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
-      packed = p.g[g].family <= FAM_DROP;
+    if (p.g[g].lds_nbins && bin >= p.g[g].lds_base && bin < p.g[g].lds_base + p.g[g].lds_nbins) gi = g;
+  if (gi < 0) return;  // padding
+  const GroupPlan gp = p.g[gi];
+  const uint32_t local = bin - gp.lds_base, per = 2u * gp.nsub;  // per = 2 or 16
+  uint64_t target = gp.dense_base + local;
+  if (gp.key_mode) {
+    const uint32_t slot = gvals[local >> (31 - __builtin_clz(per))];
+    if (slot == kIplNoSlot) return;  // an empty image position: never updated
+    target = gp.dense_base + (uint64_t)slot * per + (local & (per - 1u));
+  }
+  const bool packed = gp.family <= FAM_DROP;
   const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * blockIdx.y) / gridDim.y);
   const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (blockIdx.y + 1)) / gridDim.y);
   unsigned long long cnt = 0, byt = 0;
@@ -1158,8 +1187,14 @@ __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *sta
     cnt += packed ? (w >> kL4CountShift) : w;
     byt += packed ? (w & kL4BytesMask) : 0u;
   }
-  if (cnt) atomicAdd(&d.cnt[bin], cnt);
-  if (byt) atomicAdd(&d.byt[bin], byt);
+  if (blockIdx.y == 0 && ovf) {  // exact corrections of the packed adds (L4Ctx::fix)
+    cnt += ovf[2ull * bin];
+    byt += ovf[2ull * bin + 1];
+    ovf[2ull * bin] = 0ULL;
+    ovf[2ull * bin + 1] = 0ULL;
+  }
+  if (cnt) atomicAdd(&d.cnt[target], cnt);
+  if (byt) atomicAdd(&d.byt[target], byt);
 }
 
 // Sums the fold partials of every partition of a window (layout of spill_window_kernel).
@@ -1340,10 +1375,10 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_bytes = a.ipl_bytes;
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
+  k.l4_ovf = (unsigned long long *)a.l4_ovf;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
-                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
+  const size_t lds = a.tier1 ? (size_t)a.lds_bytes : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (int)a.dense_ng;
@@ -1404,7 +1439,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
   if (a.stage_a) {
     hipLaunchKernelGGL(stage_reduce_a_kernel, dim3((a.lds_bins + 255) / 256, 8), dim3(256), 0, st,
-                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d);
+                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d,
+                       (const uint16_t *)(a.ipl + ipl_vals_offset(a.ipl_nb)), k.l4_ovf);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (!a.spill) return hipSuccess;

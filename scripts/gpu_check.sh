@@ -57,6 +57,9 @@ for s in $STEPS; do
       done
       python scripts/pmc_summary.py "$OUT/${TAG}_pmc_${cfg}.json" "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" roofline.kernel)" \
         "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" config.records_per_gpu)" "$OUT"/${TAG}_pmc_${cfg}_[0-9]* > /dev/null 2>> "$OUT/${TAG}_pmc_${cfg}_1.log" ;;
+    ablate)
+      ABLATE_ONLY="$arg" timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
+      rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;
     micro)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/mb scripts/microbench.hip > "$OUT/${TAG}_micro.err" 2>&1 || exit 1
       timeout -k 10 300 /tmp/mb > "$OUT/${TAG}_micro.jsonl" 2>> "$OUT/${TAG}_micro.err"

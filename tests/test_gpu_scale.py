@@ -18,6 +18,8 @@ MID = [
     ("c1-remote", W.C1_REMOTE, True, 10_000, {}),
     ("c2-local", W.LOCAL_FWD_DROP, False, 10_000, {}),
     ("c4-zipf", W.LOCAL_FWD_DROP, False, 10_000, {"zipf": 1.2}),
+    ("c4-flows", W.LOCAL_FWD_DROP, False, 10_000, dict(W.CONFIGS["c4"]["gen"])),
+    ("c4-flows-remote", W.C1_REMOTE, True, 10_000, dict(W.CONFIGS["c4"]["gen"])),
     ("c5-local", W.C5_SPEC, False, 100_000, {"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
 ]
 
