@@ -6,6 +6,10 @@
 // plugin, and it replaces the enricher + advanced-metrics goroutines
 // (pkg/enricher/enricher.go:68-135, pkg/module/metrics/metrics_module.go:276-305).
 //
+// One engine context per gfx950 device of the node; records are sharded over them by
+// the 5-tuple hash of retina_amd/dist.py (shard_of) and the contexts are merged into the
+// first one once per scrape epoch (gpuagg_merge: peer copies over xGMI).
+//
 // NOTE: the image this repository is built in has no Go toolchain; this file is the
 // maintainer-side binding, compiled only inside a Retina tree (build tag gpuagg).
 //
@@ -23,17 +27,26 @@ import "C"
 
 import (
 	"context"
+	"encoding/binary"
+	"errors"
 	"fmt"
+	"net"
+	"strings"
 	"sync"
 	"time"
 	"unsafe"
 
 	v1 "github.com/cilium/cilium/pkg/hubble/api/v1"
 	api "github.com/microsoft/retina/crd/api/v1alpha1"
+	"github.com/microsoft/retina/crd/api/v1alpha1/validations"
+	"github.com/microsoft/retina/pkg/common"
 	kcfg "github.com/microsoft/retina/pkg/config"
+	"github.com/microsoft/retina/pkg/controllers/cache"
 	"github.com/microsoft/retina/pkg/exporter"
 	"github.com/microsoft/retina/pkg/log"
+	"github.com/microsoft/retina/pkg/metrics"
 	"github.com/microsoft/retina/pkg/plugin/registry"
+	"github.com/microsoft/retina/pkg/utils"
 	"github.com/prometheus/client_golang/prometheus"
 	"go.uber.org/zap"
 )
@@ -43,6 +56,9 @@ const (
 	batchCapacity = 1 << 20
 	flushInterval = 100 * time.Millisecond
 	scrapeEpoch   = 5 * time.Second
+	maxSlots      = 1 << 20 // hard cap; dense counters grow with the pods actually seen
+	sparseLog2    = 22
+	channelDepth  = 10000 // like packetparser's recordsChannel (types_linux.go:37-38)
 )
 
 // Record is one decoded flow in the column layout of include/gpuagg.h. Producers
@@ -68,19 +84,40 @@ type rawSample struct {
 	b    []byte
 }
 
+// device is one engine context and its pinned batch.
+type device struct {
+	ctx   *C.gpuagg_ctx
+	batch *C.gpuagg_batch
+	n     int
+	cols  [6][]uint32
+}
+
 type gpuAgg struct {
 	cfg *kcfg.Config
 	l   *log.ZapLogger
 
-	mu      sync.Mutex
-	ctx     *C.gpuagg_ctx
-	batch   *C.gpuagg_batch
-	n       int
+	// mu serialises every ABI call (one thread per ctx at a time, include/gpuagg.h) and
+	// guards the fields below.
+	mu       sync.Mutex
+	devs     []*device
+	rawBuf   map[int][]byte // per kind: back-to-back raw records awaiting submit
+	spec     *api.MetricsSpec
+	vecs     map[string]*prometheus.GaugeVec
+	ctrs     map[string]*prometheus.CounterVec
+	ctrLast  map[string]float64 // counter series: value already added
+	dirty    bool               // cache changed since the last commit
+	version  uint64
+	stopping bool
+
 	records chan Record
 	raw     chan rawSample
-	rawBuf  map[int][]byte // per kind: back-to-back raw records awaiting submit
-	vecs    map[string]*prometheus.GaugeVec
+	done    chan struct{} // closed when Start returns
 }
+
+var (
+	instance   *gpuAgg
+	instanceMu sync.Mutex
+)
 
 func init() {
 	registry.Add(name, New)
@@ -88,43 +125,99 @@ func init() {
 
 // New is the registry.PluginFunc (registry.go:37).
 func New(cfg *kcfg.Config) registry.Plugin {
-	return &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, 1<<16),
-		raw: make(chan rawSample, 1<<16), rawBuf: map[int][]byte{}}
+	g := &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, channelDepth),
+		raw: make(chan rawSample, channelDepth), rawBuf: map[int][]byte{}}
+	instanceMu.Lock()
+	instance = g
+	instanceMu.Unlock()
+	return g
 }
 
-func (g *gpuAgg) Name() string                           { return name }
-func (g *gpuAgg) Generate(ctx context.Context) error     { return nil }
-func (g *gpuAgg) Compile(ctx context.Context) error      { return nil }
-func (g *gpuAgg) SetupChannel(c chan *v1.Event) error    { return nil } // no Hubble events
-func (g *gpuAgg) lastError() string                      { return C.GoString(C.gpuagg_last_error(g.ctx)) }
-func check(g *gpuAgg, rc C.int, what string) error {
+// Instance returns the plugin for producers and the cache tee (nil before New).
+func Instance() *gpuAgg {
+	instanceMu.Lock()
+	defer instanceMu.Unlock()
+	return instance
+}
+
+func (g *gpuAgg) Name() string                       { return name }
+func (g *gpuAgg) Generate(ctx context.Context) error { return nil }
+func (g *gpuAgg) Compile(ctx context.Context) error  { return nil }
+
+// SetupChannel: the engine aggregates on the GPU and emits no per-flow Hubble events
+// (the enricher's ExportReader contract, enricher.go:138-140,189-191, is not kept for
+// individual flows; see INTEGRATION.md).
+func (g *gpuAgg) SetupChannel(c chan *v1.Event) error { return nil }
+
+func lastError(ctx *C.gpuagg_ctx) string { return C.GoString(C.gpuagg_last_error(ctx)) }
+
+func check(ctx *C.gpuagg_ctx, rc C.int, what string) error {
 	if rc != C.GPUAGG_OK {
-		return fmt.Errorf("%s: %d: %s", what, int(rc), g.lastError())
+		return fmt.Errorf("%s: %d: %s", what, int(rc), lastError(ctx))
 	}
 	return nil
 }
 
-// Init creates the device context (one per GPU; device 0 here).
+// each applies fn to every device context; the first error wins.
+func (g *gpuAgg) each(what string, fn func(ctx *C.gpuagg_ctx) C.int) error {
+	var err error
+	for _, d := range g.devs {
+		if e := check(d.ctx, fn(d.ctx), what); e != nil && err == nil {
+			err = e
+		}
+	}
+	return err
+}
+
+// Init creates one engine context per gfx950 device (PluginManager calls Stop before
+// Init on every reconcile, pluginmanager.go:91-112).
 func (g *gpuAgg) Init() error {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	var ndev C.int
+	if rc := C.gpuagg_device_count(&ndev); rc != C.GPUAGG_OK || ndev == 0 {
+		return errors.New("gpuagg: no MI355X (gfx950) device")
+	}
 	remote := C.int32_t(0)
 	if g.cfg.RemoteContext {
 		remote = 1
 	}
-	cfg := C.gpuagg_config{
-		abi_version: C.GPUAGG_ABI_VERSION, device: 0, remote_context: remote,
-		max_slots: 1 << 20, max_ips: 1 << 21, sparse_capacity_log2: 24,
+	for dev := 0; dev < int(ndev); dev++ {
+		cfg := C.gpuagg_config{
+			abi_version: C.GPUAGG_ABI_VERSION, device: C.int32_t(dev), remote_context: remote,
+			max_slots: maxSlots, max_ips: 2 * maxSlots, sparse_capacity_log2: sparseLog2,
+		}
+		d := &device{}
+		if rc := C.gpuagg_create(&cfg, &d.ctx); rc != C.GPUAGG_OK {
+			g.destroyLocked()
+			return fmt.Errorf("gpuagg_create(device %d): %d", dev, int(rc))
+		}
+		if err := check(d.ctx, C.gpuagg_alloc_batch(d.ctx, batchCapacity, &d.batch), "gpuagg_alloc_batch"); err != nil {
+			C.gpuagg_destroy(d.ctx)
+			g.destroyLocked()
+			return err
+		}
+		c := d.batch.cols
+		col := func(p *C.uint32_t) []uint32 { return unsafe.Slice((*uint32)(unsafe.Pointer(p)), batchCapacity) }
+		d.cols = [6][]uint32{col(c.src_ip), col(c.dst_ip), col(c.bytes), col(c.meta), col(c.ports), col(c.dns_id)}
+		g.devs = append(g.devs, d)
 	}
-	if rc := C.gpuagg_create(&cfg, &g.ctx); rc != C.GPUAGG_OK {
-		return fmt.Errorf("gpuagg_create: %d (an MI355X/gfx950 is required)", int(rc))
-	}
-	return check(g, C.gpuagg_alloc_batch(g.ctx, batchCapacity, &g.batch), "gpuagg_alloc_batch")
+	g.stopping = false
+	g.spec = nil
+	return nil
 }
 
-// Reconcile mirrors Module.Reconcile (metrics_module.go:142-203) for the spec's
-// context options.
+// Reconcile mirrors Module.Reconcile (metrics_module.go:142-203): nothing happens when
+// the spec is unchanged or only its namespaces changed (validations.MetricsContextOptionsCompare);
+// otherwise the AdvancedRegistry is reset and the engine re-plans its metric groups.
 func (g *gpuAgg) Reconcile(spec *api.MetricsSpec) error {
 	g.mu.Lock()
 	defer g.mu.Unlock()
+	if g.spec != nil && (g.spec.Equals(spec) ||
+		validations.MetricsContextOptionsCompare(g.spec.ContextOptions, spec.ContextOptions)) {
+		g.spec = spec
+		return nil
+	}
 	opts := make([]C.gpuagg_metric_options, len(spec.ContextOptions))
 	var frees []unsafe.Pointer
 	defer func() {
@@ -138,7 +231,7 @@ func (g *gpuAgg) Reconcile(spec *api.MetricsSpec) error {
 		}
 		arr := C.malloc(C.size_t(len(ss)+1) * C.size_t(unsafe.Sizeof(uintptr(0))))
 		frees = append(frees, arr)
-		view := (*[1 << 20]*C.char)(arr)
+		view := unsafe.Slice((**C.char)(arr), len(ss)+1)
 		for i, s := range ss {
 			cs := C.CString(s)
 			frees = append(frees, unsafe.Pointer(cs))
@@ -157,13 +250,29 @@ func (g *gpuAgg) Reconcile(spec *api.MetricsSpec) error {
 	if len(opts) > 0 {
 		p = &opts[0]
 	}
+	if err := g.each("gpuagg_reconcile", func(ctx *C.gpuagg_ctx) C.int {
+		return C.gpuagg_reconcile(ctx, p, C.size_t(len(opts)))
+	}); err != nil {
+		return err
+	}
 	exporter.ResetAdvancedMetricsRegistry()
 	g.vecs = map[string]*prometheus.GaugeVec{}
-	return check(g, C.gpuagg_reconcile(g.ctx, p, C.size_t(len(opts))), "gpuagg_reconcile")
+	g.ctrs = map[string]*prometheus.CounterVec{}
+	g.ctrLast = map[string]float64{}
+	g.spec = spec
+	return nil
 }
 
-// Write is what producers call per decoded record (Enricher.Write's replacement).
-func (g *gpuAgg) Write(r Record) { g.records <- r }
+// Write is what producers call per decoded record (Enricher.Write's replacement). It
+// never blocks the reader: a full channel drops the record and counts it, like
+// packetparser's readData (packetparser_linux.go:643-651,689-695).
+func (g *gpuAgg) Write(r Record) {
+	select {
+	case g.records <- r:
+	default:
+		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Inc()
+	}
+}
 
 // WriteRaw takes one perf RawSample of the given kind; a sample of the wrong size is
 // refused like binary.Read's size mismatch (dropreason_linux.go:347-352).
@@ -171,28 +280,63 @@ func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
 	if sz, ok := rawSize[kind]; !ok || len(sample) != sz {
 		return fmt.Errorf("gpuagg: raw sample of %d bytes for kind %d", len(sample), kind)
 	}
-	g.raw <- rawSample{kind, sample}
+	select {
+	case g.raw <- rawSample{kind, sample}:
+	default:
+		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Inc()
+	}
 	return nil
 }
 
+// shardOf is retina_amd/dist.py shard_of: fmix64 of the 5-tuple, mod the devices.
+func shardOf(r *Record, n int) int {
+	if n == 1 {
+		return 0
+	}
+	fmix := func(k uint64) uint64 {
+		k ^= k >> 33
+		k *= 0xff51afd7ed558ccd
+		k ^= k >> 33
+		k *= 0xc4ceb9fe1a85ec53
+		k ^= k >> 33
+		return k
+	}
+	lo := uint64(r.SrcIP) | uint64(r.DstIP)<<32
+	hi := uint64(r.Ports) | uint64(r.Meta&0xff)<<32
+	return int(fmix(lo^fmix(hi^0x1F2E3D4C5B6A7988)) % uint64(n))
+}
+
 // Start blocks until ctx is done (PluginManager runs it in an errgroup goroutine,
-// pluginmanager.go:166-169).
+// pluginmanager.go:166-169).  It owns the pinned batches; Stop waits for it to return
+// before the contexts are destroyed.
 func (g *gpuAgg) Start(ctx context.Context) error {
+	g.mu.Lock()
+	if len(g.devs) == 0 || g.stopping {
+		g.mu.Unlock()
+		return errors.New("gpuagg: Start before Init")
+	}
+	g.done = make(chan struct{})
+	devs := g.devs
+	g.mu.Unlock()
+	defer close(g.done)
+
 	flush := time.NewTicker(flushInterval)
 	epoch := time.NewTicker(scrapeEpoch)
 	defer flush.Stop()
 	defer epoch.Stop()
-	cols := g.batch.cols
-	col := func(p *C.uint32_t) []uint32 { return unsafe.Slice((*uint32)(unsafe.Pointer(p)), batchCapacity) }
-	src, dst, byt, meta, ports, dns := col(cols.src_ip), col(cols.dst_ip), col(cols.bytes), col(cols.meta), col(cols.ports), col(cols.dns_id)
-	submit := func() error {
-		if g.n == 0 {
+	submit := func(d *device) error {
+		if d.n == 0 {
 			return nil
 		}
 		g.mu.Lock()
 		defer g.mu.Unlock()
-		err := check(g, C.gpuagg_submit(g.ctx, g.batch, C.size_t(g.n)), "gpuagg_submit")
-		g.n = 0
+		if err := g.commitLocked(); err != nil {
+			return err
+		}
+		// returns once the H2D copy is done: the batch may be refilled while the GPU
+		// aggregates (double-buffered staging, include/gpuagg.h)
+		err := check(d.ctx, C.gpuagg_submit(d.ctx, d.batch, C.size_t(d.n)), "gpuagg_submit")
+		d.n = 0
 		return err
 	}
 	submitRaw := func(kind int) error {
@@ -202,14 +346,22 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		}
 		g.mu.Lock()
 		defer g.mu.Unlock()
-		// gpuagg_submit_raw copies the records to HBM before it returns
-		err := check(g, C.gpuagg_submit_raw(g.ctx, C.int(kind), unsafe.Pointer(&buf[0]),
+		if err := g.commitLocked(); err != nil {
+			return err
+		}
+		// raw records are not sharded by 5-tuple before decode: they go to device 0
+		err := check(devs[0].ctx, C.gpuagg_submit_raw(devs[0].ctx, C.int(kind), unsafe.Pointer(&buf[0]),
 			C.size_t(len(buf)/rawSize[kind])), "gpuagg_submit_raw")
 		g.rawBuf[kind] = buf[:0]
 		return err
 	}
 	submitAll := func() error {
-		err := submit()
+		var err error
+		for _, d := range devs {
+			if e := submit(d); e != nil && err == nil {
+				err = e
+			}
+		}
 		for kind := range rawSize {
 			if e := submitRaw(kind); e != nil && err == nil {
 				err = e
@@ -222,10 +374,13 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		case <-ctx.Done():
 			return submitAll()
 		case r := <-g.records:
-			src[g.n], dst[g.n], byt[g.n], meta[g.n], ports[g.n], dns[g.n] = r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID
-			g.n++
-			if g.n == batchCapacity {
-				if err := submit(); err != nil {
+			d := devs[shardOf(&r, len(devs))]
+			i := d.n
+			d.cols[0][i], d.cols[1][i], d.cols[2][i], d.cols[3][i], d.cols[4][i], d.cols[5][i] =
+				r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID
+			d.n++
+			if d.n == batchCapacity {
+				if err := submit(d); err != nil {
 					g.l.Error("submit failed", zap.Error(err))
 				}
 			}
@@ -241,6 +396,9 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 				g.l.Error("submit failed", zap.Error(err))
 			}
 		case <-epoch.C:
+			if err := submitAll(); err != nil {
+				g.l.Error("submit failed", zap.Error(err))
+			}
 			if err := g.publish(); err != nil {
 				g.l.Error("snapshot failed", zap.Error(err))
 			}
@@ -248,23 +406,42 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 	}
 }
 
-// publish renders the engine's series into the AdvancedRegistry gauge vectors with
-// the reference's names and labels (forward.go:100-118, drops.go:268-286, ...).
+// publish merges the devices into the first one and renders its series into the
+// AdvancedRegistry vectors with the reference's names, types, Help texts and labels
+// (forward.go:18-26, drops.go:18-23, tcpflags.go:18-24, tcpretrans.go:18-24 -- GaugeVec;
+// dns.go:21-30,50-66 -- CounterVec), then retires the slots of deleted pods.
 func (g *gpuAgg) publish() error {
 	g.mu.Lock()
 	defer g.mu.Unlock()
+	if g.stopping || len(g.devs) == 0 {
+		return nil
+	}
+	if len(g.devs) > 1 {
+		ctxs := make([]*C.gpuagg_ctx, len(g.devs))
+		for i, d := range g.devs {
+			ctxs[i] = d.ctx
+		}
+		if err := check(ctxs[0], C.gpuagg_merge(&ctxs[0], C.size_t(len(ctxs))), "gpuagg_merge"); err != nil {
+			return err
+		}
+	}
+	ctx := g.devs[0].ctx
 	var r *C.gpuagg_result
-	if err := check(g, C.gpuagg_snapshot(g.ctx, &r), "gpuagg_snapshot"); err != nil {
+	if err := check(ctx, C.gpuagg_snapshot(ctx, &r), "gpuagg_snapshot"); err != nil {
 		return err
 	}
 	defer C.gpuagg_result_free(r)
+	if lost := uint64(C.gpuagg_result_dropped(r)); lost > 0 {
+		g.l.Warn("group-by table full: series undercount", zap.Uint64("lost_updates", lost))
+	}
 	n := int(C.gpuagg_result_count(r))
 	for i := 0; i < n; i++ {
-		var metric *C.char
+		var metric, typ, help *C.char
 		var nl C.uint32_t
 		var names, values **C.char
 		var v C.uint64_t
 		C.gpuagg_result_series(r, C.size_t(i), &metric, &nl, &names, &values, &v)
+		C.gpuagg_result_family(r, C.size_t(i), &typ, &help)
 		ns := unsafe.Slice(names, int(nl))
 		vs := unsafe.Slice(values, int(nl))
 		labels := make([]string, int(nl))
@@ -273,23 +450,240 @@ func (g *gpuAgg) publish() error {
 			labels[j], lvals[j] = C.GoString(ns[j]), C.GoString(vs[j])
 		}
 		full := C.GoString(metric) // "networkobservability_<name>"
+		short := full[len(exporter.RetinaNamespace)+1:]
+		if C.GoString(typ) == "counter" {
+			vec, ok := g.ctrs[full]
+			if !ok {
+				vec = exporter.CreatePrometheusCounterVecForMetric(exporter.AdvancedRegistry, short, C.GoString(help), labels...)
+				g.ctrs[full] = vec
+			}
+			// the engine's values are cumulative since reconcile: add the increment
+			key := full + "\x00" + strings.Join(lvals, "\x00")
+			if d := float64(v) - g.ctrLast[key]; d > 0 {
+				vec.WithLabelValues(lvals...).Add(d)
+				g.ctrLast[key] = float64(v)
+			}
+			continue
+		}
 		vec, ok := g.vecs[full]
 		if !ok {
-			vec = exporter.CreatePrometheusGaugeVecForMetric(exporter.AdvancedRegistry,
-				full[len(exporter.RetinaNamespace)+1:], full, labels...)
+			vec = exporter.CreatePrometheusGaugeVecForMetric(exporter.AdvancedRegistry, short, C.GoString(help), labels...)
 			g.vecs[full] = vec
 		}
 		vec.WithLabelValues(lvals...).Set(float64(v))
 	}
+	// the epoch is published: slots no IP maps to any more are freed (their series keep
+	// the last published value, as the reference's gauges of a deleted pod do)
+	return g.each("gpuagg_retire_slots", func(c *C.gpuagg_ctx) C.int { return C.gpuagg_retire_slots(c, nil) })
+}
+
+// Stop stops Start (it waits for it) and releases the contexts.
+func (g *gpuAgg) Stop() error {
+	g.mu.Lock()
+	g.stopping = true
+	done := g.done
+	g.mu.Unlock()
+	if done != nil {
+		select { // Start returns once its ctx is cancelled by the manager
+		case <-done:
+		case <-time.After(10 * time.Second):
+			return errors.New("gpuagg: Start did not return; contexts kept")
+		}
+	}
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	g.destroyLocked()
 	return nil
 }
 
-func (g *gpuAgg) Stop() error {
+func (g *gpuAgg) destroyLocked() {
+	for _, d := range g.devs {
+		C.gpuagg_destroy(d.ctx) // frees the pinned batch too
+	}
+	g.devs = nil
+	g.done = nil
+}
+
+// ---- the IP cache ---------------------------------------------------------------------
+
+// InternDNS returns the dns_id a DNS producer writes for an AddDNSInfo payload
+// (flow_utils.go:186-220), the same on every device.
+func (g *gpuAgg) InternDNS(rcode uint32, qtypes []string, query string, ips []string, numAnswers uint32) (uint32, error) {
 	g.mu.Lock()
 	defer g.mu.Unlock()
-	if g.ctx != nil {
-		C.gpuagg_destroy(g.ctx)
-		g.ctx = nil
+	qt, q, ip := C.CString(strings.Join(qtypes, ",")), C.CString(query), C.CString(strings.Join(ips, ","))
+	defer C.free(unsafe.Pointer(qt))
+	defer C.free(unsafe.Pointer(q))
+	defer C.free(unsafe.Pointer(ip))
+	var id C.uint32_t
+	err := g.each("gpuagg_dns_intern", func(ctx *C.gpuagg_ctx) C.int {
+		return C.gpuagg_dns_intern(ctx, C.uint32_t(rcode), qt, q, ip, C.uint32_t(numAnswers), &id)
+	})
+	return uint32(id), err
+}
+
+// commitLocked installs the cache's IP -> pod map before a batch that follows a cache
+// change (versioned: earlier batches keep the previous map).
+func (g *gpuAgg) commitLocked() error {
+	if !g.dirty {
+		return nil
 	}
-	return nil
+	g.version++
+	v := C.uint64_t(g.version)
+	g.dirty = false
+	return g.each("gpuagg_cache_commit", func(ctx *C.gpuagg_ctx) C.int { return C.gpuagg_cache_commit(ctx, v) })
+}
+
+func ipv4LE(ip string) (uint32, bool) {
+	p := net.ParseIP(ip).To4()
+	if p == nil {
+		return 0, false
+	}
+	return binary.LittleEndian.Uint32(p), true // the record encoding (include/gpuagg.h)
+}
+
+// CacheTee is a cache.CacheInterface that forwards to the agent's cache and mirrors
+// every update and delete into the engine, so the GPU's IP table follows exactly the
+// reference's cache (cache.go:196-420).  cmd/standard/daemon.go wraps the cache it
+// hands to the controllers: `controllerCache = gpuagg.NewCacheTee(controllerCache)`.
+type CacheTee struct {
+	cache.CacheInterface
+}
+
+func NewCacheTee(c cache.CacheInterface) *CacheTee { return &CacheTee{CacheInterface: c} }
+
+func withEngine(fn func(g *gpuAgg) error) error {
+	g := Instance()
+	if g == nil {
+		return nil
+	}
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if len(g.devs) == 0 {
+		return nil
+	}
+	err := fn(g)
+	g.dirty = true
+	return err
+}
+
+func (t *CacheTee) UpdateRetinaEndpoint(ep *common.RetinaEndpoint) error {
+	if err := t.CacheInterface.UpdateRetinaEndpoint(ep); err != nil {
+		return err
+	}
+	ips, err := ep.IPs()
+	if err != nil {
+		return err
+	}
+	var v4 []uint32
+	for _, s := range ips {
+		if x, ok := ipv4LE(s); ok {
+			v4 = append(v4, x)
+		}
+	}
+	if len(v4) == 0 {
+		return nil
+	}
+	return withEngine(func(g *gpuAgg) error {
+		ns, pod := C.CString(ep.Namespace()), C.CString(ep.Name())
+		defer C.free(unsafe.Pointer(ns))
+		defer C.free(unsafe.Pointer(pod))
+		var kind, wname *C.char // getWorkloads: the first owner reference (enricher.go:169-183)
+		if refs := ep.OwnerRefs(); len(refs) > 0 && refs[0] != nil {
+			kind, wname = C.CString(refs[0].Kind), C.CString(refs[0].Name)
+			defer C.free(unsafe.Pointer(kind))
+			defer C.free(unsafe.Pointer(wname))
+		}
+		return g.each("gpuagg_cache_update_endpoint", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_update_endpoint(ctx, ns, pod, kind, wname, (*C.uint32_t)(unsafe.Pointer(&v4[0])), C.size_t(len(v4)))
+		})
+	})
+}
+
+func (t *CacheTee) DeleteRetinaEndpoint(epKey string) error {
+	if err := t.CacheInterface.DeleteRetinaEndpoint(epKey); err != nil {
+		return err
+	}
+	nsName := strings.SplitN(epKey, "/", 2)
+	if len(nsName) != 2 {
+		return nil
+	}
+	return withEngine(func(g *gpuAgg) error {
+		ns, pod := C.CString(nsName[0]), C.CString(nsName[1])
+		defer C.free(unsafe.Pointer(ns))
+		defer C.free(unsafe.Pointer(pod))
+		return g.each("gpuagg_cache_delete_endpoint", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_delete_endpoint(ctx, ns, pod)
+		})
+	})
+}
+
+func (t *CacheTee) UpdateRetinaSvc(svc *common.RetinaSvc) error {
+	if err := t.CacheInterface.UpdateRetinaSvc(svc); err != nil {
+		return err
+	}
+	ip, err := svc.GetPrimaryIP()
+	if err != nil {
+		return err
+	}
+	x, ok := ipv4LE(ip)
+	if !ok {
+		return nil
+	}
+	return withEngine(func(g *gpuAgg) error {
+		ns, n := C.CString(svc.Namespace()), C.CString(svc.Name())
+		defer C.free(unsafe.Pointer(ns))
+		defer C.free(unsafe.Pointer(n))
+		return g.each("gpuagg_cache_update_service", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_update_service(ctx, ns, n, C.uint32_t(x))
+		})
+	})
+}
+
+func (t *CacheTee) DeleteRetinaSvc(svcKey string) error {
+	if err := t.CacheInterface.DeleteRetinaSvc(svcKey); err != nil {
+		return err
+	}
+	nsName := strings.SplitN(svcKey, "/", 2)
+	if len(nsName) != 2 {
+		return nil
+	}
+	return withEngine(func(g *gpuAgg) error {
+		ns, n := C.CString(nsName[0]), C.CString(nsName[1])
+		defer C.free(unsafe.Pointer(ns))
+		defer C.free(unsafe.Pointer(n))
+		return g.each("gpuagg_cache_delete_service", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_delete_service(ctx, ns, n)
+		})
+	})
+}
+
+func (t *CacheTee) UpdateRetinaNode(node *common.RetinaNode) error {
+	if err := t.CacheInterface.UpdateRetinaNode(node); err != nil {
+		return err
+	}
+	x, ok := ipv4LE(node.IPString())
+	if !ok {
+		return nil
+	}
+	return withEngine(func(g *gpuAgg) error {
+		n := C.CString(node.Name())
+		defer C.free(unsafe.Pointer(n))
+		return g.each("gpuagg_cache_update_node", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_update_node(ctx, n, C.uint32_t(x))
+		})
+	})
+}
+
+func (t *CacheTee) DeleteRetinaNode(nodeName string) error {
+	if err := t.CacheInterface.DeleteRetinaNode(nodeName); err != nil {
+		return err
+	}
+	return withEngine(func(g *gpuAgg) error {
+		n := C.CString(nodeName)
+		defer C.free(unsafe.Pointer(n))
+		return g.each("gpuagg_cache_delete_node", func(ctx *C.gpuagg_ctx) C.int {
+			return C.gpuagg_cache_delete_node(ctx, n)
+		})
+	})
 }

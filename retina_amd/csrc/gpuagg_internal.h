@@ -83,8 +83,6 @@ struct GroupPlan {
   uint64_t dense_base;
   uint32_t key_mode;  // dense: 0 constant key, 1 slot key
   uint32_t nbins;     // dense: bins of this group (nkeys * 2 * nsub)
-  uint32_t lds_base;  // tier-1 launch: first LDS bin of the group (keyed by IP position)
-  uint32_t lds_nbins; // tier-1 launch: LDS bins of the group, 0 = spilled (slot-keyed HBM)
 };
 
 struct Plan {
@@ -206,7 +204,6 @@ constexpr uint32_t kL4CountShift = 20;
 constexpr uint32_t kL4BytesMask = (1u << kL4CountShift) - 1;
 constexpr uint32_t kL4ByteLimit = 1u << kL4CountShift;
 constexpr uint32_t kL4ExtraBytes = 64 * 4 + kMaxSpillWindows * 4;  // dummies + spill counters
-constexpr uint32_t kL4RingBytes = 16 * 128 * 8;  // per-wave rings of spilled records (16 waves)
 GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
 }

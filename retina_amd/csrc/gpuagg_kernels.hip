@@ -40,6 +40,7 @@ struct DevSparse {
   unsigned long long *k0, *k1, *k2, *cnt, *byt;
   uint32_t mask;
   unsigned long long *dropped;
+  uint32_t compact;  // 64-bit keys (see sparse_add_compact), 2 words per slot at k0
 };
 struct DevSketch {
   uint32_t *cms;
@@ -73,7 +74,6 @@ struct KArgs {
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
-  unsigned long long *l4_ovf;  // tier-1: [2 * lds_bins] exact-correction pairs
   Plan p;
 };
 
@@ -101,11 +101,33 @@ __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
   return ip_pick(ip, e1, e2);
 }
 
+// Compact table (plans whose every sparse key fits 64 bits: local context whose only
+// sparse groups are DNS -- k1 == 0 and k2 = dns id, so key = k0 | dns id): one 16-byte
+// slot (key, count) per entry; the claiming CAS publishes the whole key, so an insert is
+// one CAS and one add and a key never occupies two slots.
+__device__ __forceinline__ void sparse_add_compact(const DevSparse &s, uint64_t key, uint64_t c) {
+  uint32_t h = (uint32_t)fmix64(key ^ 0x243F6A8885A308D3ULL) & s.mask;
+  for (uint32_t probe = 0; probe < kSparseMaxProbe; ++probe) {
+    unsigned long long *slot = s.k0 + 2ull * h;
+    const unsigned long long cur = atomicCAS(&slot[0], 0ULL, (unsigned long long)key);
+    if (cur == 0ULL || cur == key) {
+      atomicAdd(&slot[1], (unsigned long long)c);
+      return;
+    }
+    h = (h + 1) & s.mask;
+  }
+  atomicAdd(s.dropped, 1ULL);
+}
+
 // Insert-or-add into the sparse table. No lane ever waits for another: a lane that
 // meets a slot whose key is still being published moves on, so a key may occupy
 // more than one slot; the host sums duplicates when it renders series.
 __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint64_t k1,
                                            uint64_t k2, uint64_t c, uint64_t b) {
+  if (s.compact) {
+    sparse_add_compact(s, k0 | (k2 & 0xFFFFFFFFULL), c);
+    return;
+  }
   uint32_t h = (uint32_t)key_hash(k0, k1, k2) & s.mask;
   for (uint32_t probe = 0; probe < kSparseMaxProbe; ++probe) {
     const size_t o = (size_t)h * kSparseSlotWords;  // slot h's line (k1 = k0 + 1, ...)
@@ -263,7 +285,63 @@ __device__ __forceinline__ bool family_matches(uint32_t fam, uint32_t verdict, u
   return false;
 }
 
-// One record through every metric group.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)lane);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Wave-level key de-duplication before the global table (BASELINE.json north_star): the
+// lanes of a wave inserting the same key merge into the lowest of them, which inserts the
+// summed count and bytes once -- a Zipf heavy hitter costs one global CAS/add chain per
+// wave instead of one per lane.  Lanes are bucketed by 6 key-hash bits (6 ballots); only
+// buckets holding several lanes compare full keys, one leader key per round, so a wave of
+// distinct keys pays the ballots and one vote.  Called by the whole wave (converged);
+// `valid` is false on lanes with nothing to insert.
+__device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, uint64_t k0, uint64_t k1,
+                                              uint64_t k2, uint64_t b) {
+  const uint64_t vm = __ballot(valid);
+  if (!vm) return;
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t x = (uint32_t)(k0 ^ (k0 >> 29) ^ k1 ^ (k1 >> 31) ^ k2 ^ (k2 >> 27));
+  const uint32_t h = (x * 0x9E3779B1u) >> 26;
+  uint64_t eq = vm;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const bool bit = (h >> i) & 1u;
+    const uint64_t B = __ballot(bit);
+    eq &= bit ? B : ~B;
+  }
+  bool pending = valid && __popcll(eq) > 1;
+  bool keep = valid;
+  uint64_t c = 1, pm;
+  while ((pm = __ballot(pending)) != 0) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(pm);
+    const bool same = pending && k0 == readlane64(k0, leader) && k1 == readlane64(k1, leader) &&
+                      k2 == readlane64(k2, leader);
+    const uint64_t m = __ballot(same);
+    const uint64_t bsum = wave_sum64(same ? b : 0ULL);
+    if (same) {
+      pending = false;
+      if (lane == leader) {
+        c = (uint64_t)__popcll(m);
+        b = bsum;
+      } else {
+        keep = false;
+      }
+    }
+  }
+  if (keep) sparse_add(s, k0, k1, k2, c, b);
+}
+
+// One record through every metric group.  Converged: every lane of the wave runs it
+// (inactive lanes carry no endpoint and an unmatched verdict), so the sparse inserts can
+// de-duplicate keys across the wave (sparse_insert).
 __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
                                              const DevSparse &s, uint32_t sip, uint32_t dip,
                                              uint32_t nbytes, uint32_t meta, uint32_t ports,
@@ -276,9 +354,9 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
   const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16;
 
   for (int g = 0; g < p.ngroups; ++g) {
-    const GroupPlan gp = p.g[g];
+    const GroupPlan gp = p.g[g];  // plan: wave-uniform
     const uint32_t fam = gp.family;
-    if (!family_matches(fam, verdict, proto, dnstype, flagmask)) continue;
+    const bool hit = family_matches(fam, verdict, proto, dnstype, flagmask);
     const uint32_t addb = (fam <= FAM_DROP) ? nbytes : 0u;
 
     if (p.local) {
@@ -289,22 +367,18 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
       const bool d_ok = ld.slot >= 0 && !ld.api;
       if (fam == FAM_DNS_REQ || fam == FAM_DNS_RESP) {
         // dns.go:506-540: exactly one update; both sides -> pick by TrafficDirection.
-        int side;
-        if (s_ok && d_ok) side = (tdir == 1) ? 0 : 1;
-        else if (d_ok) side = 0;
-        else if (s_ok) side = 1;
-        else continue;
+        const int side = (s_ok && d_ok) ? ((tdir == 1) ? 0 : 1) : (d_ok ? 0 : 1);
         const SideKey k = side == 0 ? side_key(gp.src_opts, dip, ld, dport, proto)
                                     : side_key(gp.src_opts, sip, ls, sport, proto);
-        sparse_add(s, key0(g, (uint32_t)side, k.slot1, k.ip), key1(k.port17, 0, 0),
-                   key2(0, dns), 1, 0);
+        sparse_insert(s, hit && (s_ok || d_ok), key0(g, (uint32_t)side, k.slot1, k.ip), key1(k.port17, 0, 0),
+                      key2(0, dns), 0);
         continue;
       }
       for (int side = 0; side < 2; ++side) {  // 0 ingress (dst), 1 egress (src)
-        const bool ok = side == 0 ? d_ok : s_ok;
-        if (!ok) continue;
+        const bool ok = hit && (side == 0 ? d_ok : s_ok);
         const Lk &lk = side == 0 ? ld : ls;
         if (!gp.sparse) {
+          if (!ok) continue;
           const uint32_t key = gp.key_mode ? (uint32_t)lk.slot : 0u;
           const uint32_t row = (uint32_t)gp.dense_base + (key * 2u + (uint32_t)side) * gp.nsub;
           if (fam == FAM_TCPFLAGS) {
@@ -312,18 +386,20 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
           } else {
             ds.add(row + (fam == FAM_DROP ? reason : 0u), addb);
           }
-        } else {
-          const SideKey k = side == 0 ? side_key(gp.src_opts, dip, ld, dport, proto)
-                                      : side_key(gp.src_opts, sip, ls, sport, proto);
-          if (fam == FAM_TCPFLAGS) {
-            for (uint32_t m = flagmask; m; m &= m - 1) {
-              const uint32_t sub = ((uint32_t)__builtin_ctz(m) << 3) | (uint32_t)side;
-              sparse_add(s, key0(g, sub, k.slot1, k.ip), key1(k.port17, 0, 0), 0, 1, 0);
-            }
-          } else {
-            const uint32_t sub = ((fam == FAM_DROP ? reason : 0u) << 3) | (uint32_t)side;
-            sparse_add(s, key0(g, sub, k.slot1, k.ip), key1(k.port17, 0, 0), 0, 1, addb);
+          continue;
+        }
+        const SideKey k = side == 0 ? side_key(gp.src_opts, dip, ld, dport, proto)
+                                    : side_key(gp.src_opts, sip, ls, sport, proto);
+        if (fam == FAM_TCPFLAGS) {
+          uint32_t m = ok ? flagmask : 0u;
+          while (__ballot(m != 0)) {  // converged: trips = most flags of any lane
+            const uint32_t sub = (m ? ((uint32_t)__builtin_ctz(m) << 3) : 0u) | (uint32_t)side;
+            sparse_insert(s, m != 0, key0(g, sub, k.slot1, k.ip), key1(k.port17, 0, 0), 0, 0);
+            m &= m - 1;
           }
+        } else {
+          const uint32_t sub = ((fam == FAM_DROP ? reason : 0u) << 3) | (uint32_t)side;
+          sparse_insert(s, ok, key0(g, sub, k.slot1, k.ip), key1(k.port17, 0, 0), 0, addb);
         }
       }
     } else {
@@ -332,16 +408,18 @@ __device__ __forceinline__ void apply_groups(const Plan &p, const DenseSink &ds,
       const SideKey kd = side_key(gp.dst_opts, dip, ld, dport, proto);
       const uint64_t k1 = key1(ks.port17, kd.port17, kd.slot1);
       if (fam == FAM_TCPFLAGS) {
-        for (uint32_t m = flagmask; m; m &= m - 1) {
-          const uint32_t sub = (uint32_t)__builtin_ctz(m) << 3;
-          sparse_add(s, key0(g, sub, ks.slot1, ks.ip), k1, key2(kd.ip, 0), 1, 0);
+        uint32_t m = hit ? flagmask : 0u;
+        while (__ballot(m != 0)) {
+          const uint32_t sub = m ? (uint32_t)__builtin_ctz(m) << 3 : 0u;
+          sparse_insert(s, m != 0, key0(g, sub, ks.slot1, ks.ip), k1, key2(kd.ip, 0), 0);
+          m &= m - 1;
         }
       } else {
         uint32_t sub = 0, dnsv = 0;
         if (fam == FAM_FWD || fam == FAM_RETRANS) sub = tdir << 1;
         else if (fam == FAM_DROP) sub = (reason << 3) | (tdir << 1);
         else dnsv = dns;
-        sparse_add(s, key0(g, sub, ks.slot1, ks.ip), k1, key2(kd.ip, dnsv), 1, addb);
+        sparse_insert(s, hit, key0(g, sub, ks.slot1, ks.ip), k1, key2(kd.ip, dnsv), addb);
       }
     }
   }
@@ -382,20 +460,26 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
 // Workgroup b owns records [b*chunk, (b+1)*chunk). With kVec every lane takes 4
 // consecutive records per step (16-byte loads per column), issues the 16 IP-table
 // loads of their 8 addresses back to back, then walks the 4 records in a rolled loop
-// (register rotation keeps one copy of the per-record code).
+// (register rotation keeps one copy of the per-record code).  Both loops are
+// wave-uniform -- lanes past the end read the last element and pass an inactive record
+// (no endpoint, an unmatched verdict) -- so f may use cross-lane operations.
+constexpr uint32_t kInactiveMeta = kVerdictUnencodable << 8;
 template <bool kVec, class F>
 __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f) {
   const bool need_bytes = a.p.need_bytes;  // no forward / drop group: the column is not read
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
+  const uint32_t lane = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
+  const Lk none{-1, 0};
   uint64_t tail = start;
-  if (kVec && start < end) {
-    const uint64_t vend = start + ((end - start) & ~3ULL);
+  if (kVec && start + 4 <= end) {
+    const uint64_t v0 = start >> 2, vend = v0 + ((end - start) >> 2), vlast = vend - 1;
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
     const uint4 *p4 = (const uint4 *)a.c.ports, *q4 = (const uint4 *)a.c.dns;
-    for (uint64_t i = start + 4ULL * threadIdx.x; i < vend; i += 4ULL * blockDim.x) {
-      const uint64_t v = i >> 2;
+    for (uint64_t vw = v0 + wave0; vw < vend; vw += blockDim.x) {
+      const bool act = vw + lane < vend;
+      const uint64_t v = act ? vw + lane : vlast;
       const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
       const uint4 vb = need_bytes ? b4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
@@ -414,21 +498,27 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       uint32_t s0 = vs.x, s1 = vs.y, s2 = vs.z, s3 = vs.w, d0 = vd.x, d1 = vd.y, d2 = vd.z, d3 = vd.w;
       uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
       uint32_t p0 = vp.x, p1 = vp.y, p2 = vp.z, p3 = vp.w, q0 = vq.x, q1 = vq.y, q2 = vq.z, q3 = vq.w;
+      if (!act) {
+        ls0 = ls1 = ls2 = ls3 = ld0 = ld1 = ld2 = ld3 = none;
+        m0 = m1 = m2 = m3 = kInactiveMeta;
+      }
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
-        f(s0, d0, b0, m0, p0, q0, ls0, ld0);
+        f(s0, d0, b0, m0, p0, q0, ls0, ld0, act);
         s0 = s1; s1 = s2; s2 = s3; d0 = d1; d1 = d2; d2 = d3;
         b0 = b1; b1 = b2; b2 = b3; m0 = m1; m1 = m2; m2 = m3;
         p0 = p1; p1 = p2; p2 = p3; q0 = q1; q1 = q2; q2 = q3;
         ls0 = ls1; ls1 = ls2; ls2 = ls3; ld0 = ld1; ld1 = ld2; ld2 = ld3;
       }
     }
-    tail = vend;
+    tail = start + ((end - start) & ~3ULL);
   }
-  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
+  for (uint64_t i0 = tail + wave0; i0 < end; i0 += blockDim.x) {
+    const bool act = i0 + lane < end;
+    const uint64_t i = act ? i0 + lane : end - 1;
     const uint32_t sip = a.c.src[i], dip = a.c.dst[i];
-    f(sip, dip, need_bytes ? a.c.bytes[i] : 0u, a.c.meta[i], need_ports ? a.c.ports[i] : 0u,
-      need_dns ? a.c.dns[i] : 0u, ip_lookup(a.t, sip), ip_lookup(a.t, dip));
+    f(sip, dip, need_bytes ? a.c.bytes[i] : 0u, act ? a.c.meta[i] : kInactiveMeta, need_ports ? a.c.ports[i] : 0u,
+      need_dns ? a.c.dns[i] : 0u, act ? ip_lookup(a.t, sip) : none, act ? ip_lookup(a.t, dip) : none, act);
   }
 }
 
@@ -460,9 +550,9 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   const DenseSink ds = dense_sink_init(a, lds);
   for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
                         [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports,
-                            uint32_t dns, const Lk &ls, const Lk &ld) {
+                            uint32_t dns, const Lk &ls, const Lk &ld, bool act) {
                           apply_groups(a.p, ds, a.s, sip, dip, nb, meta, ports, dns, ls, ld);
-                          if (kSketch) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
+                          if (kSketch && act) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
                         });
   dense_flush(a, ds);
 }
@@ -492,7 +582,7 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   }
   for_each_record<kVec>(a, false, false,
                         [&](uint32_t, uint32_t, uint32_t nb, uint32_t meta, uint32_t, uint32_t,
-                            const Lk &ls, const Lk &ld) {
+                            const Lk &ls, const Lk &ld, bool) {
     const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
     const bool s_ok = ls.slot >= 0 && !ls.api;  // getLocalCtxValues (types.go:379-416)
     const bool d_ok = ld.slot >= 0 && !ld.api;
@@ -549,29 +639,25 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   dense_flush(a, ds);
 }
 
-// ---- tier-1: IP keys and 32-bit bins in LDS, bins indexed by IP-table position -------
-// LDS holds only the KEYS of the bucketized-cuckoo IP image (u32[2nb]); a probe yields
-// the position j of the matching key, or P = 2nb (not a pod, or the apiserver pseudo
-// pod, which local context treats alike, types.go:407-413).  Endpoint-keyed groups whose
-// bins fit LDS count per (position, side, sub) instead of (slot, side, sub), so no probe
-// reads a slot id.  stage_reduce_a_kernel maps positions to slots through the image's
-// u16 value array in HBM when it folds the workgroups' copies: a pod's secondary IPs are
-// other positions that add into the same slot bins there.  Groups whose bins do not fit
-// (C2: the 10 % drops into 10k x 2 x 8 bins) stay slot-keyed in HBM: their records are
-// queued in a per-wave LDS ring and spilled 64 at a time, reading their slots from the
-// value array once per queued record.
+// ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
+// Probe of the LDS cuckoo image: two 8-byte bucket reads and 4 compares give the index
+// of the matching key (or ~0u); the u16 slot id is read separately so all key reads of
+// a thread's records can be in flight together.
 __device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32_t nb, uint32_t seed,
                                                     uint32_t ip) {
   uint32_t b1, b2;
   ipl_buckets(ip, seed, nb, b1, b2);
   const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
-  uint32_t j = nb * 2;  // P: not found
+  uint32_t j = nb * 2;  // sentinel entry: kIplNoSlot
   j = k1.x == ip ? b1 * 2 : j;
   j = k1.y == ip ? b1 * 2 + 1 : j;
   j = k2.x == ip ? b2 * 2 : j;
   j = k2.y == ip ? b2 * 2 + 1 : j;
   return j;
 }
+
+// slot id, or kIplNoSlot (not a pod, or the apiserver pseudo pod)
+__device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
 
 struct L4Ctx {
   uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
@@ -584,78 +670,37 @@ struct L4Ctx {
     return valid & (((old & kL4BytesMask) + b > kL4BytesMask) | (old >= 0xFFE00000u) |
                     (nb >= kL4ByteLimit));
   }
-  // Exact correction after a packed add (count:12 | bytes:20) into LDS bin `lbin` returned
-  // `old`: a carry out of the bytes field, a wrap of the count field, or a packet too big
-  // for the field.  The difference goes into a per-bin overflow pair in HBM (`ovf`,
-  // indexed like the LDS bins, folded by stage_reduce_a_kernel) -- LDS bins are keyed
-  // by position, so the slot-keyed dense counters cannot take it here.  Rare; the test
-  // is 3 VALU ops.
-  unsigned long long *ovf;  // [2 * L4]: count, bytes per LDS bin
-  __device__ __forceinline__ void fix(bool valid, uint32_t old, uint32_t nb, uint32_t lbin) const {
+  // Exact correction after a packed add (count:12 | bytes:20) returned `old`: a carry
+  // out of the bytes field, a wrap of the count field, or a packet too big for the
+  // field is booked into the global counters.  Rare; the test is 3 VALU ops.
+  __device__ __forceinline__ void fix(bool valid, uint32_t old, uint32_t nb, uint32_t bin) const {
     const uint32_t b = nb < kL4ByteLimit ? nb : 0u;
-    if (!(valid && ((old & kL4BytesMask) + b > kL4BytesMask || old >= 0xFFE00000u || nb >= kL4ByteLimit)))
+    if (!(valid && ((old & kL4BytesMask) + b > kL4BytesMask || old >= 0xFFE00000u ||
+                    nb >= kL4ByteLimit)))
       return;
-    unsigned long long *o = ovf + 2ull * lbin;
-    if (nb >= kL4ByteLimit) atomicAdd(&o[1], (unsigned long long)nb);
+    if (nb >= kL4ByteLimit) atomicAdd(&d.byt[bin], (unsigned long long)nb);
     const uint32_t carry = ((old & kL4BytesMask) + b) >> kL4CountShift;
     const uint32_t wrap = ((old >> kL4CountShift) + 1u + carry) >> (32 - kL4CountShift);
     if (carry) {
-      atomicAdd(&o[1], (unsigned long long)kL4ByteLimit);
-      atomicAdd(&o[0], ~0ULL);  // the carry also bumped the count field
+      atomicAdd(&d.byt[bin], (unsigned long long)kL4ByteLimit);
+      atomicAdd(&d.cnt[bin], ~0ULL);  // the carry also bumped the count field
     }
-    if (wrap) atomicAdd(&o[0], 1ULL << (32 - kL4CountShift));
+    if (wrap) atomicAdd(&d.cnt[bin], 1ULL << (32 - kL4CountShift));
   }
 };
 static_assert(kL4CountShift == 20, "fix() thresholds assume count:12 | bytes:20");
 
-// A record's fields as the tier-1 group updates read them.
-struct Rec {
-  uint32_t nbytes, verdict, reason, flagmask;
-};
-__device__ __forceinline__ Rec rec_of(uint32_t nbytes, uint32_t meta, bool any_flags) {
-  Rec r;
-  r.nbytes = nbytes;
-  r.verdict = meta_verdict(meta);
-  r.reason = meta_reason(meta);
-  r.flagmask = (any_flags && r.verdict == kVerdictForwarded && meta_proto(meta) == 6)
-                   ? flag_label_mask(meta_flags(meta)) : 0u;
-  return r;
-}
-// Ring entry word 1: bytes:20 | verdict class:2 | reason:3 | flag mask:7 (records whose
-// bytes do not fit take the direct path).
-constexpr uint32_t kRingByteLimit = 1u << 20;
-__device__ __forceinline__ uint32_t rec_pack(const Rec &r) {
-  const uint32_t cls = r.verdict == kVerdictForwarded ? 1u : r.verdict == kVerdictDropped ? 2u
-                       : r.verdict == kVerdictRetrans ? 3u : 0u;
-  return (r.nbytes & (kRingByteLimit - 1)) | (cls << 20) | (r.reason << 22) | (r.flagmask << 25);
-}
-__device__ __forceinline__ Rec rec_unpack(uint32_t w) {
-  const uint32_t cls = (w >> 20) & 3u;
-  Rec r;
-  r.nbytes = w & (kRingByteLimit - 1);
-  r.verdict = cls == 1u ? kVerdictForwarded : cls == 2u ? kVerdictDropped : cls == 3u ? kVerdictRetrans : 0u;
-  r.reason = (w >> 22) & 7u;
-  r.flagmask = w >> 25;
-  return r;
-}
-
-// Does a record update group f (tier-1 families only: fwd / drop / tcpflags / retrans)?
-__device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t flagmask) {
-  if (f == FAM_TCPFLAGS) return flagmask != 0;
-  return verdict == (f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans);
-}
-
 // Group descriptors of the dense local-context plan, compile-time indexed (SGPRs).
 // SIG != 0 also fixes every group's family and LDS residency at compile time (4 bits per
-// group: family + 1, bit 3 = in LDS; see sig_group), so the per-record family dispatch
-// folds away; SIG == 0 reads them from the plan.
+// group: family + 1, bit 3 = in LDS; see tier1_signature), so the per-record family
+// dispatch folds away; SIG == 0 reads them from the plan.
 template <int NG, uint32_t SIG>
 struct DenseGroups {
-  uint32_t fam[NG], base[NG], lbase[NG], nsub[NG], keyed[NG];
+  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
   bool inl[NG];
   bool any_flags;
   bool any_spilled;  // some group's bins are outside LDS
-  __device__ __forceinline__ DenseGroups(const Plan &p) {
+  __device__ __forceinline__ DenseGroups(const Plan &p, uint32_t L) {
     any_flags = false;
     any_spilled = false;
 #pragma unroll
@@ -666,55 +711,91 @@ struct DenseGroups {
         inl[g] = (SIG >> (4 * g + 3)) & 1u;
       } else {
         fam[g] = g < p.ngroups ? p.g[g].family : (uint32_t)FAM_COUNT;
-        inl[g] = p.g[g].lds_nbins != 0;
+        inl[g] = p.g[g].dense_base + p.g[g].nbins <= L;
       }
       base[g] = (uint32_t)p.g[g].dense_base;
-      lbase[g] = p.g[g].lds_base;
       nsub[g] = p.g[g].nsub;
       keyed[g] = p.g[g].key_mode;
       any_flags |= fam[g] == FAM_TCPFLAGS;
       any_spilled |= fam[g] != FAM_COUNT && !inl[g];
     }
   }
-  // does record r update some spilled group?
-  __device__ __forceinline__ bool hits_spilled(const Rec &r) const {
-    bool h = false;
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-      if (fam[g] != FAM_COUNT && !inl[g]) h |= fam_hit(fam[g], r.verdict, r.flagmask);
-    return h;
-  }
 };
 
-// R records of one thread through the groups (tier-1).  Group-outer / record-inner: a
-// group's 2R returning LDS adds are all issued before any result is inspected, so their
-// latency overlaps.  ks / kd: source / destination key, `none` when the side is no pod.
-// kMode 0: every group, keys are IP positions (only when no group is spilled)
-//       1: LDS groups only, keys are IP positions
-//       2: spilled groups only, keys are slots, whole wave converged (ring flush)
-//       3: spilled groups only, keys are slots, any lanes (per-lane reservation)
-template <int NG, uint32_t SIG, int R, int kMode>
+// Does a record update group f (tier-1 families only: fwd / drop / tcpflags / retrans)?
+__device__ __forceinline__ bool fam_hit(uint32_t f, uint32_t verdict, uint32_t flagmask) {
+  if (f == FAM_TCPFLAGS) return flagmask != 0;
+  return verdict == (f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans);
+}
+
+// Wave-level compaction queue for the records that update a spilled group (one whose
+// bins are not in LDS).  Such records are rare (C2: the 10 % drops), so updating them
+// in place would issue every spill instruction for ~5 active lanes of 64.  Instead each
+// step pushes them into three queue registers (one entry per lane) with ds_permute --
+// LDS crossbar, no LDS memory -- and the spill code runs once per 64 queued records
+// with every lane busy.  Push = ballot + mbcnt + a bijective lane permutation: hits go
+// to queue positions [n, n + hits), misses to the remaining ones, so every lane
+// receives exactly one value.
+struct SpillQ {
+  uint32_t e0, e1, e2;  // queued entries: slots (ss | sd << 16), bytes, meta
+  uint32_t n;           // queued entries (wave-uniform), lanes [0, n)
+  uint32_t r0, r1, r2;  // this push's permuted values (wrap-around part on overflow)
+  // push; returns true when the queue holds 64 entries (caller flushes, then next())
+  __device__ __forceinline__ bool push(bool v, uint32_t lane, uint32_t a0, uint32_t a1, uint32_t a2) {
+    const uint64_t m = __ballot(v);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const uint32_t pos = v ? n + below : n + cnt + (lane - below);
+    const int addr = (int)((pos & 63u) << 2);
+    r0 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a0);
+    r1 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a1);
+    r2 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a2);
+    const bool got = lane >= n && lane < n + cnt;
+    e0 = got ? r0 : e0;
+    e1 = got ? r1 : e1;
+    e2 = got ? r2 : e2;
+    n += cnt;
+    return n >= 64;
+  }
+  // after flushing a full queue: the wrapped entries become the queue
+  __device__ __forceinline__ void next() { e0 = r0; e1 = r1; e2 = r2; n -= 64; }
+};
+
+// R records of one thread through every group (tier-1).  Group-outer / record-inner:
+// a group's 2R returning LDS adds are all issued before any result is inspected, so
+// their latency overlaps.  ss/sd: source / destination slot or kIplNoSlot.
+// kMode: 0 every group; 1 LDS groups only (spilled ones go through SpillQ); 2 spilled
+// groups only (the SpillQ flush).
+template <int NG, uint32_t SIG, int R, int kMode = 0>
 __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const L4Ctx &l4,
-                                           const DenseSink &ds, const Rec (&rec)[R],
-                                           const uint32_t (&ks)[R], const uint32_t (&kd)[R], uint32_t none) {
+                                           const DenseSink &ds, const uint32_t (&nbytes)[R],
+                                           const uint32_t (&meta)[R], const uint32_t (&ss)[R],
+                                           const uint32_t (&sd)[R]) {
+  uint32_t verdict[R], reason[R], flagmask[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    verdict[k] = meta_verdict(meta[k]);
+    reason[k] = meta_reason(meta[k]);
+    flagmask[k] = (G.any_flags && verdict[k] == kVerdictForwarded && meta_proto(meta[k]) == 6)
+                      ? flag_label_mask(meta_flags(meta[k])) : 0u;
+  }
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const uint32_t f = G.fam[g];
     if (f == FAM_COUNT) continue;
-    if ((kMode == 1 && !G.inl[g]) || (kMode >= 2 && G.inl[g])) continue;
-    const uint32_t b0 = G.inl[g] ? G.lbase[g] : G.base[g];
+    if ((kMode == 1 && !G.inl[g]) || (kMode == 2 && G.inl[g])) continue;
     uint32_t rd[R], rs[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {  // keys < 2^16, nsub <= 64: 24-bit multiplies
-      const uint32_t xd = G.keyed[g] ? kd[k] : 0u, xs = G.keyed[g] ? ks[k] : 0u;
-      rd[k] = b0 + mul_u24(xd * 2u, G.nsub[g]);       // side 0: ingress (dst)
-      rs[k] = b0 + mul_u24(xs * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
+    for (int k = 0; k < R; ++k) {  // slots < 2^16, nsub <= 64: 24-bit multiplies
+      const uint32_t kd = G.keyed[g] ? sd[k] : 0u, ks = G.keyed[g] ? ss[k] : 0u;
+      rd[k] = G.base[g] + mul_u24(kd * 2u, G.nsub[g]);       // side 0: ingress (dst)
+      rs[k] = G.base[g] + mul_u24(ks * 2u + 1u, G.nsub[g]);  // side 1: egress (src)
     }
     if (f == FAM_TCPFLAGS) {
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        uint32_t m = rec[k].flagmask;
-        const bool d_ok = kd[k] != none, s_ok = ks[k] != none;
+        uint32_t m = flagmask[k];
+        const bool d_ok = sd[k] != kIplNoSlot, s_ok = ss[k] != kIplNoSlot;
         if (G.inl[g]) {
           while (__ballot(m != 0)) {
             const bool v = m != 0;
@@ -733,15 +814,16 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       }
       continue;
     }
-    const uint32_t want = f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped : kVerdictRetrans;
+    const uint32_t want = f == FAM_FWD ? kVerdictForwarded : f == FAM_DROP ? kVerdictDropped
+                                                                          : kVerdictRetrans;
     bool vd[R], vs[R];
     uint32_t bd[R], bs[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      const bool hit = rec[k].verdict == want;
-      const uint32_t sub = f == FAM_DROP ? rec[k].reason : 0u;
-      vd[k] = hit & (kd[k] != none);  // '&': no short-circuit branches
-      vs[k] = hit & (ks[k] != none);
+      const bool hit = verdict[k] == want;
+      const uint32_t sub = f == FAM_DROP ? reason[k] : 0u;
+      vd[k] = hit & (sd[k] != kIplNoSlot);  // '&': no short-circuit branches
+      vs[k] = hit & (ss[k] != kIplNoSlot);
       bd[k] = rd[k] + sub;
       bs[k] = rs[k] + sub;
     }
@@ -750,22 +832,19 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
         uint32_t od[R], os[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-          const uint32_t add = (1u << kL4CountShift) | (rec[k].nbytes < kL4ByteLimit ? rec[k].nbytes : 0u);
+          const uint32_t add = (1u << kL4CountShift) | (nbytes[k] < kL4ByteLimit ? nbytes[k] : 0u);
           od[k] = atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], add);
           os[k] = atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], add);
         }
         bool need = false;
 #pragma unroll
         for (int k = 0; k < R; ++k)
-        {
-          need |= L4Ctx::fix_needed(vd[k], od[k], rec[k].nbytes);
-          need |= L4Ctx::fix_needed(vs[k], os[k], rec[k].nbytes);
-        }
+          need |= L4Ctx::fix_needed(vd[k], od[k], nbytes[k]) | L4Ctx::fix_needed(vs[k], os[k], nbytes[k]);
         if (__builtin_expect(__ballot(need) != 0, 0)) {  // rare: a carry, a wrap or a jumbo size
 #pragma unroll
           for (int k = 0; k < R; ++k) {
-            l4.fix(vd[k], od[k], rec[k].nbytes, bd[k]);
-            l4.fix(vs[k], os[k], rec[k].nbytes, bs[k]);
+            l4.fix(vd[k], od[k], nbytes[k], bd[k]);
+            l4.fix(vs[k], os[k], nbytes[k], bs[k]);
           }
         }
       } else {
@@ -783,7 +862,7 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       for (int k = 0; k < R; ++k) {
         wd[k] = ds.window(bd[k]);
         ws[k] = ds.window(bs[k]);
-        if (kMode == 2) {  // ring flush: converged wave
+        if (kMode == 2) {  // SpillQ flush: converged wave
           pd[k] = wave_reserve(vd[k], wd[k], ds.ctr, ds.wbits);
           ps[k] = wave_reserve(vs[k], ws[k], ds.ctr, ds.wbits);
         } else {
@@ -793,14 +872,14 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        const uint32_t add_b = f <= FAM_DROP ? rec[k].nbytes : 0u;
+        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
         if (vd[k]) ds.spill_put(bd[k], wd[k], pd[k], add_b);
         if (vs[k]) ds.spill_put(bs[k], ws[k], ps[k], add_b);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        const uint32_t add_b = f <= FAM_DROP ? rec[k].nbytes : 0u;
+        const uint32_t add_b = f <= FAM_DROP ? nbytes[k] : 0u;
         if (vd[k]) ds.spill_add(bd[k], add_b);
         if (vs[k]) ds.spill_add(bs[k], add_b);
       }
@@ -808,39 +887,31 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
   }
 }
 
-constexpr uint32_t kRing = 128;  // ring entries per wave (uint2: positions, packed record)
-
 template <int NG, bool kVec, uint32_t SIG>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t nb = a.ipl_nb, P = 2u * nb;
+  const uint32_t nb = a.ipl_nb;
   const uint32_t *keys = (const uint32_t *)smem;
-  const uint32_t kbytes = ipl_vals_offset(nb);  // the key array, 16-byte padded
-  const uint16_t *gvals = (const uint16_t *)(a.ipl + kbytes);  // HBM: position -> slot
-  uint32_t *bins = (uint32_t *)(smem + kbytes);
-  const uint32_t L4 = a.lds_bins;  // even (host)
-  unsigned int *ctr = bins + L4 + 64;
-  for (uint32_t i = threadIdx.x; i < kbytes / 16; i += blockDim.x) ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
+  const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+  uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
+  const uint32_t L4 = a.lds_bins;
+  for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
+    ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
   for (uint32_t i = threadIdx.x; i < L4 + 64 + kMaxSpillWindows; i += blockDim.x) bins[i] = 0u;
   __syncthreads();
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const L4Ctx l4{bins, L4 + lane, a.d, a.l4_ovf};
-  const DenseSink ds = make_sink(a, nullptr, 0, ctr);
-  const DenseGroups<NG, SIG> G(a.p);
+  const L4Ctx l4{bins, L4 + lane, a.d};
+  const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
+  const DenseGroups<NG, SIG> G(a.p, L4);
   const uint32_t seed = a.ipl_seed;
-  uint2 *ring = (uint2 *)(ctr + kMaxSpillWindows) + (threadIdx.x >> 6) * kRing;
-  uint32_t head = 0, nq = 0;  // wave-uniform ring state
-  // spill updates of `cnt` queued records from the ring head (lanes >= cnt hold none)
-  auto ring_flush = [&](uint32_t cnt) {
-    const uint2 e = ring[(head + lane) & (kRing - 1)];
-    const bool valid = lane < cnt;
-    const uint32_t ps = e.x & 0xFFFFu, pd = e.x >> 16;
-    const uint32_t ss[1] = {valid && ps != P ? (uint32_t)gvals[ps] : kIplNoSlot};
-    const uint32_t sd[1] = {valid && pd != P ? (uint32_t)gvals[pd] : kIplNoSlot};
-    const Rec r1[1] = {rec_unpack(e.y)};
-    l4_records<NG, SIG, 1, 2>(G, l4, ds, r1, ss, sd, kIplNoSlot);
-    head = (head + cnt) & (kRing - 1);
-    nq -= cnt;
+  SpillQ q{};
+  // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
+  auto q_flush = [&](bool full) {
+    const bool valid = full || lane < q.n;
+    const uint32_t s1[1] = {valid ? (q.e0 & 0xFFFFu) : kIplNoSlot};
+    const uint32_t d1[1] = {valid ? (q.e0 >> 16) : kIplNoSlot};
+    const uint32_t b1[1] = {q.e1}, m1[1] = {q.e2};
+    l4_records<NG, SIG, 1, 2>(G, l4, ds, b1, m1, s1, d1);
   };
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -851,8 +922,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t v0 = start >> 2, vn = (end - start) >> 2, vend = v0 + vn;
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
-    // the loop is wave-uniform (the ring's ballots need every lane present): lanes past
-    // the end load a clamped vector and update nothing
+    // the loop is wave-uniform (SpillQ's cross-lane pushes need every lane present):
+    // lanes past the end load a clamped vector and update nothing
     const uint64_t vwave = v0 + (threadIdx.x & ~63u);
     const uint64_t vlast = vend - 1;  // vn >= 1
     uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
@@ -868,75 +939,82 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t j[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);  // every lane: no branch
+      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
+      uint32_t sl[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) j[k] = act ? j[k] : P;
-      const uint32_t js[4] = {j[0], j[1], j[2], j[3]}, jd[4] = {j[4], j[5], j[6], j[7]};
-      const Rec rec[4] = {rec_of(vb.x, vm.x, G.any_flags), rec_of(vb.y, vm.y, G.any_flags),
-                          rec_of(vb.z, vm.z, G.any_flags), rec_of(vb.w, vm.w, G.any_flags)};
+      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
+      const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
+      const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
       if (!G.any_spilled) {
-        l4_records<NG, SIG, 4, 0>(G, l4, ds, rec, js, jd, P);
+        l4_records<NG, SIG, 4, 0>(G, l4, ds, by, me, ss, sd);
         continue;
       }
-      l4_records<NG, SIG, 4, 1>(G, l4, ds, rec, js, jd, P);
-      // records that update a spilled group -> this wave's LDS ring
-      uint64_t bal[4];
-      uint32_t T = 0;
-      bool big = false;
+      l4_records<NG, SIG, 4, 1>(G, l4, ds, by, me, ss, sd);
+      // records that update a spilled group -> SpillQ (rolled: one copy of the flush)
+      uint32_t x0 = ss[0] | sd[0] << 16, x1 = ss[1] | sd[1] << 16, x2 = ss[2] | sd[2] << 16,
+               x3 = ss[3] | sd[3] << 16;
+      uint32_t y0 = by[0], y1 = by[1], y2 = by[2], y3 = by[3];
+      uint32_t z0 = me[0], z1 = me[1], z2 = me[2], z3 = me[3];
+#ifdef EXP_UNROLL_PUSH
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
       for (int k = 0; k < 4; ++k) {
-        const bool need = G.hits_spilled(rec[k]) & ((js[k] != P) | (jd[k] != P));
-        bal[k] = __ballot(need);
-        T += (uint32_t)__popcll(bal[k]);
-        big |= need & (rec[k].nbytes >= kRingByteLimit);
-      }
-      if (__builtin_expect(__ballot(big) != 0 || nq + T > kRing, 0)) {
-        // rare: a packet too big for the ring word, or a step that would overflow the
-        // ring: these 4 records' spilled updates directly, slots read from HBM
-        uint32_t ss[4], sd[4];
+        const uint32_t ver = meta_verdict(z0);
+        const uint32_t fm = (G.any_flags && ver == kVerdictForwarded && meta_proto(z0) == 6)
+                                ? flag_label_mask(meta_flags(z0)) : 0u;
+        bool need = false;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool need = (bal[k] >> lane) & 1u;
-          ss[k] = need && js[k] != P ? (uint32_t)gvals[js[k]] : kIplNoSlot;
-          sd[k] = need && jd[k] != P ? (uint32_t)gvals[jd[k]] : kIplNoSlot;
+        for (int g = 0; g < NG; ++g)
+          if (G.fam[g] != FAM_COUNT && !G.inl[g]) need |= fam_hit(G.fam[g], ver, fm);
+        need = need & (x0 != 0xFFFFFFFFu);  // some side is a pod
+        if (q.push(need, lane, x0, y0, z0)) {
+          q_flush(true);
+          q.next();
         }
-        l4_records<NG, SIG, 4, 2>(G, l4, ds, rec, ss, sd, kIplNoSlot);
-        continue;
+        x0 = x1; x1 = x2; x2 = x3;
+        y0 = y1; y1 = y2; y2 = y3;
+        z0 = z1; z1 = z2; z2 = z3;
       }
-      uint32_t pos = head + nq;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
-        if ((bal[k] >> lane) & 1u) ring[(pos + rank) & (kRing - 1)] = make_uint2(js[k] | (jd[k] << 16), rec_pack(rec[k]));
-        pos += (uint32_t)__popcll(bal[k]);
-      }
-      nq += T;
-      while (nq >= 64) ring_flush(64);
     }
     tail = start + (vn << 2);
   }
-  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {  // < 4 records per workgroup
-    const uint32_t js[1] = {ipl_probe_index(keys, nb, seed, a.c.src[i])};
-    const uint32_t jd[1] = {ipl_probe_index(keys, nb, seed, a.c.dst[i])};
-    const Rec rec[1] = {rec_of(a.c.bytes[i], a.c.meta[i], G.any_flags)};
-    if (!G.any_spilled) {
-      l4_records<NG, SIG, 1, 0>(G, l4, ds, rec, js, jd, P);
-      continue;
-    }
-    l4_records<NG, SIG, 1, 1>(G, l4, ds, rec, js, jd, P);
-    const uint32_t ss[1] = {js[0] != P ? (uint32_t)gvals[js[0]] : kIplNoSlot};
-    const uint32_t sd[1] = {jd[0] != P ? (uint32_t)gvals[jd[0]] : kIplNoSlot};
-    l4_records<NG, SIG, 1, 3>(G, l4, ds, rec, ss, sd, kIplNoSlot);
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
+    const uint32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
+    const uint32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
+    const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
+    l4_records<NG, SIG, 1>(G, l4, ds, by, me, ss, sd);
   }
-  if (G.any_spilled && nq) ring_flush(nq);  // wave-uniform
+  if (G.any_spilled && q.n) q_flush(false);
 
   __syncthreads();
-  // staged flush: plain 16-byte stores of this workgroup's bins; stage_reduce_a_kernel
-  // maps positions to slots and sums the copies
-  uint4 *dst = (uint4 *)(a.stage_a + (size_t)blockIdx.x * a.stage_a_stride);
-  for (uint32_t i = threadIdx.x; i < a.stage_a_stride / 4; i += blockDim.x) dst[i] = ((const uint4 *)bins)[i];
-  spill_counts_out(a, ctr);
+  if (a.stage_a) {
+    // staged flush: plain 16-byte stores of this workgroup's bins; stage_reduce_kernel
+    // sums the copies (a global atomic per bin per workgroup costs more)
+    uint4 *dst = (uint4 *)(a.stage_a + (size_t)blockIdx.x * a.stage_a_stride);
+    for (uint32_t i = threadIdx.x; i < a.stage_a_stride / 4; i += blockDim.x) dst[i] = ((const uint4 *)bins)[i];
+  } else {
+    // flush group by group (each LDS group is contiguous): 256-byte contiguous atomics
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (G.fam[g] == FAM_COUNT || !G.inl[g]) continue;
+      const bool with_bytes = G.fam[g] <= FAM_DROP;
+      const uint32_t hi = G.base[g] + a.p.g[g].nbins;
+      for (uint32_t i = G.base[g] + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t w = bins[i];
+        if (!w) continue;
+        if (with_bytes) {
+          atomicAdd(&a.d.cnt[i], (unsigned long long)(w >> kL4CountShift));
+          const uint32_t by = w & kL4BytesMask;
+          if (by) atomicAdd(&a.d.byt[i], (unsigned long long)by);
+        } else {
+          atomicAdd(&a.d.cnt[i], (unsigned long long)w);
+        }
+      }
+    }
+  }
+  spill_counts_out(a, bins + L4 + 64);
 }
 
 // ---- sketch pass (config C3): count-min by window partition, HLL direct -------------
@@ -1155,29 +1233,17 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
 }
 
-// Folds the tier-1 workgroups' staged u32 bins (keyed by IP position) into the slot-keyed
-// dense counters: bin -> (group, position, side, sub) -> slot through the image's value
-// array.  blockIdx.y takes 1/gridDim.y of the copies, so each bin gets gridDim.y global
-// atomics instead of one per workgroup; y == 0 also takes the bin's overflow pair.
+// Sums the tier-1 workgroups' staged u32 bins: blockIdx.y takes 1/gridDim.y of the
+// copies, so each bin gets gridDim.y global atomics instead of one per workgroup.
 __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *stage, uint32_t ncopies,
                                                              uint32_t stride, uint32_t L4, Plan p,
-                                                             DevDense d, const uint16_t *gvals,
-                                                             unsigned long long *ovf) {
+                                                             DevDense d) {
   const uint32_t bin = blockIdx.x * blockDim.x + threadIdx.x;
   if (bin >= L4) return;
-  int gi = -1;
+  bool packed = false;
   for (int g = 0; g < p.ngroups; ++g)
-    if (p.g[g].lds_nbins && bin >= p.g[g].lds_base && bin < p.g[g].lds_base + p.g[g].lds_nbins) gi = g;
-  if (gi < 0) return;  // padding
-  const GroupPlan gp = p.g[gi];
-  const uint32_t local = bin - gp.lds_base, per = 2u * gp.nsub;  // per = 2 or 16
-  uint64_t target = gp.dense_base + local;
-  if (gp.key_mode) {
-    const uint32_t slot = gvals[local >> (31 - __builtin_clz(per))];
-    if (slot == kIplNoSlot) return;  // an empty image position: never updated
-    target = gp.dense_base + (uint64_t)slot * per + (local & (per - 1u));
-  }
-  const bool packed = gp.family <= FAM_DROP;
+    if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
+      packed = p.g[g].family <= FAM_DROP;
   const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * blockIdx.y) / gridDim.y);
   const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (blockIdx.y + 1)) / gridDim.y);
   unsigned long long cnt = 0, byt = 0;
@@ -1187,14 +1253,8 @@ __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *sta
     cnt += packed ? (w >> kL4CountShift) : w;
     byt += packed ? (w & kL4BytesMask) : 0u;
   }
-  if (blockIdx.y == 0 && ovf) {  // exact corrections of the packed adds (L4Ctx::fix)
-    cnt += ovf[2ull * bin];
-    byt += ovf[2ull * bin + 1];
-    ovf[2ull * bin] = 0ULL;
-    ovf[2ull * bin + 1] = 0ULL;
-  }
-  if (cnt) atomicAdd(&d.cnt[target], cnt);
-  if (byt) atomicAdd(&d.byt[target], byt);
+  if (cnt) atomicAdd(&d.cnt[bin], cnt);
+  if (byt) atomicAdd(&d.byt[bin], byt);
 }
 
 // Sums the fold partials of every partition of a window (layout of spill_window_kernel).
@@ -1229,6 +1289,22 @@ __global__ void sparse_init_kernel(unsigned long long *k0, size_t n) {
 
 __global__ void sparse_export_kernel(DevSparse s, size_t cap_slots, unsigned long long *out,
                                      size_t out_cap, unsigned long long *counter) {
+  if (s.compact) {  // (key, count) slots, exported in the wide entry format
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cap_slots;
+         i += (size_t)gridDim.x * blockDim.x) {
+      const unsigned long long key = s.k0[2 * i];
+      if (!key) continue;
+      const unsigned long long pos = atomicAdd(counter, 1ULL);
+      if (pos >= out_cap) continue;
+      unsigned long long *o = out + pos * kSparseEntryWords;
+      o[0] = key & 0xFFFFFFFF00000000ULL;
+      o[1] = 0ULL;
+      o[2] = key & 0xFFFFFFFFULL;
+      o[3] = s.k0[2 * i + 1];
+      o[4] = 0ULL;
+    }
+    return;
+  }
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cap_slots;
        i += (size_t)gridDim.x * blockDim.x) {
     const size_t q = i * kSparseSlotWords;
@@ -1339,7 +1415,7 @@ hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipSt
 static DevSparse dev_sparse(const SparseView &v) {
   return DevSparse{(unsigned long long *)v.k0, (unsigned long long *)v.k1,
                    (unsigned long long *)v.k2, (unsigned long long *)v.cnt,
-                   (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped};
+                   (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped, v.compact};
 }
 
 template <class K>
@@ -1375,10 +1451,10 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_bytes = a.ipl_bytes;
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
-  k.l4_ovf = (unsigned long long *)a.l4_ovf;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  const size_t lds = a.tier1 ? (size_t)a.lds_bytes : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
+  const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
+                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (int)a.dense_ng;
@@ -1439,8 +1515,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
   if (a.stage_a) {
     hipLaunchKernelGGL(stage_reduce_a_kernel, dim3((a.lds_bins + 255) / 256, 8), dim3(256), 0, st,
-                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d,
-                       (const uint16_t *)(a.ipl + ipl_vals_offset(a.ipl_nb)), k.l4_ovf);
+                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (!a.spill) return hipSuccess;
@@ -1460,6 +1535,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
 }
 
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st) {
+  if (v.compact) return hipMemsetAsync(v.k0, 0, slots * 16, st);
   hipLaunchKernelGGL(sparse_init_kernel, dim3(2048), dim3(256), 0, st,
                      (unsigned long long *)v.k0, slots);
   return hipGetLastError();

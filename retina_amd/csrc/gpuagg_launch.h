@@ -16,6 +16,7 @@ struct SparseView {
   uint64_t *k0, *k1, *k2, *cnt, *byt;
   uint32_t mask;
   uint64_t *dropped;
+  uint32_t compact;  // 64-bit keys, 2 words (key, count) per slot at k0
 };
 
 struct LaunchArgs {
@@ -50,8 +51,6 @@ struct LaunchArgs {
   // staged flushes (null: flush with global atomics)
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;
-  uint64_t *l4_ovf;         // tier-1: [2 * lds_bins] exact corrections, zero between launches
-  uint32_t lds_bytes;       // tier-1: dynamic LDS of the launch
   uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
 };
 

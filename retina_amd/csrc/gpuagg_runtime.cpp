@@ -229,8 +229,6 @@ struct gpuagg_ctx {
   // staged flushes: per-workgroup LDS bins (tier-1) and per-partition fold windows
   uint32_t *d_stage_a = nullptr;
   size_t stage_a_alloc = 0;
-  uint64_t *d_l4_ovf = nullptr;  // tier-1 exact-correction pairs per LDS bin
-  size_t l4_ovf_alloc = 0;
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
   // raw perf-record decode (gpuagg_decode.hip)
@@ -403,6 +401,7 @@ int reset_state(gpuagg_ctx *c) {
 
 int ensure_sparse(gpuagg_ctx *c) {
   if (c->sparse_slots) return GPUAGG_OK;
+  // (the compact layout needs 2 of the 8 words per slot; one allocation serves both)
   const uint32_t lg = c->cfg.sparse_capacity_log2 ? c->cfg.sparse_capacity_log2 : 22;
   if (lg < 4 || lg > 30) return fail(c, GPUAGG_EINVAL, "sparse_capacity_log2 %u out of [4,30]", lg);
   const size_t n = (size_t)1 << lg;
@@ -634,45 +633,23 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     return L;
   };
-  a.lds_bins = prefix(kLdsMaxBins);  // u64 slot-keyed LDS bins (dense_local / generic kernels)
-  uint32_t spill_lo = a.lds_bins;    // first dense bin kept in HBM spill lists
-  for (int g = 0; g < c->plan.ngroups; ++g) a.plan.g[g].lds_base = a.plan.g[g].lds_nbins = 0;
-  // tier-1: the LDS image of the IP keys plus u32 bins keyed by IP position (the longest
-  // prefix of dense groups, hottest first, that fits); the remaining dense groups spill
-  // through the per-wave rings.  (With no group in LDS every update spills, but the IP
-  // probes still stay on-chip.)
+  a.lds_bins = prefix(kLdsMaxBins);
+  // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
   a.sig = 0;
-  if (a.dense_ng && c->ipl_bytes) {
-    const uint32_t P = 2u * c->ipl_nb, kbytes = ipl_vals_offset(c->ipl_nb);
-    auto lds_size = [&](int g) { return ((c->plan.g[g].key_mode ? P : 1u) * 2u * c->plan.g[g].nsub + 1u) & ~1u; };
-    auto fit = [&](uint32_t budget_bytes) {  // groups [0, k) fit, L4 bins
-      uint32_t L = 0;
-      int k = 0;
-      for (; k < c->plan.ngroups && (uint64_t)(L + lds_size(k)) * 4 <= budget_bytes; ++k) L += lds_size(k);
-      return std::make_pair(k, L);
-    };
-    const uint32_t base_bytes = kbytes + kL4ExtraBytes;
-    if (base_bytes + kL4RingBytes < kLdsBytes) {
-      auto kl = fit(kLdsBytes - base_bytes);
-      bool ring = false;
-      if (kl.first < c->plan.ngroups) {  // some group spills: make room for the rings
-        kl = fit(kLdsBytes - base_bytes - kL4RingBytes);
-        ring = true;
-      }
+  if (a.dense_ng && c->ipl_bytes && !spans.empty() &&
+      c->ipl_bytes + kL4ExtraBytes < kLdsBytes) {
+    // (with no group in LDS every update spills, but the IP probes still stay on-chip)
+    const uint32_t L4 = prefix((kLdsBytes - c->ipl_bytes - kL4ExtraBytes) / 4);
+    {
       a.tier1 = true;
-      a.lds_bins = kl.second;
-      a.lds_bytes = base_bytes + kl.second * 4 + (ring ? kL4RingBytes : 0u);
-      uint32_t lb = 0;
-      for (int g = 0; g < kl.first; ++g) {
-        a.plan.g[g].lds_base = lb;
-        a.plan.g[g].lds_nbins = lds_size(g);
-        lb += lds_size(g);
-      }
-      spill_lo = kl.first < c->plan.ngroups ? (uint32_t)c->plan.g[kl.first].dense_base : (uint32_t)c->dense_len;
+      a.lds_bins = L4;
+      a.sig = 0;
       if (c->plan.ngroups <= 8) {  // groups in layout order, as the kernel indexes them
         uint32_t sig = 0;
-        for (int g = 0; g < c->plan.ngroups; ++g) sig |= sig_group(c->plan.g[g].family, g < kl.first) << (4 * g);
+        for (int g = 0; g < c->plan.ngroups; ++g)
+          sig |= sig_group(c->plan.g[g].family, c->plan.g[g].dense_base + c->plan.g[g].nbins <= L4)
+                 << (4 * g);
         a.sig = sig;
       }
       a.ipl = c->d_ipl;
@@ -703,22 +680,15 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.nwin = 0;
     a.stage_b = nullptr;
     a.stage_a = nullptr;
-    a.stage_a_stride = 0;
-    a.l4_ovf = nullptr;
     if (a.tier1 && a.lds_bins) {  // per-workgroup copies of the LDS bins, summed after
       a.stage_a_stride = (a.lds_bins + 3u) & ~3u;
       if ((rc = ensure_buf(c, &c->d_stage_a, &c->stage_a_alloc, (size_t)a.blocks * a.stage_a_stride)))
         return rc;
       a.stage_a = c->d_stage_a;
-      if (c->l4_ovf_alloc < 2ull * a.lds_bins) {  // correction pairs: zero, and re-zeroed by the reduce
-        if ((rc = ensure_buf(c, &c->d_l4_ovf, &c->l4_ovf_alloc, 2ull * a.lds_bins))) return rc;
-        HIPCHK(c, hipMemsetAsync(c->d_l4_ovf, 0, c->l4_ovf_alloc * 8, c->stream));
-      }
-      a.l4_ovf = c->d_l4_ovf;
     }
-    if (c->dense_len > spill_lo) {
+    if (c->dense_len > a.lds_bins) {
       // bins past the LDS window: per-workgroup spill lists bucketed by fold window
-      const uint64_t rem = c->dense_len - spill_lo;
+      const uint64_t rem = c->dense_len - a.lds_bins;
       const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
       // overflow falls back to global atomics; a multiple of 4 keeps lists 16-byte aligned
       const uint64_t cap = ((2 * a.chunk / nwin + 4096) + 3) & ~3ULL;
@@ -731,7 +701,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         a.spill = c->d_spill;
         a.spill_count = c->d_spill_count;
         a.nwin = nwin;
-        a.spill_lo = spill_lo;
+        a.spill_lo = a.lds_bins;
         a.win_shift = kFoldWindowShift;
         a.win_blocks = nwin * std::max<uint32_t>(1u, 2u * c->n_cu / nwin);  // one wave of 2 per CU
         // fold partials are stored (not atomically added) and summed by a reduce pass
@@ -873,7 +843,6 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_spill);
   dev_free(c->d_spill_count);
   dev_free(c->d_stage_a);
-  dev_free(c->d_l4_ovf);
   dev_free(c->d_stage_b);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
@@ -1107,6 +1076,14 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
 
   // (re)allocate state: dense counters for the slots in use, zeroed
   if (any_sparse && (rc = ensure_sparse(c))) return rc;
+  // compact group-by keys when every sparse key fits 64 bits: local context whose only
+  // sparse groups are DNS without ip / port options (key = group|side|slot|dns id)
+  bool compact = local && any_sparse;
+  for (size_t g = 0; g < groups.size(); ++g)
+    if (groups[g].sparse)
+      compact &= (groups[g].family == FAM_DNS_REQ || groups[g].family == FAM_DNS_RESP) &&
+                 !(groups[g].src_opts & (OPT_IP | OPT_PORT));
+  c->sv.compact = compact ? 1u : 0u;
   c->inst = inst;
   c->groups = groups;
   c->plan = p;

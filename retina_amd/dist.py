@@ -147,7 +147,10 @@ def merge_engine(engine, group=None, dst: int = 0) -> None:
         reduce(st.hll, st.hll_len, "|u1", dist.ReduceOp.MAX)
     # sparse table: every rank's compact entries gathered on dst and inserted-and-added
     cap = int(st.sparse_len)
-    local = torch.zeros((max(cap, 1), 5), dtype=torch.int64, device=device)
+    local = torch.empty((max(cap, 1), 5), dtype=torch.int64, device=device)
+    # the engine writes on its own stream: nothing of torch's may still be pending on
+    # this memory (a zero-fill racing the export was seen to wipe exported rows)
+    torch.cuda.synchronize(device)
     n = engine.sparse_export(local.data_ptr(), cap) if cap else 0
     torch.cuda.synchronize(device)
     blocks = gather_entries(local.cpu() if on_host else local, n, dst, group)

@@ -250,7 +250,13 @@ class GpuAgg:
 
     @staticmethod
     def device_columns(src_ip, dst_ip, nbytes, meta, ports=None, dns_id=None) -> "_abi.Columns":
-        """Columns from device tensors (torch int32/uint32, contiguous, on this device)."""
+        """Columns from device tensors (torch int32/uint32, contiguous, on this device).
+
+        The engine reads them on its own HIP stream, which does not wait for torch's: the
+        device is synchronised here so every pending write to the tensors has landed."""
+        import torch
+        torch.cuda.synchronize(src_ip.device)
+
         def ptr(t):
             if t is None:
                 return None
@@ -261,12 +267,19 @@ class GpuAgg:
         self._check(self.lib.gpuagg_submit_device(self.h, C.byref(cols), n))
 
     # -- raw perf records (gpuagg_decode.hip) ----------------------------------------
+    def _torch_sync(self) -> None:
+        """Device memory handed over as raw pointers may have torch work pending on it."""
+        import torch
+        torch.cuda.synchronize(self.device)
+
     def decode_device(self, kind: int, raw_ptr: int, n: int, out: "_abi.Columns") -> None:
         """Decode n raw records (device pointer) into device columns, async."""
+        self._torch_sync()
         self._check(self.lib.gpuagg_decode_device(self.h, kind, C.c_void_p(raw_ptr), n, C.byref(out)))
 
     def submit_raw_device(self, kind: int, raw_ptr: int, n: int) -> None:
         """Decode + aggregate n raw records already in this device's HBM, async."""
+        self._torch_sync()
         self._check(self.lib.gpuagg_submit_raw_device(self.h, kind, C.c_void_p(raw_ptr), n))
 
     def submit_raw(self, kind: int, raw: np.ndarray, chunk: int = 1 << 22) -> None:
@@ -372,11 +385,13 @@ class GpuAgg:
         return d
 
     def sparse_export(self, dev_ptr: int, cap: int) -> int:
+        self._torch_sync()
         n = C.c_size_t()
         self._check(self.lib.gpuagg_sparse_export(self.h, C.c_void_p(dev_ptr), cap, C.byref(n)))
         return n.value
 
     def sparse_import(self, dev_ptr: int, n: int) -> None:
+        self._torch_sync()
         self._check(self.lib.gpuagg_sparse_import(self.h, C.c_void_p(dev_ptr), n))
 
     def stats(self) -> Dict[str, float]:
