@@ -10,7 +10,7 @@ import numpy as np
 
 U64 = np.uint64
 M1, M2 = U64(0xff51afd7ed558ccd), U64(0xc4ceb9fe1a85ec53)
-CMS_SEED, CMS_STEP, HLL_SEED = U64(0x5EED5EED5EED5EED), U64(0x9E3779B97F4A7C15), U64(0xA5A5A5A5DEADBEEF)
+CMS_SEED, HLL_SEED = U64(0x5EED5EED5EED5EED), U64(0xA5A5A5A5DEADBEEF)
 
 
 def fmix64(k: np.ndarray) -> np.ndarray:
@@ -24,16 +24,22 @@ def fmix64(k: np.ndarray) -> np.ndarray:
     return k
 
 
+def cms_cols(base: np.ndarray, r: int, width: int) -> np.ndarray:
+    """Row r's column: h1 + r*h2 (double hashing of the 64-bit base; h2 odd)."""
+    h1 = base & U64(0xFFFFFFFF)
+    h2 = (base >> U64(32)) | U64(1)
+    with np.errstate(over="ignore"):
+        return ((h1 + U64(r) * h2) & U64(width - 1)).astype(np.int64)
+
+
 def cms_update(cms: np.ndarray, src, dst, ports, proto) -> None:
     """cms: uint32 [depth, width]; one +1 per record per row."""
     depth, width = cms.shape
     lo = src.astype(U64) | (dst.astype(U64) << U64(32))
     hi = ports.astype(U64) | (proto.astype(U64) << U64(32))
     base = fmix64(lo ^ fmix64(hi ^ CMS_SEED))
-    with np.errstate(over="ignore"):
-        for r in range(depth):
-            col = (fmix64(base + U64(r + 1) * CMS_STEP) & U64(width - 1)).astype(np.int64)
-            cms[r] += np.bincount(col, minlength=width).astype(np.uint32)
+    for r in range(depth):
+        cms[r] += np.bincount(cms_cols(base, r, width), minlength=width).astype(np.uint32)
 
 
 def _bitlen64(w: np.ndarray) -> np.ndarray:
@@ -72,9 +78,7 @@ def cms_estimate(cms: np.ndarray, src, dst, ports, proto) -> np.ndarray:
     hi = np.asarray(ports).astype(U64) | (np.asarray(proto).astype(U64) << U64(32))
     base = fmix64(lo ^ fmix64(hi ^ CMS_SEED))
     est = None
-    with np.errstate(over="ignore"):
-        for r in range(depth):
-            col = (fmix64(base + U64(r + 1) * CMS_STEP) & U64(width - 1)).astype(np.int64)
-            v = cms[r, col].astype(np.int64)
-            est = v if est is None else np.minimum(est, v)
+    for r in range(depth):
+        v = cms[r, cms_cols(base, r, width)].astype(np.int64)
+        est = v if est is None else np.minimum(est, v)
     return est

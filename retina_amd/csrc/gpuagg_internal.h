@@ -242,15 +242,18 @@ constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------
 constexpr uint64_t kCmsSeed = 0x5EED5EED5EED5EEDULL;
-constexpr uint64_t kCmsRowStep = 0x9E3779B97F4A7C15ULL;
 constexpr uint64_t kHllSeed = 0xA5A5A5A5DEADBEEFULL;
 GA_HD uint64_t cms_base(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
   const uint64_t lo = (uint64_t)src | ((uint64_t)dst << 32);
   const uint64_t hi = (uint64_t)ports | ((uint64_t)proto << 32);
   return fmix64(lo ^ fmix64(hi ^ kCmsSeed));
 }
+// Row r's column: double hashing of the 64-bit base (Kirsch & Mitzenmacher, "Less hashing,
+// same performance"): h1 + r*h2 with h1, h2 the base's halves (h2 odd), so a record costs
+// two 64-bit mixes, not one per row.
 GA_HD uint32_t cms_col(uint64_t base, uint32_t row, uint32_t wmask) {
-  return (uint32_t)fmix64(base + (uint64_t)(row + 1) * kCmsRowStep) & wmask;
+  const uint32_t h1 = (uint32_t)base, h2 = (uint32_t)(base >> 32) | 1u;
+  return (h1 + row * h2) & wmask;
 }
 GA_HD uint64_t hll_hash(uint32_t dst) { return fmix64((uint64_t)dst ^ kHllSeed); }
 

@@ -955,11 +955,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
                x3 = ss[3] | sd[3] << 16;
       uint32_t y0 = by[0], y1 = by[1], y2 = by[2], y3 = by[3];
       uint32_t z0 = me[0], z1 = me[1], z2 = me[2], z3 = me[3];
-#ifdef EXP_UNROLL_PUSH
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
       for (int k = 0; k < 4; ++k) {
         const uint32_t ver = meta_verdict(z0);
         const uint32_t fm = (G.any_flags && ver == kVerdictForwarded && meta_proto(z0) == 6)
@@ -1035,17 +1031,26 @@ struct SketchK {
   uint32_t *counts;  // [gridDim.x][nwin]
   uint32_t *hll;
   uint32_t p;
+  // HLL updates bucketed by source-pod window (2^hshift pods, <= 128 KiB of registers):
+  // u32 entries pod-in-window << 24 | register << 6 | rank; hnwin = 0: direct CAS
+  uint32_t hshift, hnwin, hcap;
+  uint32_t *hlists;   // [gridDim.x][hnwin][hcap]
+  uint32_t *hcounts;  // [gridDim.x][hnwin]
+  uint32_t hll_slots; // slots covered by the registers
 };
 
 __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];  // [nwin] list fill counters
-  for (uint32_t i = threadIdx.x; i < k.nwin; i += blockDim.x) wcnt[i] = 0u;
+  // [nwin] count-min list fill counters, then [hnwin] HLL list fill counters
+  extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];
+  uint32_t *hcnt = wcnt + k.nwin;
+  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnwin; i += blockDim.x) wcnt[i] = 0u;
   __syncthreads();
   const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
   const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
   const uint32_t wmask = (1u << k.wlog2) - 1u, hi_bits = k.wlog2 - k.wshift;
   const uint32_t omask = (1u << k.wshift) - 1u;
   uint16_t *mine = k.lists + (size_t)blockIdx.x * k.nwin * k.cap;
+  uint32_t *hmine = k.hlists + (size_t)blockIdx.x * k.hnwin * k.hcap;
   for (uint64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
     const uint32_t s = k.src[i], d = k.dst[i];
     if (k.depth) {
@@ -1064,12 +1069,62 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
     }
     if (k.p) {
       const Lk ls = ip_lookup(k.t, s);
-      if (ls.slot >= 0) hll_update(k.hll, k.p, ls.slot, d);
+      if (ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
+        bool direct = k.hnwin == 0;
+        if (!direct) {
+          const uint64_t h = hll_hash(d);
+          const uint32_t idx = (uint32_t)(h >> (64 - k.p));
+          const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
+          const uint32_t w = (uint32_t)ls.slot >> k.hshift;
+          const uint32_t pos = atomicAdd(&hcnt[w], 1u);
+          direct = pos >= k.hcap;
+          if (!direct)
+            hmine[(size_t)w * k.hcap + pos] = (((uint32_t)ls.slot & ((1u << k.hshift) - 1u)) << 24) | (idx << 6) | rho;
+        }
+        if (direct) hll_update(k.hll, k.p, ls.slot, d);
+      }
     }
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
     k.counts[(size_t)blockIdx.x * k.nwin + w] = wcnt[w] < k.cap ? wcnt[w] : k.cap;
+  for (uint32_t w = threadIdx.x; w < k.hnwin; w += blockDim.x)
+    k.hcounts[(size_t)blockIdx.x * k.hnwin + w] = hcnt[w] < k.hcap ? hcnt[w] : k.hcap;
+}
+
+// Workgroup w folds HLL window w: its pods' registers (<= 128 KiB) are loaded into LDS,
+// every scatter workgroup's list for the window is applied with byte-max (a 32-bit CAS on
+// the register's word; one wave per list), and the registers are stored back -- one
+// coalesced read and write of the register array instead of a random global CAS per record.
+__global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k, uint32_t n_lists) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t regs[];
+  const uint32_t w = blockIdx.x;
+  const uint32_t pod0 = w << k.hshift;
+  const uint32_t npods = min(1u << k.hshift, k.hll_slots - pod0);
+  const size_t bytes = (size_t)npods << k.p;  // multiple of 16 (p >= 4)
+  uint4 *g = (uint4 *)((uint8_t *)k.hll + ((size_t)pod0 << k.p));
+  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) ((uint4 *)regs)[i] = g[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+  const uint32_t imask = (1u << k.p) - 1u;
+  for (uint32_t l = threadIdx.x >> 6; l < n_lists; l += nwaves) {
+    const uint32_t cnt = k.hcounts[(size_t)l * k.hnwin + w];
+    const uint32_t *e = k.hlists + ((size_t)l * k.hnwin + w) * k.hcap;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+      const uint32_t x = e[j];
+      const uint32_t byte = ((x >> 24) << k.p) + ((x >> 6) & imask), rho = x & 63u;
+      uint32_t *word = &regs[byte >> 2];
+      const uint32_t sh = (byte & 3u) * 8u;
+      uint32_t old = *word;
+      while (((old >> sh) & 0xFFu) < rho) {
+        const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rho << sh));
+        if (prev == old) break;
+        old = prev;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) g[i] = ((const uint4 *)regs)[i];
 }
 
 // Workgroup b folds window b % nwin over scatter workgroups [part*L/P, (part+1)*L/P).
@@ -1126,16 +1181,39 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   k.counts = a.counts;
   k.hll = (uint32_t *)a.hll;
   k.p = a.hll_p;
-  hipLaunchKernelGGL(sketch_scatter_kernel, dim3(a.blocks), dim3(1024), (size_t)a.nwin * 4, st, k);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !a.nwin || !a.cms_depth) return e;
-  const size_t lds = (size_t)4 << a.win_shift;
-  if (lds > 64 * 1024 &&
-      (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds)) != hipSuccess)
+  k.hshift = a.hll_shift;
+  k.hnwin = a.hll_nwin;
+  k.hcap = a.hll_cap;
+  k.hlists = a.hll_lists;
+  k.hcounts = a.hll_counts;
+  k.hll_slots = a.hll_slots;
+  const size_t scatter_lds = (size_t)(a.nwin + a.hll_nwin) * 4;
+  hipError_t e;
+  if (scatter_lds > 64 * 1024 &&
+      (e = hipFuncSetAttribute((const void *)sketch_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)scatter_lds)) != hipSuccess)
     return e;
-  hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
-  return hipGetLastError();
+  hipLaunchKernelGGL(sketch_scatter_kernel, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (a.nwin && a.cms_depth) {
+    const size_t lds = (size_t)4 << a.win_shift;
+    if (lds > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (a.hll_nwin && a.hll_p) {
+    const size_t lds = (size_t)1 << (a.hll_p + a.hll_shift);
+    if (lds > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void *)hll_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(hll_fold_kernel, dim3(a.hll_nwin), dim3(1024), lds, st, k, a.blocks);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.

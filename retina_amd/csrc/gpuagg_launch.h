@@ -85,6 +85,9 @@ struct SketchArgs {
   uint32_t fold_blocks;     // multiple of nwin
   uint8_t *hll;
   uint32_t hll_p;
+  uint32_t hll_slots;               // slots covered by the registers
+  uint32_t hll_shift, hll_nwin, hll_cap;  // HLL windows of 2^hll_shift pods; nwin 0: direct CAS
+  uint32_t *hll_lists, *hll_counts;
 };
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
 

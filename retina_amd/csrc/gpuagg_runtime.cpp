@@ -239,6 +239,10 @@ struct gpuagg_ctx {
   size_t sk_lists_alloc = 0;
   uint32_t *d_sk_counts = nullptr;
   size_t sk_counts_alloc = 0;
+  uint32_t *d_hll_lists = nullptr;
+  size_t hll_lists_alloc = 0;
+  uint32_t *d_hll_counts = nullptr;
+  size_t hll_counts_alloc = 0;
   std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch pass start, end
 };
 
@@ -530,6 +534,9 @@ void drain_timing(gpuagg_ctx *c) {
 // Count-min windows: 2^15 columns (128 KiB of LDS in the fold); at most 4096 windows
 // (16 KiB of scatter counters), else every update is a direct global atomic.
 constexpr uint32_t kCmsWindowShift = 15, kCmsMaxWindows = 4096;
+// HLL windows: 2^shift source pods whose registers fit 128 KiB of LDS (entries carry the
+// pod-in-window in 8 bits and the register index in 18, so p <= 17 and shift <= 8)
+constexpr uint32_t kHllWindowLog2Bytes = 17, kHllMaxWindows = 8192;
 
 // The sketch pass over n records: count-min scatter + fold, HLL direct (SketchArgs).
 int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
@@ -545,6 +552,13 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   s.hll_p = c->hll_len ? c->cfg.hll_precision : 0;
   s.blocks = c->n_cu;
   s.win_shift = std::min<uint32_t>(kCmsWindowShift, s.cms_wlog2);
+  s.hll_slots = s.hll_p ? (uint32_t)(c->hll_len >> s.hll_p) : 0;
+  uint64_t hnwin = 0;
+  if (s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
+    s.hll_shift = std::min<uint32_t>(8u, kHllWindowLog2Bytes - s.hll_p);
+    hnwin = ((uint64_t)s.hll_slots + (1u << s.hll_shift) - 1) >> s.hll_shift;
+    if (hnwin > kHllMaxWindows) hnwin = 0;
+  }
   const uint64_t nwin = s.cms_depth ? ((uint64_t)s.cms_depth << (s.cms_wlog2 - s.win_shift)) : 0;
   const uint64_t per_launch = (uint64_t)s.blocks << 20;  // <= 2^20 records per scatter workgroup
   std::array<hipEvent_t, 2> ev{};
@@ -571,6 +585,19 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       s.lists = c->d_sk_lists;
       s.counts = c->d_sk_counts;
       s.fold_blocks = (uint32_t)nwin * std::max<uint32_t>(1u, c->n_cu / (uint32_t)nwin);
+    }
+    s.hll_nwin = 0;
+    if (hnwin) {
+      // at most one entry per record; a uniform spread gives chunk / hnwin per list, +25 %
+      // + 64 of headroom (overflow is exact: it falls back to a global CAS)
+      const uint64_t mean = s.chunk / hnwin;
+      const uint64_t cap = (mean + mean / 4 + 64 + 15) & ~15ULL;
+      if ((rc = ensure_buf(c, &c->d_hll_lists, &c->hll_lists_alloc, (size_t)s.blocks * hnwin * cap))) return rc;
+      if ((rc = ensure_buf(c, &c->d_hll_counts, &c->hll_counts_alloc, (size_t)s.blocks * hnwin))) return rc;
+      s.hll_nwin = (uint32_t)hnwin;
+      s.hll_cap = (uint32_t)cap;
+      s.hll_lists = c->d_hll_lists;
+      s.hll_counts = c->d_hll_counts;
     }
     HIPCHK(c, launch_sketch(s, c->stream));
   }
@@ -846,6 +873,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_stage_b);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
+  dev_free(c->d_hll_lists);
+  dev_free(c->d_hll_counts);
   dev_free(c->d_decode_oor);
   for (auto &st : c->stg) {
     for (auto &p : st.cols) dev_free(p);

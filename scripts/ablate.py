@@ -10,6 +10,7 @@ prints one JSON line per variant with the HIP-event time per launch:
   c4-zipf   C2 spec on C4's Zipf(1.2) records (LDS atomic contention)
   *-hbm-ip-table  same with FLAG_NO_LDS_IP_TABLE (IP table in HBM, u64 LDS bins)
   remote    C1 remote spec (sparse table)
+  c5*       C5 batch (100k pods) with the C5 spec, and with each of its metrics alone
   raw-packet  decode of 72-byte packetparser records (C2 columns re-encoded) + C2 forward
               aggregation; decode_ms is the decode kernel, 92 B/record of HBM traffic
 """
@@ -79,6 +80,20 @@ def main():
         run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
         del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+    if not ONLY or any(v.startswith("c5") for v in ONLY):  # C5 spec split by metric
+        del cols
+        c5 = W.CONFIGS["c5"]
+        p5 = W.make_pods(c5["pods"], seed=c5["seed"])
+        n5 = c5["records"]
+        cols5, _ = gen_device_records(n5, p5, c5["seed"], dev, dict(c5["gen"]))
+        spec = W.C5_SPEC
+        run("c5", spec, p5, cols5, n5)
+        run("c5-flags", spec[:1], p5, cols5, n5)
+        run("c5-retrans", spec[1:2], p5, cols5, n5)
+        run("c5-dns", spec[2:], p5, cols5, n5)
+        run("c5-dense", spec[:2], p5, cols5, n5)
+        run("c5-none", [], p5, cols5, n5)
+        return
     if not ONLY or "raw-packet" in ONLY:
         run_raw(pods, cols, n)
 
