@@ -1039,22 +1039,20 @@ struct SketchK {
   uint32_t hll_slots; // slots covered by the registers
 };
 
-__global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
-  // [nwin] count-min list fill counters, then [hnwin] HLL list fill counters
-  extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];
-  uint32_t *hcnt = wcnt + k.nwin;
-  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnwin; i += blockDim.x) wcnt[i] = 0u;
-  __syncthreads();
-  const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
-  const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
-  const uint32_t wmask = (1u << k.wlog2) - 1u, hi_bits = k.wlog2 - k.wshift;
-  const uint32_t omask = (1u << k.wshift) - 1u;
-  uint16_t *mine = k.lists + (size_t)blockIdx.x * k.nwin * k.cap;
-  uint32_t *hmine = k.hlists + (size_t)blockIdx.x * k.hnwin * k.hcap;
-  for (uint64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-    const uint32_t s = k.src[i], d = k.dst[i];
+// One record's sketch updates: each count-min row's column is appended to the list of
+// its window (row, column >> wshift) and each HLL (pod, register, rank) to the list of
+// its pod window; a full list falls back to the global atomic (exact, slow).
+struct SketchLists {
+  const SketchK &k;
+  uint32_t *wcnt, *hcnt;
+  uint16_t *mine;
+  uint32_t *hmine;
+  uint32_t wmask, hi_bits, omask;
+  __device__ __forceinline__ void record(uint32_t s, uint32_t d, uint32_t ports, uint32_t meta,
+                                         const Lk &ls) const {
     if (k.depth) {
-      const uint64_t base = cms_base(s, d, k.ports[i], meta_proto(k.meta[i]));
+      const uint64_t base = cms_base(s, d, ports, meta_proto(meta));
+#pragma unroll 4
       for (uint32_t r = 0; r < k.depth; ++r) {
         const uint32_t col = cms_col(base, r, wmask);
         bool direct = k.nwin == 0;
@@ -1067,23 +1065,70 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
         if (direct) atomicAdd(&k.cms[((size_t)r << k.wlog2) + col], 1u);
       }
     }
-    if (k.p) {
-      const Lk ls = ip_lookup(k.t, s);
-      if (ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
-        bool direct = k.hnwin == 0;
-        if (!direct) {
-          const uint64_t h = hll_hash(d);
-          const uint32_t idx = (uint32_t)(h >> (64 - k.p));
-          const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
-          const uint32_t w = (uint32_t)ls.slot >> k.hshift;
-          const uint32_t pos = atomicAdd(&hcnt[w], 1u);
-          direct = pos >= k.hcap;
-          if (!direct)
-            hmine[(size_t)w * k.hcap + pos] = (((uint32_t)ls.slot & ((1u << k.hshift) - 1u)) << 24) | (idx << 6) | rho;
-        }
-        if (direct) hll_update(k.hll, k.p, ls.slot, d);
+    if (k.p && ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
+      bool direct = k.hnwin == 0;
+      if (!direct) {
+        const uint64_t h = hll_hash(d);
+        const uint32_t idx = (uint32_t)(h >> (64 - k.p));
+        const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
+        const uint32_t w = (uint32_t)ls.slot >> k.hshift;
+        const uint32_t pos = atomicAdd(&hcnt[w], 1u);
+        direct = pos >= k.hcap;
+        if (!direct)
+          hmine[(size_t)w * k.hcap + pos] = (((uint32_t)ls.slot & ((1u << k.hshift) - 1u)) << 24) | (idx << 6) | rho;
       }
+      if (direct) hll_update(k.hll, k.p, ls.slot, d);
     }
+  }
+};
+
+// Sketch pass over the records.  kVec: 4 consecutive records per lane per step (16-byte
+// loads per column) and the 8 IP-table probes of their 4 sources issued back to back, so
+// a wave keeps ~12 loads in flight instead of waiting on one record's probe at a time.
+template <bool kVec>
+__global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
+  // [nwin] count-min list fill counters, then [hnwin] HLL list fill counters
+  extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];
+  uint32_t *hcnt = wcnt + k.nwin;
+  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnwin; i += blockDim.x) wcnt[i] = 0u;
+  __syncthreads();
+  const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
+  const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
+  const SketchLists L{k, wcnt, hcnt, k.lists + (size_t)blockIdx.x * k.nwin * k.cap,
+                      k.hlists + (size_t)blockIdx.x * k.hnwin * k.hcap, (1u << k.wlog2) - 1u,
+                      k.wlog2 - k.wshift, (1u << k.wshift) - 1u};
+  const bool need_ports = k.depth != 0 && k.ports;
+  const Lk none{-1, 0};
+  uint64_t tail = start;
+  if (kVec && start + 4 <= end) {
+    const uint64_t v0 = start >> 2, vend = v0 + ((end - start) >> 2);
+    const uint4 *s4 = (const uint4 *)k.src, *d4 = (const uint4 *)k.dst;
+    const uint4 *p4 = (const uint4 *)k.ports, *m4 = (const uint4 *)k.meta;
+    for (uint64_t v = v0 + threadIdx.x; v < vend; v += blockDim.x) {
+      const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
+      const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
+      Lk ls[4] = {none, none, none, none};
+      if (k.p) {
+        const uint32_t ip[4] = {vs.x, vs.y, vs.z, vs.w};
+        uint64_t e1[4], e2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          e1[j] = k.t.slots[ip_h1(ip[j], k.t.seed) & k.t.mask];
+          e2[j] = k.t.slots[ip_h2(ip[j], k.t.seed) & k.t.mask];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ls[j] = ip_pick(ip[j], e1[j], e2[j]);
+      }
+      L.record(vs.x, vd.x, vp.x, vm.x, ls[0]);
+      L.record(vs.y, vd.y, vp.y, vm.y, ls[1]);
+      L.record(vs.z, vd.z, vp.z, vm.z, ls[2]);
+      L.record(vs.w, vd.w, vp.w, vm.w, ls[3]);
+    }
+    tail = start + ((end - start) & ~3ULL);
+  }
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
+    const uint32_t s = k.src[i];
+    L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i], k.p ? ip_lookup(k.t, s) : none);
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
@@ -1188,12 +1233,18 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   k.hcounts = a.hll_counts;
   k.hll_slots = a.hll_slots;
   const size_t scatter_lds = (size_t)(a.nwin + a.hll_nwin) * 4;
+  // 16-byte loads need aligned columns and workgroup chunks of whole vectors
+  const bool vec = a.chunk % 4 == 0 && ((uintptr_t)k.src | (uintptr_t)k.dst | (uintptr_t)k.meta |
+                                        (uintptr_t)(k.ports ? k.ports : k.src)) % 16 == 0;
+  const void *fn = vec ? (const void *)sketch_scatter_kernel<true> : (const void *)sketch_scatter_kernel<false>;
   hipError_t e;
   if (scatter_lds > 64 * 1024 &&
-      (e = hipFuncSetAttribute((const void *)sketch_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)scatter_lds)) != hipSuccess)
+      (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scatter_lds)) != hipSuccess)
     return e;
-  hipLaunchKernelGGL(sketch_scatter_kernel, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  if (vec)
+    hipLaunchKernelGGL(sketch_scatter_kernel<true>, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  else
+    hipLaunchKernelGGL(sketch_scatter_kernel<false>, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (a.nwin && a.cms_depth) {
     const size_t lds = (size_t)4 << a.win_shift;

@@ -554,7 +554,8 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   s.win_shift = std::min<uint32_t>(kCmsWindowShift, s.cms_wlog2);
   s.hll_slots = s.hll_p ? (uint32_t)(c->hll_len >> s.hll_p) : 0;
   uint64_t hnwin = 0;
-  if (s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
+  const bool direct = c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH;
+  if (!direct && s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
     s.hll_shift = std::min<uint32_t>(8u, kHllWindowLog2Bytes - s.hll_p);
     hnwin = ((uint64_t)s.hll_slots + (1u << s.hll_shift) - 1) >> s.hll_shift;
     if (hnwin > kHllMaxWindows) hnwin = 0;
@@ -571,9 +572,9 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     s.cols = ColsView{cv.src_ip + off, cv.dst_ip + off, nullptr, cv.meta + off,
                       cv.ports ? cv.ports + off : nullptr, nullptr};
     s.n = m;
-    s.chunk = (m + s.blocks - 1) / s.blocks;
+    s.chunk = ((m + s.blocks - 1) / s.blocks + 3) & ~3ULL;  // whole 4-record vectors
     s.nwin = 0;
-    if (nwin && nwin <= kCmsMaxWindows) {
+    if (!direct && nwin && nwin <= kCmsMaxWindows) {
       // expected entries per list = chunk * depth / nwin; +12.5 % + 2048 of headroom
       // (overflow is exact but slow: it falls back to a global atomic)
       const uint64_t mean = s.chunk * s.cms_depth / nwin;

@@ -36,11 +36,11 @@ DROP = W.LOCAL_FWD_DROP[2:]
 ONLY = set(filter(None, os.environ.get("ABLATE_ONLY", "").split(",")))
 
 
-def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0):
+def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, **kw):
     if ONLY and name not in ONLY:
         return
     g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
-               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags)
+               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags, **kw)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     dc = GpuAgg.device_columns(*cols)
@@ -56,8 +56,11 @@ def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0):
     g.close()
     ms = st["kernel_ms"] / max(1, st["kernel_launches"])
     fold = st["fold_ms"] / max(1, st["kernel_launches"])
-    print(json.dumps({"lib": os.path.basename(os.environ.get("GPUAGG_LIB", "")), "variant": name, "records": n, "launch_ms": ms, "fold_ms": fold, "wall_ms": wall * 1e3,
-                      "grec_s": n / ms / 1e6, "hbm_frac_16B": 16 * n / (ms * 1e-3) / 8e12}), flush=True)
+    sk = st["sketch_ms"] / max(1, st["sketch_launches"])
+    print(json.dumps({"lib": os.path.basename(os.environ.get("GPUAGG_LIB", "")), "variant": name, "records": n,
+                      "launch_ms": ms, "fold_ms": fold, "sketch_ms": sk, "wall_ms": wall * 1e3,
+                      "grec_s": n / max(ms, 1e-9) / 1e6, "hbm_frac_16B": 16 * n / (max(ms, 1e-9) * 1e-3) / 8e12}),
+          flush=True)
 
 
 def main():
@@ -80,6 +83,19 @@ def main():
         run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
         del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+    if not ONLY or any(v.startswith("c3") for v in ONLY):  # C3 sketch pass split by sketch
+        del cols
+        c3 = W.CONFIGS["c3"]
+        n3 = 1 << 27
+        cols3, _ = gen_device_records(n3, pods, c3["seed"], dev, dict(c3["gen"]))
+        cms = dict(cms_depth=4, cms_width_log2=20)
+        run("c3-none", W.LOCAL_FWD_DROP, pods, cols3, n3)
+        run("c3", W.LOCAL_FWD_DROP, pods, cols3, n3, **cms, hll_precision=14)
+        run("c3-cms", W.LOCAL_FWD_DROP, pods, cols3, n3, **cms)
+        run("c3-cms-direct", W.LOCAL_FWD_DROP, pods, cols3, n3, flags=2, **cms)
+        run("c3-hll", W.LOCAL_FWD_DROP, pods, cols3, n3, hll_precision=14)
+        run("c3-hll-direct", W.LOCAL_FWD_DROP, pods, cols3, n3, flags=2, hll_precision=14)
+        return
     if not ONLY or any(v.startswith("c5") for v in ONLY):  # C5 spec split by metric
         del cols
         c5 = W.CONFIGS["c5"]

@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, bench lines, rocprofv3 summaries, PMC passes.
 #   bash scripts/gpu_check.sh TAG STEP...
 # STEP: build | tests[:PYTEST_ARGS] | smoke | bench:CFG | prof:CFG | pmc:CFG | micro | microlds
-#       (CFG = c1..c5, default c2; tests:k=EXPR runs `-k EXPR`)
+#       (CFG = c1..c5, default c2; tests:k=A,B runs `-k "A or B"`)
 # Every GPU step has its own time limit; a crash, abort or timeout stops the script.
 TAG=${1:-run}
 shift
@@ -24,7 +24,8 @@ for s in $STEPS; do
       python -c "import __graft_entry__ as g; g.build()" > "$OUT/${TAG}_build.log" 2>&1 || exit 1 ;;
     tests)
       sel=()
-      [ -n "$arg" ] && sel=(-k "${arg#k=}")
+      # k=a,b,c selects tests matching any of a, b, c (steps are split on whitespace)
+      [ -n "$arg" ] && { k=${arg#k=}; sel=(-k "${k//,/ or }"); }
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${sel[@]}" \
         > "$OUT/${TAG}_pytest.log" 2>&1
       rc=$?; echo "pytest rc=$rc" >> "$OUT/${TAG}_pytest.log"
