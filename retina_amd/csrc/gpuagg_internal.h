@@ -238,6 +238,8 @@ GA_HD uint64_t key_hash(uint64_t k0, uint64_t k1, uint64_t k2) {
   return fmix64(k0 ^ fmix64(k1 ^ fmix64(k2 ^ 0x243F6A8885A308D3ULL)));
 }
 constexpr uint32_t kSparseMaxProbe = 1u << 16;
+// compact table segments: 2^13 (key, count) slots = 128 KiB, folded in LDS
+constexpr uint32_t kSparseSegLog2 = 13, kSparseMaxSegLists = 4096;
 constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------

@@ -41,6 +41,12 @@ struct DevSparse {
   uint32_t mask;
   unsigned long long *dropped;
   uint32_t compact;  // 64-bit keys (see sparse_add_compact), 2 words per slot at k0
+  uint32_t seg_log2; // compact: probes stay in the key's 2^seg_log2-slot segment
+  // compact keys bucketed per segment (aggregate_kernel sets this workgroup's lists and
+  // the LDS fill counters; null: sparse_insert adds in place)
+  unsigned long long *lists;
+  uint32_t *lctr;
+  uint32_t lcap;
 };
 struct DevSketch {
   uint32_t *cms;
@@ -74,6 +80,10 @@ struct KArgs {
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
+  // compact group-by keys bucketed per table segment (generic kernel), or null
+  unsigned long long *sp_lists;
+  uint32_t *sp_counts;
+  uint32_t sp_nwin, sp_cap;
   Plan p;
 };
 
@@ -105,16 +115,20 @@ __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
 // sparse groups are DNS -- k1 == 0 and k2 = dns id, so key = k0 | dns id): one 16-byte
 // slot (key, count) per entry; the claiming CAS publishes the whole key, so an insert is
 // one CAS and one add and a key never occupies two slots.
+// Linear probing wraps inside the key's segment of 2^seg_log2 slots, so one segment
+// (128 KiB) can be folded in LDS (sparse_fold_kernel) with the same probe sequence.
+__device__ __forceinline__ uint32_t compact_home(const DevSparse &s, uint64_t key) {
+  return (uint32_t)fmix64(key ^ 0x243F6A8885A308D3ULL) & s.mask;
+}
 __device__ __forceinline__ void sparse_add_compact(const DevSparse &s, uint64_t key, uint64_t c) {
-  uint32_t h = (uint32_t)fmix64(key ^ 0x243F6A8885A308D3ULL) & s.mask;
-  for (uint32_t probe = 0; probe < kSparseMaxProbe; ++probe) {
-    unsigned long long *slot = s.k0 + 2ull * h;
+  const uint32_t h = compact_home(s, key), smask = (1u << s.seg_log2) - 1u, seg = h & ~smask;
+  for (uint32_t probe = 0; probe <= smask; ++probe) {
+    unsigned long long *slot = s.k0 + 2ull * (seg | ((h + probe) & smask));
     const unsigned long long cur = atomicCAS(&slot[0], 0ULL, (unsigned long long)key);
     if (cur == 0ULL || cur == key) {
       atomicAdd(&slot[1], (unsigned long long)c);
       return;
     }
-    h = (h + 1) & s.mask;
   }
   atomicAdd(s.dropped, 1ULL);
 }
@@ -305,6 +319,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
 // `valid` is false on lanes with nothing to insert.
 __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, uint64_t k0, uint64_t k1,
                                               uint64_t k2, uint64_t b) {
+  if (s.lists) {  // compact keys: append to the segment's list (LDS fill counter)
+    if (!valid) return;
+    const uint64_t key = k0 | (k2 & 0xFFFFFFFFULL);
+    const uint32_t w = compact_home(s, key) >> s.seg_log2;
+    const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
+    if (pos < s.lcap) s.lists[(size_t)w * s.lcap + pos] = key;
+    else sparse_add_compact(s, key, 1);  // full list: in place (exact)
+    return;
+  }
   const uint64_t vm = __ballot(valid);
   if (!vm) return;
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -547,14 +570,61 @@ __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds)
 template <bool kVec, bool kSketch>
 __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
-  const DenseSink ds = dense_sink_init(a, lds);
+  // LDS: dense bins + extras, then the segment-list fill counters
+  uint32_t *sctr = (uint32_t *)&lds[a.lds_bins + kLdsExtraWords];
+  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) sctr[i] = 0u;
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr too)
+  DevSparse s = a.s;
+  if (a.sp_lists) {
+    s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap;
+    s.lctr = sctr;
+    s.lcap = a.sp_cap;
+  }
   for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
                         [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports,
                             uint32_t dns, const Lk &ls, const Lk &ld, bool act) {
-                          apply_groups(a.p, ds, a.s, sip, dip, nb, meta, ports, dns, ls, ld);
+                          apply_groups(a.p, ds, s, sip, dip, nb, meta, ports, dns, ls, ld);
                           if (kSketch && act) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
                         });
-  dense_flush(a, ds);
+  dense_flush(a, ds);  // (starts with a barrier)
+  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
+    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+}
+
+// Workgroup w folds table segment w: its 2^seg_log2 (key, count) slots are loaded into
+// LDS, every aggregation workgroup's list of keys for the segment is inserted with LDS
+// 64-bit CAS + add (the probe sequence of sparse_add_compact), and the segment is
+// stored back -- coalesced segment traffic instead of two memory-side atomics per key.
+__global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const unsigned long long *lists,
+                                                           const uint32_t *counts, uint32_t n_lists,
+                                                           uint32_t nwin, uint32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long seg[];
+  const uint32_t w = blockIdx.x, nslot = 1u << s.seg_log2, smask = nslot - 1u;
+  ulonglong2 *g = (ulonglong2 *)(s.k0 + 2ull * ((size_t)w << s.seg_log2));
+  for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) ((ulonglong2 *)seg)[i] = g[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+  for (uint32_t l = threadIdx.x >> 6; l < n_lists; l += nwaves) {
+    const uint32_t cnt = counts[(size_t)l * nwin + w];
+    const unsigned long long *e = lists + ((size_t)l * nwin + w) * cap;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+      const unsigned long long key = e[j];
+      const uint32_t h = compact_home(s, key);
+      bool done = false;
+      for (uint32_t probe = 0; probe <= smask; ++probe) {
+        const uint32_t i = (h + probe) & smask;
+        const unsigned long long cur = atomicCAS(&seg[2 * i], 0ULL, key);
+        if (cur == 0ULL || cur == key) {
+          atomicAdd(&seg[2 * i + 1], 1ULL);
+          done = true;
+          break;
+        }
+      }
+      if (!done) atomicAdd(s.dropped, 1ULL);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) g[i] = ((const ulonglong2 *)seg)[i];
 }
 
 // Dense local-context fast path: every group is endpoint-keyed (forward / drop /
@@ -1255,7 +1325,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  if (a.hll_nwin && a.hll_p) {
+  if (a.hll_nwin && a.hll_p && !getenv("GPUAGG_EXP_HSHIFT")) {
     const size_t lds = (size_t)1 << (a.hll_p + a.hll_shift);
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)hll_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1544,7 +1614,8 @@ hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipSt
 static DevSparse dev_sparse(const SparseView &v) {
   return DevSparse{(unsigned long long *)v.k0, (unsigned long long *)v.k1,
                    (unsigned long long *)v.k2, (unsigned long long *)v.cnt,
-                   (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped, v.compact};
+                   (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped, v.compact,
+                   v.seg_log2, nullptr, nullptr, 0u};
 }
 
 template <class K>
@@ -1580,10 +1651,14 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_bytes = a.ipl_bytes;
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
+  k.sp_lists = (unsigned long long *)a.sp_lists;
+  k.sp_counts = a.sp_counts;
+  k.sp_nwin = a.sp_lists ? a.sp_nwin : 0u;
+  k.sp_cap = a.sp_cap;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
-                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8;
+                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (int)a.dense_ng;
@@ -1645,6 +1720,15 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (a.stage_a) {
     hipLaunchKernelGGL(stage_reduce_a_kernel, dim3((a.lds_bins + 255) / 256, 8), dim3(256), 0, st,
                        a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (a.sp_lists) {
+    const size_t seg_lds = (size_t)16 << a.sparse.seg_log2;
+    if ((e = hipFuncSetAttribute((const void *)sparse_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)seg_lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(sparse_fold_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, k.s,
+                       (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (!a.spill) return hipSuccess;

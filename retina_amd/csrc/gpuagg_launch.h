@@ -17,6 +17,7 @@ struct SparseView {
   uint32_t mask;
   uint64_t *dropped;
   uint32_t compact;  // 64-bit keys, 2 words (key, count) per slot at k0
+  uint32_t seg_log2; // compact: a key probes only its 2^seg_log2-slot segment
 };
 
 struct LaunchArgs {
@@ -52,6 +53,10 @@ struct LaunchArgs {
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;
   uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
+  // compact group-by keys bucketed per table segment (null: inserted in place)
+  uint64_t *sp_lists;       // [blocks][sp_nwin][sp_cap] keys
+  uint32_t *sp_counts;      // [blocks][sp_nwin]
+  uint32_t sp_nwin, sp_cap;
 };
 
 // Raw perf-record decode (gpuagg_decode.hip); kinds match GPUAGG_RAW_* of gpuagg.h.

@@ -239,6 +239,10 @@ struct gpuagg_ctx {
   size_t sk_lists_alloc = 0;
   uint32_t *d_sk_counts = nullptr;
   size_t sk_counts_alloc = 0;
+  uint64_t *d_sp_lists = nullptr;
+  size_t sp_lists_alloc = 0;
+  uint32_t *d_sp_counts = nullptr;
+  size_t sp_counts_alloc = 0;
   uint32_t *d_hll_lists = nullptr;
   size_t hll_lists_alloc = 0;
   uint32_t *d_hll_counts = nullptr;
@@ -419,6 +423,7 @@ int ensure_sparse(gpuagg_ctx *c) {
   c->sv.cnt = c->sv.k0 + 3;
   c->sv.byt = c->sv.k0 + 4;
   c->sv.mask = (uint32_t)(n - 1);
+  c->sv.seg_log2 = std::min<uint32_t>(lg, kSparseSegLog2);
   c->sparse_slots = n;
   return GPUAGG_OK;
 }
@@ -557,6 +562,9 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   const bool direct = c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH;
   if (!direct && s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
     s.hll_shift = std::min<uint32_t>(8u, kHllWindowLog2Bytes - s.hll_p);
+    // EXPERIMENT (timing of the scatter only; the fold is skipped, results are wrong)
+    static const char *xs = getenv("GPUAGG_EXP_HSHIFT");
+    if (xs) s.hll_shift = (uint32_t)atoi(xs);
     hnwin = ((uint64_t)s.hll_slots + (1u << s.hll_shift) - 1) >> s.hll_shift;
     if (hnwin > kHllMaxWindows) hnwin = 0;
   }
@@ -661,7 +669,13 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     return L;
   };
-  a.lds_bins = prefix(kLdsMaxBins);
+  // compact group-by keys (generic kernel) go through per-segment lists whose fill
+  // counters take LDS words from the dense window
+  const bool generic = !a.dense_ng;
+  const uint64_t sp_nwin = c->sparse_slots ? c->sparse_slots >> c->sv.seg_log2 : 0;
+  const bool sp_lists = generic && c->sv.compact && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
+                        !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH);
+  a.lds_bins = prefix(kLdsMaxBins - (sp_lists ? (uint32_t)(sp_nwin + 1) / 2 : 0u));
   // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
   a.sig = 0;
@@ -737,6 +751,21 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
         a.stage_b = c->d_stage_b;
       }
+    }
+    a.sp_lists = nullptr;
+    a.sp_counts = nullptr;
+    a.sp_nwin = 0;
+    if (sp_lists) {
+      // at most one compact (DNS) insert per record; hashed keys spread evenly over the
+      // segments: chunk / nwin per list + 25 % + 64 (a full list inserts in place, exact)
+      const uint64_t mean = a.chunk / sp_nwin;
+      const uint64_t cap = mean + mean / 4 + 64;
+      if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc, (size_t)a.blocks * sp_nwin * cap))) return rc;
+      if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * sp_nwin))) return rc;
+      a.sp_lists = c->d_sp_lists;
+      a.sp_counts = c->d_sp_counts;
+      a.sp_nwin = (uint32_t)sp_nwin;
+      a.sp_cap = (uint32_t)cap;
     }
     std::array<hipEvent_t, 3> ev{};
     if (c->timing) {
@@ -874,6 +903,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_stage_b);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
+  dev_free(c->d_sp_lists);
+  dev_free(c->d_sp_counts);
   dev_free(c->d_hll_lists);
   dev_free(c->d_hll_counts);
   dev_free(c->d_decode_oor);
