@@ -603,24 +603,37 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
   ulonglong2 *g = (ulonglong2 *)(s.k0 + 2ull * ((size_t)w << s.seg_log2));
   for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) ((ulonglong2 *)seg)[i] = g[i];
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
-  for (uint32_t l = threadIdx.x >> 6; l < n_lists; l += nwaves) {
-    const uint32_t cnt = counts[(size_t)l * nwin + w];
-    const unsigned long long *e = lists + ((size_t)l * nwin + w) * cap;
-    for (uint32_t j = lane; j < cnt; j += 64) {
-      const unsigned long long key = e[j];
-      const uint32_t h = compact_home(s, key);
-      bool done = false;
-      for (uint32_t probe = 0; probe <= smask; ++probe) {
-        const uint32_t i = (h + probe) & smask;
-        const unsigned long long cur = atomicCAS(&seg[2 * i], 0ULL, key);
-        if (cur == 0ULL || cur == key) {
-          atomicAdd(&seg[2 * i + 1], 1ULL);
-          done = true;
-          break;
-        }
+  auto insert = [&](unsigned long long key) {
+    const uint32_t h = compact_home(s, key);
+    for (uint32_t probe = 0; probe <= smask; ++probe) {
+      const uint32_t i = (h + probe) & smask;
+      const unsigned long long cur = atomicCAS(&seg[2 * i], 0ULL, key);
+      if (cur == 0ULL || cur == key) {
+        atomicAdd(&seg[2 * i + 1], 1ULL);
+        return;
       }
-      if (!done) atomicAdd(s.dropped, 1ULL);
+    }
+    atomicAdd(s.dropped, 1ULL);
+  };
+  // Lists are short (tens of keys), so a lane owns a whole list: a wave loads 64 counts
+  // at once and then 8 keys per lane per round trip (cap is even: 16-byte pairs).
+  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+  for (uint32_t l0 = (threadIdx.x >> 6) * 64u; l0 < n_lists; l0 += nwaves * 64u) {
+    const uint32_t l = l0 + lane;
+    const uint32_t cnt = l < n_lists ? counts[(size_t)l * nwin + w] : 0u;
+    const ulonglong2 *e2 = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap);
+    uint32_t mx = cnt;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    for (uint32_t k = 0; k < mx; k += 8) {
+      ulonglong2 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = k + 2 * q < cnt ? e2[k / 2 + q] : make_ulonglong2(0ULL, 0ULL);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (k + 2 * q < cnt) insert(v[q].x);
+        if (k + 2 * q + 1 < cnt) insert(v[q].y);
+      }
     }
   }
   __syncthreads();
@@ -1109,6 +1122,21 @@ struct SketchK {
   uint32_t hll_slots; // slots covered by the registers
 };
 
+// Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
+// flight per lane before the updates (fold kernels are latency-bound on list reads).
+template <class F>
+__device__ __forceinline__ void walk_u4(const uint4 *e4, uint32_t n4, uint32_t t, uint32_t stride, F &&f) {
+  uint32_t j = t;
+  for (; j + 3 * stride < n4; j += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = e4[j + q * stride];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f(v[q]);
+  }
+  for (; j < n4; j += stride) f(e4[j]);
+}
+
 // One record's sketch updates: each count-min row's column is appended to the list of
 // its window (row, column >> wshift) and each HLL (pod, register, rank) to the list of
 // its pod window; a full list falls back to the global atomic (exact, slow).
@@ -1174,9 +1202,26 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
     const uint64_t v0 = start >> 2, vend = v0 + ((end - start) >> 2);
     const uint4 *s4 = (const uint4 *)k.src, *d4 = (const uint4 *)k.dst;
     const uint4 *p4 = (const uint4 *)k.ports, *m4 = (const uint4 *)k.meta;
-    for (uint64_t v = v0 + threadIdx.x; v < vend; v += blockDim.x) {
-      const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
-      const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
+    // software pipeline: the next step's record loads are in flight while this step's
+    // probes and list appends run
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint64_t v = v0 + threadIdx.x;
+    uint4 ns = z4, nd = z4, nm = z4, np = z4;
+    if (v < vend) {
+      ns = s4[v];
+      nd = d4[v];
+      nm = m4[v];
+      np = need_ports ? p4[v] : z4;
+    }
+    for (; v < vend; v += blockDim.x) {
+      const uint4 vs = ns, vd = nd, vm = nm, vp = np;
+      const uint64_t vn = v + blockDim.x;
+      if (vn < vend) {
+        ns = s4[vn];
+        nd = d4[vn];
+        nm = m4[vn];
+        np = need_ports ? p4[vn] : z4;
+      }
       Lk ls[4] = {none, none, none, none};
       if (k.p) {
         const uint32_t ip[4] = {vs.x, vs.y, vs.z, vs.w};
@@ -1222,21 +1267,28 @@ __global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k, uint32_t n_li
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
   const uint32_t imask = (1u << k.p) - 1u;
+  auto apply = [&](uint32_t x) {
+    const uint32_t byte = ((x >> 24) << k.p) + ((x >> 6) & imask), rho = x & 63u;
+    uint32_t *word = &regs[byte >> 2];
+    const uint32_t sh = (byte & 3u) * 8u;
+    uint32_t old = *word;
+    while (((old >> sh) & 0xFFu) < rho) {
+      const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rho << sh));
+      if (prev == old) break;
+      old = prev;
+    }
+  };
   for (uint32_t l = threadIdx.x >> 6; l < n_lists; l += nwaves) {
     const uint32_t cnt = k.hcounts[(size_t)l * k.hnwin + w];
-    const uint32_t *e = k.hlists + ((size_t)l * k.hnwin + w) * k.hcap;
-    for (uint32_t j = lane; j < cnt; j += 64) {
-      const uint32_t x = e[j];
-      const uint32_t byte = ((x >> 24) << k.p) + ((x >> 6) & imask), rho = x & 63u;
-      uint32_t *word = &regs[byte >> 2];
-      const uint32_t sh = (byte & 3u) * 8u;
-      uint32_t old = *word;
-      while (((old >> sh) & 0xFFu) < rho) {
-        const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rho << sh));
-        if (prev == old) break;
-        old = prev;
-      }
-    }
+    const uint32_t *e = k.hlists + ((size_t)l * k.hnwin + w) * k.hcap;  // 16-byte aligned (hcap % 16 == 0)
+    const uint32_t n4 = cnt >> 2;
+    walk_u4((const uint4 *)e, n4, lane, 64u, [&](const uint4 &v) {
+      apply(v.x);
+      apply(v.y);
+      apply(v.z);
+      apply(v.w);
+    });
+    for (uint32_t j = (n4 << 2) + lane; j < cnt; j += 64) apply(e[j]);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) g[i] = ((const uint4 *)regs)[i];
@@ -1251,20 +1303,21 @@ __global__ __launch_bounds__(1024) void cms_fold_kernel(SketchK k, uint32_t n_li
   __syncthreads();
   const uint32_t l0 = (uint32_t)((uint64_t)part * n_lists / nparts);
   const uint32_t l1 = (uint32_t)((uint64_t)(part + 1) * n_lists / nparts);
-  for (uint32_t l = l0; l < l1; ++l) {
+  // one wave per list, four 16-byte loads in flight per lane
+  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+  for (uint32_t l = l0 + (threadIdx.x >> 6); l < l1; l += nwaves) {
     const uint32_t c = k.counts[(size_t)l * k.nwin + w];
     const uint16_t *e = k.lists + ((size_t)l * k.nwin + w) * k.cap;  // 16-byte aligned (cap % 8 == 0)
     const uint32_t n8 = c >> 3;
-    for (uint32_t j = threadIdx.x; j < n8; j += blockDim.x) {
-      const uint4 v = ((const uint4 *)e)[j];
+    walk_u4((const uint4 *)e, n8, lane, 64u, [&](const uint4 &v) {
       const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         atomicAdd(&cwin[x[q] & 0xFFFFu], 1u);
         atomicAdd(&cwin[x[q] >> 16], 1u);
       }
-    }
-    for (uint32_t j = (n8 << 3) + threadIdx.x; j < c; j += blockDim.x) atomicAdd(&cwin[e[j]], 1u);
+    });
+    for (uint32_t j = (n8 << 3) + lane; j < c; j += 64) atomicAdd(&cwin[e[j]], 1u);
   }
   __syncthreads();
   const uint32_t hi_bits = k.wlog2 - k.wshift;

@@ -759,7 +759,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       // at most one compact (DNS) insert per record; hashed keys spread evenly over the
       // segments: chunk / nwin per list + 25 % + 64 (a full list inserts in place, exact)
       const uint64_t mean = a.chunk / sp_nwin;
-      const uint64_t cap = mean + mean / 4 + 64;
+      const uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
       if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc, (size_t)a.blocks * sp_nwin * cap))) return rc;
       if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * sp_nwin))) return rc;
       a.sp_lists = c->d_sp_lists;
