@@ -95,9 +95,10 @@ def main():
         run("c3-cms-direct", W.LOCAL_FWD_DROP, pods, cols3, n3, flags=2, **cms)
         run("c3-hll", W.LOCAL_FWD_DROP, pods, cols3, n3, hll_precision=14)
         run("c3-hll-direct", W.LOCAL_FWD_DROP, pods, cols3, n3, flags=2, hll_precision=14)
-        return
+        del cols3
+        cols = None
     if not ONLY or any(v.startswith("c5") for v in ONLY):  # C5 spec split by metric
-        del cols
+        cols = None
         c5 = W.CONFIGS["c5"]
         p5 = W.make_pods(c5["pods"], seed=c5["seed"])
         n5 = c5["records"]
