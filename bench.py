@@ -148,7 +148,9 @@ def pmc_traffic(cfg_name: str, kernel: str):
     except ValueError:
         return None, "unreadable %s" % os.path.relpath(path, ROOT)
     names = pmc.get("kernel", [])
-    if not kernel or not any(kernel in k for k in names):
+    # a composite "a+b+c" (the sketch pass) needs every part profiled
+    parts = [p for p in (kernel or "").split("+") if p]
+    if not parts or not all(any(p in k for k in names) for p in parts):
         return None, "%s profiles %s, not %s: refused" % (os.path.relpath(path, ROOT), names, kernel)
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 

@@ -1120,6 +1120,8 @@ struct SketchK {
   uint32_t *hlists;   // [gridDim.x][hnwin][hcap]
   uint32_t *hcounts;  // [gridDim.x][hnwin]
   uint32_t hll_slots; // slots covered by the registers
+  const uint8_t *ipl; // LDS image of every pod IP (source lookups), or null: HBM table
+  uint32_t ipl_nb, ipl_seed, ipl_bytes;
 };
 
 // Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
@@ -1183,13 +1185,24 @@ struct SketchLists {
 // Sketch pass over the records.  kVec: 4 consecutive records per lane per step (16-byte
 // loads per column) and the 8 IP-table probes of their 4 sources issued back to back, so
 // a wave keeps ~12 loads in flight instead of waiting on one record's probe at a time.
-template <bool kVec>
+template <bool kVec, bool kLdsIp>
 __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
-  // [nwin] count-min list fill counters, then [hnwin] HLL list fill counters
+  // [nwin] count-min list fill counters, then [hnwin] HLL list fill counters, then
+  // (kLdsIp) the IP image at the next 16-byte boundary
   extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];
   uint32_t *hcnt = wcnt + k.nwin;
+  const uint32_t img_off = (k.nwin + k.hnwin + 3u) & ~3u;
+  const uint32_t *keys = wcnt + img_off;
+  const uint16_t *vals = (const uint16_t *)((const uint8_t *)keys + ipl_vals_offset(k.ipl_nb));
   for (uint32_t i = threadIdx.x; i < k.nwin + k.hnwin; i += blockDim.x) wcnt[i] = 0u;
+  if (kLdsIp)
+    for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
+      ((uint4 *)(wcnt + img_off))[i] = ((const uint4 *)k.ipl)[i];
   __syncthreads();
+  auto lds_lookup = [&](uint32_t ip) {
+    const uint32_t v = vals[ipl_probe_index(keys, k.ipl_nb, k.ipl_seed, ip)];
+    return Lk{v == kIplNoSlot ? -1 : (int32_t)v, 0u};
+  };
   const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
   const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
   const SketchLists L{k, wcnt, hcnt, k.lists + (size_t)blockIdx.x * k.nwin * k.cap,
@@ -1223,7 +1236,12 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
         np = need_ports ? p4[vn] : z4;
       }
       Lk ls[4] = {none, none, none, none};
-      if (k.p) {
+      if (kLdsIp) {
+        ls[0] = lds_lookup(vs.x);
+        ls[1] = lds_lookup(vs.y);
+        ls[2] = lds_lookup(vs.z);
+        ls[3] = lds_lookup(vs.w);
+      } else if (k.p) {
         const uint32_t ip[4] = {vs.x, vs.y, vs.z, vs.w};
         uint64_t e1[4], e2[4];
 #pragma unroll
@@ -1243,7 +1261,8 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
     const uint32_t s = k.src[i];
-    L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i], k.p ? ip_lookup(k.t, s) : none);
+    L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i],
+             kLdsIp ? lds_lookup(s) : k.p ? ip_lookup(k.t, s) : none);
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
@@ -1355,19 +1374,31 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   k.hlists = a.hll_lists;
   k.hcounts = a.hll_counts;
   k.hll_slots = a.hll_slots;
-  const size_t scatter_lds = (size_t)(a.nwin + a.hll_nwin) * 4;
+  size_t scatter_lds = (size_t)((a.nwin + a.hll_nwin + 3u) & ~3u) * 4;
+  // source lookups in an LDS image of the IP table when it fits next to the counters
+  const bool lds_ip = a.ipl && a.hll_p && scatter_lds + a.ipl_bytes <= kLdsBytes;
+  if (lds_ip) {
+    k.ipl = a.ipl;
+    k.ipl_nb = a.ipl_nb;
+    k.ipl_seed = a.ipl_seed;
+    k.ipl_bytes = a.ipl_bytes;
+    scatter_lds += a.ipl_bytes;
+  }
   // 16-byte loads need aligned columns and workgroup chunks of whole vectors
   const bool vec = a.chunk % 4 == 0 && ((uintptr_t)k.src | (uintptr_t)k.dst | (uintptr_t)k.meta |
                                         (uintptr_t)(k.ports ? k.ports : k.src)) % 16 == 0;
-  const void *fn = vec ? (const void *)sketch_scatter_kernel<true> : (const void *)sketch_scatter_kernel<false>;
+  const void *fn = vec ? (lds_ip ? (const void *)sketch_scatter_kernel<true, true>
+                                 : (const void *)sketch_scatter_kernel<true, false>)
+                       : (lds_ip ? (const void *)sketch_scatter_kernel<false, true>
+                                 : (const void *)sketch_scatter_kernel<false, false>);
   hipError_t e;
   if (scatter_lds > 64 * 1024 &&
       (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scatter_lds)) != hipSuccess)
     return e;
-  if (vec)
-    hipLaunchKernelGGL(sketch_scatter_kernel<true>, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
-  else
-    hipLaunchKernelGGL(sketch_scatter_kernel<false>, dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  if (vec && lds_ip) hipLaunchKernelGGL((sketch_scatter_kernel<true, true>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  else if (vec) hipLaunchKernelGGL((sketch_scatter_kernel<true, false>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  else if (lds_ip) hipLaunchKernelGGL((sketch_scatter_kernel<false, true>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
+  else hipLaunchKernelGGL((sketch_scatter_kernel<false, false>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (a.nwin && a.cms_depth) {
     const size_t lds = (size_t)4 << a.win_shift;

@@ -93,6 +93,8 @@ struct SketchArgs {
   uint32_t hll_slots;               // slots covered by the registers
   uint32_t hll_shift, hll_nwin, hll_cap;  // HLL windows of 2^hll_shift pods; nwin 0: direct CAS
   uint32_t *hll_lists, *hll_counts;
+  const uint8_t *ipl;               // LDS image of every pod IP for the source lookup, or null
+  uint32_t ipl_nb, ipl_seed, ipl_bytes;
 };
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
 

@@ -178,6 +178,9 @@ struct gpuagg_ctx {
   // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
   uint8_t *d_ipl = nullptr;
   size_t ipl_alloc = 0;
+  uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
+  size_t ipl_all_alloc = 0;
+  uint32_t ipl_all_nb = 0, ipl_all_seed = 0, ipl_all_bytes = 0;
   uint32_t ipl_nb = 0, ipl_seed = 0, ipl_bytes = 0;
   uint64_t ip_version = 0;
 
@@ -558,6 +561,12 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   s.blocks = c->n_cu;
   s.win_shift = std::min<uint32_t>(kCmsWindowShift, s.cms_wlog2);
   s.hll_slots = s.hll_p ? (uint32_t)(c->hll_len >> s.hll_p) : 0;
+  if (s.hll_p && c->ipl_all_bytes) {
+    s.ipl = c->d_ipl_all;
+    s.ipl_nb = c->ipl_all_nb;
+    s.ipl_seed = c->ipl_all_seed;
+    s.ipl_bytes = c->ipl_all_bytes;
+  }
   uint64_t hnwin = 0;
   const bool direct = c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH;
   if (!direct && s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
@@ -889,6 +898,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   }
   dev_free(c->d_ip);
   dev_free(c->d_ipl);
+  dev_free(c->d_ipl_all);
   dev_free(c->d_dense_cnt);
   dev_free(c->d_dense_byt);
   dev_free(c->sv.k0);  // k1, k2, cnt, byt point into the same array
@@ -1260,6 +1270,7 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
+  dev_free(c->d_ipl_all);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
@@ -1268,6 +1279,27 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       c->ipl_nb = im.nb;
       c->ipl_seed = im.seed;
       c->ipl_bytes = bytes;
+    }
+  }
+  // LDS image of every pod IP (the apiserver pseudo pod included: it is a source pod for
+  // the HLL) for the sketch pass
+  c->ipl_all_bytes = 0;
+  if (c->cfg.hll_precision && !(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
+    std::vector<std::pair<uint32_t, uint32_t>> ents;
+    for (const auto &kv : last) ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
+    IplImage im;
+    if (ipl_build(ents, &im)) {
+      const uint32_t bytes = (uint32_t)im.bytes.size();
+      if (bytes > c->ipl_all_alloc) {
+        dev_free(c->d_ipl_all);
+        c->ipl_all_alloc = 0;
+        if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
+        c->ipl_all_alloc = bytes;
+      }
+      HIPCHK(c, hipMemcpy(c->d_ipl_all, im.bytes.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_all_nb = im.nb;
+      c->ipl_all_seed = im.seed;
+      c->ipl_all_bytes = bytes;
     }
   }
   c->ip_seed = seed;
