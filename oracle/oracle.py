@@ -171,6 +171,7 @@ class Flow:
     extensions: Optional[RetinaMetadata] = None
     dns: Optional[DNS] = None  # flow.L7.Dns
     l7_type: str = ""
+    time_ns: int = 0           # ToFlow's ts (decodeTime keeps every nanosecond, flow_utils.go:307-317)
 
 
 # ---------------------------------------------------------------------------------
@@ -249,6 +250,7 @@ def decode_packet(raw: bytes) -> Flow:
     add_tcp_flags(f, (flags & TCP_FLAG_SYN) >> 1, (flags & TCP_FLAG_ACK) >> 4,
                   flags & TCP_FLAG_FIN, (flags & TCP_FLAG_RST) >> 2,
                   (flags & TCP_FLAG_PSH) >> 3, (flags & TCP_FLAG_URG) >> 5)
+    f.time_ns = t_nsec
     if f.trace_observation_point == OBS_TO_NETWORK:
         meta.tcp_id = tsval
     elif f.trace_observation_point == OBS_FROM_NETWORK:

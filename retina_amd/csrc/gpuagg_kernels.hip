@@ -1114,11 +1114,17 @@ struct SketchK {
   uint32_t *counts;  // [gridDim.x][nwin]
   uint32_t *hll;
   uint32_t p;
-  // HLL updates bucketed by source-pod window (2^hshift pods, <= 128 KiB of registers):
-  // u32 entries pod-in-window << 24 | register << 6 | rank; hnwin = 0: direct CAS
-  uint32_t hshift, hnwin, hcap;
-  uint32_t *hlists;   // [gridDim.x][hnwin][hcap]
-  uint32_t *hcounts;  // [gridDim.x][hnwin]
+  // HLL updates bucketed in two levels: the scatter appends to the list of the source
+  // pod's super-window (2^hsshift pods, few lists, so L2 keeps them whole-line), the
+  // split pass re-buckets each super-window into fine windows (2^hshift pods, <= 128 KiB
+  // of registers), the fold applies a fine window in LDS.  u32 entry:
+  // pod-in-super-window << (p + 6) | register << 6 | rank.  hnsup = 0: direct CAS.
+  uint32_t hshift, hsshift, hnsup, hnwin, hcap;
+  uint32_t *hlists;   // level 1: [gridDim.x][hnsup][hcap]
+  uint32_t *hcounts;  // [gridDim.x][hnsup]
+  uint32_t hb2, hcap2;  // split workgroups per super-window, level-2 list capacity
+  uint32_t *hlists2;  // level 2: [hnsup][hb2][2^(hsshift - hshift)][hcap2]
+  uint32_t *hcounts2; // [hnsup][hb2][2^(hsshift - hshift)]
   uint32_t hll_slots; // slots covered by the registers
   const uint8_t *ipl; // LDS image of every pod IP (source lookups), or null: HBM table
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
@@ -1166,16 +1172,17 @@ struct SketchLists {
       }
     }
     if (k.p && ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
-      bool direct = k.hnwin == 0;
+      bool direct = k.hnsup == 0;
       if (!direct) {
         const uint64_t h = hll_hash(d);
         const uint32_t idx = (uint32_t)(h >> (64 - k.p));
         const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
-        const uint32_t w = (uint32_t)ls.slot >> k.hshift;
+        const uint32_t w = (uint32_t)ls.slot >> k.hsshift;
         const uint32_t pos = atomicAdd(&hcnt[w], 1u);
         direct = pos >= k.hcap;
         if (!direct)
-          hmine[(size_t)w * k.hcap + pos] = (((uint32_t)ls.slot & ((1u << k.hshift) - 1u)) << 24) | (idx << 6) | rho;
+          hmine[(size_t)w * k.hcap + pos] =
+              (((uint32_t)ls.slot & ((1u << k.hsshift) - 1u)) << (k.p + 6)) | (idx << 6) | rho;
       }
       if (direct) hll_update(k.hll, k.p, ls.slot, d);
     }
@@ -1191,10 +1198,10 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
   // (kLdsIp) the IP image at the next 16-byte boundary
   extern __shared__ __attribute__((aligned(16))) uint32_t wcnt[];
   uint32_t *hcnt = wcnt + k.nwin;
-  const uint32_t img_off = (k.nwin + k.hnwin + 3u) & ~3u;
+  const uint32_t img_off = (k.nwin + k.hnsup + 3u) & ~3u;
   const uint32_t *keys = wcnt + img_off;
   const uint16_t *vals = (const uint16_t *)((const uint8_t *)keys + ipl_vals_offset(k.ipl_nb));
-  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnwin; i += blockDim.x) wcnt[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnsup; i += blockDim.x) wcnt[i] = 0u;
   if (kLdsIp)
     for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
       ((uint4 *)(wcnt + img_off))[i] = ((const uint4 *)k.ipl)[i];
@@ -1206,7 +1213,7 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
   const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
   const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
   const SketchLists L{k, wcnt, hcnt, k.lists + (size_t)blockIdx.x * k.nwin * k.cap,
-                      k.hlists + (size_t)blockIdx.x * k.hnwin * k.hcap, (1u << k.wlog2) - 1u,
+                      k.hlists + (size_t)blockIdx.x * k.hnsup * k.hcap, (1u << k.wlog2) - 1u,
                       k.wlog2 - k.wshift, (1u << k.wshift) - 1u};
   const bool need_ports = k.depth != 0 && k.ports;
   const Lk none{-1, 0};
@@ -1267,17 +1274,66 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
     k.counts[(size_t)blockIdx.x * k.nwin + w] = wcnt[w] < k.cap ? wcnt[w] : k.cap;
-  for (uint32_t w = threadIdx.x; w < k.hnwin; w += blockDim.x)
-    k.hcounts[(size_t)blockIdx.x * k.hnwin + w] = hcnt[w] < k.hcap ? hcnt[w] : k.hcap;
+  for (uint32_t w = threadIdx.x; w < k.hnsup; w += blockDim.x)
+    k.hcounts[(size_t)blockIdx.x * k.hnsup + w] = hcnt[w] < k.hcap ? hcnt[w] : k.hcap;
+}
+
+// HLL level 2: workgroup (super-window s, part b) reads scatter lists b, b + hb2, ... of
+// super-window s and appends each entry to its fine window's list (s, b, fine window);
+// a full list applies the entry with the global CAS (exact).
+__global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_lists) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t fcnt[];
+  const uint32_t s = blockIdx.x / k.hb2, b = blockIdx.x % k.hb2;
+  const uint32_t fshift = k.hsshift - k.hshift, nfine = 1u << fshift;
+  for (uint32_t i = threadIdx.x; i < nfine; i += blockDim.x) fcnt[i] = 0u;
+  __syncthreads();
+  const size_t base2 = ((size_t)s * k.hb2 + b) * nfine;
+  uint32_t *out = k.hlists2 + base2 * k.hcap2;
+  const uint32_t psh = k.p + 6, pmask = (1u << k.hsshift) - 1u;
+  auto put = [&](uint32_t x) {
+    const uint32_t pod = (x >> psh) & pmask, wf = pod >> k.hshift;
+    const uint32_t pos = atomicAdd(&fcnt[wf], 1u);
+    if (pos < k.hcap2) {
+      out[(size_t)wf * k.hcap2 + pos] = x;
+      return;
+    }
+    const uint32_t slot = (s << k.hsshift) | pod;  // full list: the global CAS
+    const size_t byte = ((size_t)slot << k.p) + ((x >> 6) & ((1u << k.p) - 1u));
+    const uint32_t rho = x & 63u, sh = (uint32_t)(byte & 3) * 8u;
+    uint32_t *word = k.hll + (byte >> 2);
+    uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((old >> sh) & 0xFFu) < rho) {
+      const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rho << sh));
+      if (prev == old) break;
+      old = prev;
+    }
+  };
+  for (uint32_t l = b; l < n_lists; l += k.hb2) {
+    const uint32_t cnt = k.hcounts[(size_t)l * k.hnsup + s];
+    const uint32_t *e = k.hlists + ((size_t)l * k.hnsup + s) * k.hcap;  // 16-byte aligned (hcap % 16 == 0)
+    const uint32_t n4 = cnt >> 2;
+    walk_u4((const uint4 *)e, n4, threadIdx.x, blockDim.x, [&](const uint4 &v) {
+      put(v.x);
+      put(v.y);
+      put(v.z);
+      put(v.w);
+    });
+    for (uint32_t j = (n4 << 2) + threadIdx.x; j < cnt; j += blockDim.x) put(e[j]);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nfine; i += blockDim.x)
+    k.hcounts2[base2 + i] = fcnt[i] < k.hcap2 ? fcnt[i] : k.hcap2;
 }
 
 // Workgroup w folds HLL window w: its pods' registers (<= 128 KiB) are loaded into LDS,
 // every scatter workgroup's list for the window is applied with byte-max (a 32-bit CAS on
 // the register's word; one wave per list), and the registers are stored back -- one
 // coalesced read and write of the register array instead of a random global CAS per record.
-__global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k, uint32_t n_lists) {
+__global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k) {
   extern __shared__ __attribute__((aligned(16))) uint32_t regs[];
   const uint32_t w = blockIdx.x;
+  const uint32_t fshift = k.hsshift - k.hshift, nfine = 1u << fshift;
+  const uint32_t s = w >> fshift, wf = w & (nfine - 1u);
   const uint32_t pod0 = w << k.hshift;
   const uint32_t npods = min(1u << k.hshift, k.hll_slots - pod0);
   const size_t bytes = (size_t)npods << k.p;  // multiple of 16 (p >= 4)
@@ -1286,8 +1342,9 @@ __global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k, uint32_t n_li
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
   const uint32_t imask = (1u << k.p) - 1u;
+  const uint32_t psh = k.p + 6, fmask = (1u << k.hshift) - 1u;
   auto apply = [&](uint32_t x) {
-    const uint32_t byte = ((x >> 24) << k.p) + ((x >> 6) & imask), rho = x & 63u;
+    const uint32_t byte = (((x >> psh) & fmask) << k.p) + ((x >> 6) & imask), rho = x & 63u;
     uint32_t *word = &regs[byte >> 2];
     const uint32_t sh = (byte & 3u) * 8u;
     uint32_t old = *word;
@@ -1297,9 +1354,11 @@ __global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k, uint32_t n_li
       old = prev;
     }
   };
-  for (uint32_t l = threadIdx.x >> 6; l < n_lists; l += nwaves) {
-    const uint32_t cnt = k.hcounts[(size_t)l * k.hnwin + w];
-    const uint32_t *e = k.hlists + ((size_t)l * k.hnwin + w) * k.hcap;  // 16-byte aligned (hcap % 16 == 0)
+  // list (s, b, wf) of every split workgroup b: one wave per list
+  for (uint32_t b = threadIdx.x >> 6; b < k.hb2; b += nwaves) {
+    const size_t li = ((size_t)s * k.hb2 + b) * nfine + wf;
+    const uint32_t cnt = k.hcounts2[li];
+    const uint32_t *e = k.hlists2 + li * k.hcap2;  // 16-byte aligned (hcap2 % 16 == 0)
     const uint32_t n4 = cnt >> 2;
     walk_u4((const uint4 *)e, n4, lane, 64u, [&](const uint4 &v) {
       apply(v.x);
@@ -1369,12 +1428,18 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   k.hll = (uint32_t *)a.hll;
   k.p = a.hll_p;
   k.hshift = a.hll_shift;
+  k.hsshift = a.hll_sshift;
+  k.hnsup = a.hll_nsup;
   k.hnwin = a.hll_nwin;
   k.hcap = a.hll_cap;
   k.hlists = a.hll_lists;
   k.hcounts = a.hll_counts;
+  k.hb2 = a.hll_b2;
+  k.hcap2 = a.hll_cap2;
+  k.hlists2 = a.hll_lists2;
+  k.hcounts2 = a.hll_counts2;
   k.hll_slots = a.hll_slots;
-  size_t scatter_lds = (size_t)((a.nwin + a.hll_nwin + 3u) & ~3u) * 4;
+  size_t scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   // source lookups in an LDS image of the IP table when it fits next to the counters
   const bool lds_ip = a.ipl && a.hll_p && scatter_lds + a.ipl_bytes <= kLdsBytes;
   if (lds_ip) {
@@ -1409,13 +1474,16 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  if (a.hll_nwin && a.hll_p && !getenv("GPUAGG_EXP_HSHIFT")) {
+  if (a.hll_nsup && a.hll_p) {
+    hipLaunchKernelGGL(hll_split_kernel, dim3(a.hll_nsup * a.hll_b2), dim3(1024),
+                       (size_t)4 << (a.hll_sshift - a.hll_shift), st, k, a.blocks);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t lds = (size_t)1 << (a.hll_p + a.hll_shift);
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)hll_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(hll_fold_kernel, dim3(a.hll_nwin), dim3(1024), lds, st, k, a.blocks);
+    hipLaunchKernelGGL(hll_fold_kernel, dim3(a.hll_nwin), dim3(1024), lds, st, k);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

@@ -91,8 +91,12 @@ struct SketchArgs {
   uint8_t *hll;
   uint32_t hll_p;
   uint32_t hll_slots;               // slots covered by the registers
-  uint32_t hll_shift, hll_nwin, hll_cap;  // HLL windows of 2^hll_shift pods; nwin 0: direct CAS
+  // HLL two-level bucketing (see SketchK): fine windows of 2^hll_shift pods, super-windows
+  // of 2^hll_sshift pods; hll_nsup 0: direct CAS
+  uint32_t hll_shift, hll_sshift, hll_nsup, hll_nwin, hll_cap;
   uint32_t *hll_lists, *hll_counts;
+  uint32_t hll_b2, hll_cap2;
+  uint32_t *hll_lists2, *hll_counts2;
   const uint8_t *ipl;               // LDS image of every pod IP for the source lookup, or null
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
 };

@@ -250,6 +250,10 @@ struct gpuagg_ctx {
   size_t hll_lists_alloc = 0;
   uint32_t *d_hll_counts = nullptr;
   size_t hll_counts_alloc = 0;
+  uint32_t *d_hll_lists2 = nullptr;
+  size_t hll_lists2_alloc = 0;
+  uint32_t *d_hll_counts2 = nullptr;
+  size_t hll_counts2_alloc = 0;
   std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch pass start, end
 };
 
@@ -567,15 +571,20 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     s.ipl_seed = c->ipl_all_seed;
     s.ipl_bytes = c->ipl_all_bytes;
   }
-  uint64_t hnwin = 0;
+  // HLL bucketing: fine windows of 2^hll_shift pods (128 KiB of registers, the fold's
+  // LDS), super-windows of 2^hll_sshift pods (~16 of them, the scatter's lists); pod bits
+  // of an entry: 26 - p
+  uint64_t hnwin = 0, hnsup = 0;
   const bool direct = c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH;
   if (!direct && s.hll_p && s.hll_p <= kHllWindowLog2Bytes && s.hll_slots) {
     s.hll_shift = std::min<uint32_t>(8u, kHllWindowLog2Bytes - s.hll_p);
-    // EXPERIMENT (timing of the scatter only; the fold is skipped, results are wrong)
-    static const char *xs = getenv("GPUAGG_EXP_HSHIFT");
-    if (xs) s.hll_shift = (uint32_t)atoi(xs);
+    uint32_t ss = s.hll_shift;
+    while ((((uint64_t)s.hll_slots + (1u << ss) - 1) >> ss) > 16 && ss < 26 - s.hll_p && ss < s.hll_shift + 10) ++ss;
+    s.hll_sshift = ss;
     hnwin = ((uint64_t)s.hll_slots + (1u << s.hll_shift) - 1) >> s.hll_shift;
-    if (hnwin > kHllMaxWindows) hnwin = 0;
+    hnsup = ((uint64_t)s.hll_slots + (1u << ss) - 1) >> ss;
+    if (hnwin > kHllMaxWindows || hnsup > 1024) hnwin = hnsup = 0;
+    s.hll_b2 = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, c->n_cu / std::max<uint64_t>(1, hnsup)));
   }
   const uint64_t nwin = s.cms_depth ? ((uint64_t)s.cms_depth << (s.cms_wlog2 - s.win_shift)) : 0;
   const uint64_t per_launch = (uint64_t)s.blocks << 20;  // <= 2^20 records per scatter workgroup
@@ -604,18 +613,29 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       s.counts = c->d_sk_counts;
       s.fold_blocks = (uint32_t)nwin * std::max<uint32_t>(1u, c->n_cu / (uint32_t)nwin);
     }
-    s.hll_nwin = 0;
-    if (hnwin) {
-      // at most one entry per record; a uniform spread gives chunk / hnwin per list, +25 %
-      // + 64 of headroom (overflow is exact: it falls back to a global CAS)
-      const uint64_t mean = s.chunk / hnwin;
+    s.hll_nwin = s.hll_nsup = 0;
+    if (hnsup) {
+      // at most one entry per record; uniform pods give chunk / nsup per scatter list and
+      // m / (nsup * b2 * nfine) per split list: +25 % + 64 of headroom each (a full list
+      // applies the update with the global CAS, exact)
+      const uint64_t nfine = (uint64_t)1 << (s.hll_sshift - s.hll_shift);
+      const uint64_t mean = s.chunk / hnsup;
       const uint64_t cap = (mean + mean / 4 + 64 + 15) & ~15ULL;
-      if ((rc = ensure_buf(c, &c->d_hll_lists, &c->hll_lists_alloc, (size_t)s.blocks * hnwin * cap))) return rc;
-      if ((rc = ensure_buf(c, &c->d_hll_counts, &c->hll_counts_alloc, (size_t)s.blocks * hnwin))) return rc;
+      const uint64_t mean2 = m / (hnsup * s.hll_b2 * nfine);
+      const uint64_t cap2 = (mean2 + mean2 / 4 + 64 + 15) & ~15ULL;
+      if ((rc = ensure_buf(c, &c->d_hll_lists, &c->hll_lists_alloc, (size_t)s.blocks * hnsup * cap))) return rc;
+      if ((rc = ensure_buf(c, &c->d_hll_counts, &c->hll_counts_alloc, (size_t)s.blocks * hnsup))) return rc;
+      const size_t n2 = (size_t)hnsup * s.hll_b2 * nfine;
+      if ((rc = ensure_buf(c, &c->d_hll_lists2, &c->hll_lists2_alloc, n2 * cap2))) return rc;
+      if ((rc = ensure_buf(c, &c->d_hll_counts2, &c->hll_counts2_alloc, n2))) return rc;
+      s.hll_nsup = (uint32_t)hnsup;
       s.hll_nwin = (uint32_t)hnwin;
       s.hll_cap = (uint32_t)cap;
       s.hll_lists = c->d_hll_lists;
       s.hll_counts = c->d_hll_counts;
+      s.hll_cap2 = (uint32_t)cap2;
+      s.hll_lists2 = c->d_hll_lists2;
+      s.hll_counts2 = c->d_hll_counts2;
     }
     HIPCHK(c, launch_sketch(s, c->stream));
   }
@@ -916,6 +936,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_sp_lists);
   dev_free(c->d_sp_counts);
   dev_free(c->d_hll_lists);
+  dev_free(c->d_hll_lists2);
+  dev_free(c->d_hll_counts2);
   dev_free(c->d_hll_counts);
   dev_free(c->d_decode_oor);
   for (auto &st : c->stg) {
