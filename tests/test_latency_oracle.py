@@ -53,7 +53,7 @@ def test_filters_and_second_wrap():
     m.process_flow(_flow(t + 2_000_000, api, node, 443, 1000, 2, 1, 1, 9))
     assert m.latency.count == 1 and m.latency.total == -998.0
     assert m.latency.buckets[0] == 1
-    assert m.no_response == 0 and len(m.cache) == 1  # the tcp-id-7 flow never entered
+    assert m.no_response is None and not m.cache  # ignored flows never entered
 
 
 def test_go_round_half_away_from_zero():
