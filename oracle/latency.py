@@ -3,7 +3,7 @@
 Follows pkg/module/metrics/latency.go of the reference:
   * NewLatencyMetrics / Init (:73-150): three metrics, selected by name
     `node_apiserver_latency` (histogram adv_node_apiserver_latency),
-    `node_apiserver_tcp_handshake_latency` (histogram adv_node_apiserver_tcp_handshake_latency),
+    `node_apiserver_handshake_latency` (histogram adv_node_apiserver_tcp_handshake_latency),
     `node_apiserver_no_response` (counter vec adv_node_apiserver_no_response, label
     "no_response"); histograms use prometheus.LinearBuckets(0, 0.5, 10) (:35-39);
   * ProcessFlow (:178-201): TCP with a non-zero TCP id (utils.GetTCPID, flow_utils.go:176-183)
@@ -39,7 +39,7 @@ LIMIT = 100_000             # latency.go:35
 BUCKETS = [0.5 * i for i in range(10)]  # LinearBuckets(start 0, width 0.5, count 10)
 
 LATENCY = "node_apiserver_latency"
-HANDSHAKE = "node_apiserver_tcp_handshake_latency"
+HANDSHAKE = "node_apiserver_handshake_latency"  # utils/metric_names.go:29
 NO_RESPONSE = "node_apiserver_no_response"
 FAMILY = {
     LATENCY: ("networkobservability_adv_node_apiserver_latency", "Latency of node apiserver in ms"),

@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "libgpuagg.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["gpuagg_kernels.hip", "gpuagg_decode.hip", "gpuagg_runtime.cpp"]
+SOURCES = ["gpuagg_kernels.hip", "gpuagg_decode.hip", "gpuagg_latency.hip", "gpuagg_runtime.cpp"]
 HEADERS = ["gpuagg_internal.h", "gpuagg_launch.h", os.path.join("..", "..", "include", "gpuagg.h")]
 
 
@@ -43,9 +43,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I", CSRC,
               "-I", os.path.join(ROOT, "include")]
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS]
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(CSRC, os.path.splitext(s)[0] + ".o")
+        objs.append(obj)
+        if not force and _newer(obj, [src] + hdrs):  # up to date: reuse the object
+            continue
         if s.endswith(".hip"):
             cmd = [HIPCC, "--offload-arch=" + ARCH, "-munsafe-fp-atomics"] + common + ["-c", src, "-o", obj]
         else:
@@ -54,7 +58,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-        objs.append(obj)
     tmp = LIB + ".tmp"
     _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
          + ["-Wl,--version-script=" + os.path.join(CSRC, "gpuagg.map")])

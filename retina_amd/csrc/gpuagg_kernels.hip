@@ -1128,6 +1128,10 @@ struct SketchK {
   uint32_t hll_slots; // slots covered by the registers
   const uint8_t *ipl; // LDS image of every pod IP (source lookups), or null: HBM table
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  // LDS staging of list appends (sketch_stage_kernel): per count-min window sbc u16 and
+  // per HLL super-window sbh u32 entries (powers of two), flushed every `round` records
+  // per lane (2 or 4) as contiguous runs
+  uint32_t sbc, sbh, round;
 };
 
 // Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
@@ -1270,6 +1274,155 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
     const uint32_t s = k.src[i];
     L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i],
              kLdsIp ? lds_lookup(s) : k.p ? ip_lookup(k.t, s) : none);
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
+    k.counts[(size_t)blockIdx.x * k.nwin + w] = wcnt[w] < k.cap ? wcnt[w] : k.cap;
+  for (uint32_t w = threadIdx.x; w < k.hnsup; w += blockDim.x)
+    k.hcounts[(size_t)blockIdx.x * k.hnsup + w] = hcnt[w] < k.hcap ? hcnt[w] : k.hcap;
+}
+
+// Staged scatter (the default when LDS allows): appends land in per-window LDS staging
+// rings and are written out as contiguous runs once per round, so every list write is a
+// coalesced wave store instead of one L2 request per 2- or 4-byte entry (PMC on the
+// unstaged kernel: 45 B written per record for 12 B of list entries).  Positions are
+// reserved exactly as in the unstaged kernel, so the lists are identical; an entry whose
+// position is past the staging ring is stored directly, a full list falls back to the
+// global atomic.
+struct StagedLists {
+  const SketchK &k;
+  uint32_t *wcnt, *hcnt, *wfl, *hfl;  // fill counters and flushed positions (LDS)
+  uint16_t *cst;                      // [nwin][sbc] staging (LDS)
+  uint32_t *hst;                      // [hnsup][sbh] staging (LDS)
+  uint16_t *mine;
+  uint32_t *hmine;
+  uint32_t wmask, hi_bits, omask;
+  __device__ __forceinline__ void record(uint32_t s, uint32_t d, uint32_t ports, uint32_t meta,
+                                         const Lk &ls, bool stage) const {
+    if (k.depth) {
+      const uint64_t base = cms_base(s, d, ports, meta_proto(meta));
+#pragma unroll 4
+      for (uint32_t r = 0; r < k.depth; ++r) {
+        const uint32_t col = cms_col(base, r, wmask);
+        const uint32_t w = (r << hi_bits) | (col >> k.wshift);
+        const uint32_t pos = atomicAdd(&wcnt[w], 1u);
+        const uint16_t e = (uint16_t)(col & omask);
+        if (pos >= k.cap) atomicAdd(&k.cms[((size_t)r << k.wlog2) + col], 1u);
+        else if (stage && pos - wfl[w] < k.sbc) cst[w * k.sbc + (pos & (k.sbc - 1u))] = e;
+        else mine[(size_t)w * k.cap + pos] = e;
+      }
+    }
+    if (k.p && ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
+      const uint64_t h = hll_hash(d);
+      const uint32_t idx = (uint32_t)(h >> (64 - k.p));
+      const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
+      const uint32_t w = (uint32_t)ls.slot >> k.hsshift;
+      const uint32_t pos = atomicAdd(&hcnt[w], 1u);
+      const uint32_t e = (((uint32_t)ls.slot & ((1u << k.hsshift) - 1u)) << (k.p + 6)) | (idx << 6) | rho;
+      if (pos >= k.hcap) hll_update(k.hll, k.p, ls.slot, d);
+      else if (stage && pos - hfl[w] < k.sbh) hst[w * k.sbh + (pos & (k.sbh - 1u))] = e;
+      else hmine[(size_t)w * k.hcap + pos] = e;
+    }
+  }
+  // all threads, between barriers: write each window's staged run [flushed, filled)
+  __device__ __forceinline__ void flush() const {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    for (uint32_t w = wave; w < k.nwin; w += nwaves) {
+      const uint32_t f = wfl[w], c = min(wcnt[w], k.cap), e = min(c, f + k.sbc);
+      for (uint32_t p = f + lane; p < e; p += 64) mine[(size_t)w * k.cap + p] = cst[w * k.sbc + (p & (k.sbc - 1u))];
+      if (lane == 0) wfl[w] = c;
+    }
+    for (uint32_t w = wave; w < k.hnsup; w += nwaves) {
+      const uint32_t f = hfl[w], c = min(hcnt[w], k.hcap), e = min(c, f + k.sbh);
+      for (uint32_t p = f + lane; p < e; p += 64) hmine[(size_t)w * k.hcap + p] = hst[w * k.sbh + (p & (k.sbh - 1u))];
+      if (lane == 0) hfl[w] = c;
+    }
+  }
+};
+
+// LDS words of the staged kernel before the IP image (counters, flushed positions, rings)
+__host__ __device__ inline uint32_t stage_words(uint32_t nwin, uint32_t hnsup, uint32_t sbc, uint32_t sbh) {
+  return ((2u * (nwin + hnsup) + 3u) & ~3u) + ((nwin * sbc / 2u + 3u) & ~3u) + hnsup * sbh;
+}
+
+template <bool kLdsIp>
+__global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  uint32_t *wcnt = sm, *hcnt = sm + k.nwin, *wfl = hcnt + k.hnsup, *hfl = wfl + k.nwin;
+  uint16_t *cst = (uint16_t *)(sm + ((2u * (k.nwin + k.hnsup) + 3u) & ~3u));
+  uint32_t *hst = (uint32_t *)cst + ((k.nwin * k.sbc / 2u + 3u) & ~3u);
+  const uint32_t img_off = stage_words(k.nwin, k.hnsup, k.sbc, k.sbh);
+  const uint32_t *keys = sm + img_off;
+  const uint16_t *vals = (const uint16_t *)((const uint8_t *)keys + ipl_vals_offset(k.ipl_nb));
+  for (uint32_t i = threadIdx.x; i < 2u * (k.nwin + k.hnsup); i += blockDim.x) sm[i] = 0u;
+  if (kLdsIp)
+    for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
+      ((uint4 *)(sm + img_off))[i] = ((const uint4 *)k.ipl)[i];
+  __syncthreads();
+  auto lookup = [&](uint32_t ip) {
+    if (kLdsIp) {
+      const uint32_t v = vals[ipl_probe_index(keys, k.ipl_nb, k.ipl_seed, ip)];
+      return Lk{v == kIplNoSlot ? -1 : (int32_t)v, 0u};
+    }
+    return k.p ? ip_lookup(k.t, ip) : Lk{-1, 0};
+  };
+  const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
+  const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
+  const StagedLists L{k, wcnt, hcnt, wfl, hfl, cst, hst,
+                      k.lists + (size_t)blockIdx.x * k.nwin * k.cap,
+                      k.hlists + (size_t)blockIdx.x * k.hnsup * k.hcap, (1u << k.wlog2) - 1u,
+                      k.wlog2 - k.wshift, (1u << k.wshift) - 1u};
+  const bool need_ports = k.depth != 0 && k.ports;
+  uint64_t tail = start;
+  if (start + 4 <= end) {
+    const uint64_t v0 = start >> 2, vend = v0 + ((end - start) >> 2);
+    const uint4 *s4 = (const uint4 *)k.src, *d4 = (const uint4 *)k.dst;
+    const uint4 *p4 = (const uint4 *)k.ports, *m4 = (const uint4 *)k.meta;
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint4 ns = z4, nd = z4, nm = z4, np = z4;
+    if (v0 + threadIdx.x < vend) {
+      const uint64_t v = v0 + threadIdx.x;
+      ns = s4[v];
+      nd = d4[v];
+      nm = m4[v];
+      np = need_ports ? p4[v] : z4;
+    }
+    // block-uniform trip count: every thread reaches the flush barriers
+    for (uint64_t vb = v0; vb < vend; vb += blockDim.x) {
+      const uint64_t v = vb + threadIdx.x;
+      const bool act = v < vend;
+      const uint4 vs = ns, vd = nd, vm = nm, vp = np;
+      const uint64_t vn = v + blockDim.x;
+      if (vn < vend) {
+        ns = s4[vn];
+        nd = d4[vn];
+        nm = m4[vn];
+        np = need_ports ? p4[vn] : z4;
+      }
+      if (act) {
+        const Lk l0 = lookup(vs.x), l1 = lookup(vs.y);
+        L.record(vs.x, vd.x, vp.x, vm.x, l0, true);
+        L.record(vs.y, vd.y, vp.y, vm.y, l1, true);
+      }
+      if (k.round == 2) {
+        __syncthreads();
+        L.flush();
+        __syncthreads();
+      }
+      if (act) {
+        const Lk l2 = lookup(vs.z), l3 = lookup(vs.w);
+        L.record(vs.z, vd.z, vp.z, vm.z, l2, true);
+        L.record(vs.w, vd.w, vp.w, vm.w, l3, true);
+      }
+      __syncthreads();
+      L.flush();
+      __syncthreads();
+    }
+    tail = start + ((end - start) & ~3ULL);
+  }
+  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {  // < 4 records: unstaged
+    const uint32_t s = k.src[i];
+    L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i], lookup(s), false);
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
@@ -1439,6 +1592,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   k.hlists2 = a.hll_lists2;
   k.hcounts2 = a.hll_counts2;
   k.hll_slots = a.hll_slots;
+  hipError_t e;
   size_t scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   // source lookups in an LDS image of the IP table when it fits next to the counters
   const bool lds_ip = a.ipl && a.hll_p && scatter_lds + a.ipl_bytes <= kLdsBytes;
@@ -1452,11 +1606,39 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   // 16-byte loads need aligned columns and workgroup chunks of whole vectors
   const bool vec = a.chunk % 4 == 0 && ((uintptr_t)k.src | (uintptr_t)k.dst | (uintptr_t)k.meta |
                                         (uintptr_t)(k.ports ? k.ports : k.src)) % 16 == 0;
+  // staged scatter: rings sized for one round's expected appends x 2 (+ 64), flushed every
+  // 4 records per lane, or every 2 when the 4-record rings do not fit
+  bool staged = false;
+  if (vec && (!a.cms_depth || a.nwin) && (!a.hll_p || a.hll_nsup) && (a.nwin || a.hll_nsup)) {
+    const uint32_t img = lds_ip ? a.ipl_bytes : 0u;
+    for (uint32_t round : {4u, 2u}) {
+      const uint64_t per_round = 1024ull * round;
+      auto ring = [](uint64_t mean) {
+        uint32_t r = 64;
+        while (r < 2 * mean + 64) r <<= 1;
+        return r;
+      };
+      const uint32_t sbc = a.nwin ? ring(per_round * a.cms_depth / a.nwin) : 0u;
+      const uint32_t sbh = a.hll_nsup ? ring(per_round / a.hll_nsup) : 0u;
+      const size_t lds = (size_t)stage_words(a.nwin, a.hll_nsup, sbc, sbh) * 4 + img;
+      if (lds > kLdsBytes) continue;
+      k.sbc = sbc;
+      k.sbh = sbh;
+      k.round = round;
+      const void *fn = lds_ip ? (const void *)sketch_stage_kernel<true> : (const void *)sketch_stage_kernel<false>;
+      if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
+      if (lds_ip) hipLaunchKernelGGL((sketch_stage_kernel<true>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else hipLaunchKernelGGL((sketch_stage_kernel<false>), dim3(a.blocks), dim3(1024), lds, st, k);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      staged = true;
+      break;
+    }
+  }
+  if (!staged) {
   const void *fn = vec ? (lds_ip ? (const void *)sketch_scatter_kernel<true, true>
                                  : (const void *)sketch_scatter_kernel<true, false>)
                        : (lds_ip ? (const void *)sketch_scatter_kernel<false, true>
                                  : (const void *)sketch_scatter_kernel<false, false>);
-  hipError_t e;
   if (scatter_lds > 64 * 1024 &&
       (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scatter_lds)) != hipSuccess)
     return e;
@@ -1465,6 +1647,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   else if (lds_ip) hipLaunchKernelGGL((sketch_scatter_kernel<false, true>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   else hipLaunchKernelGGL((sketch_scatter_kernel<false, false>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  }  // unstaged
   if (a.nwin && a.cms_depth) {
     const size_t lds = (size_t)4 << a.win_shift;
     if (lds > 64 * 1024 &&
