@@ -168,9 +168,16 @@ int gpuagg_dns_intern(gpuagg_ctx *ctx, uint32_t rcode, const char *qtypes_joined
  *                  bits 21-26 TCP flags FIN,SYN,RST,PSH,ACK,URG (types_linux.go:22-31)
  *                  bit  27    IsReply
  *                  bits 28-29 RetinaMetadata.DnsType (0 UNKNOWN, 1 QUERY, 2 RESPONSE)
+ *                  bits 30-31 observation point passed to ToFlow, values 0-3
+ *                             (2 FROM_NETWORK, 3 TO_NETWORK; flow_utils.go:72-92); any
+ *                             other point is written as 0 (only 2 and 3 are read)
  *  ports           source port | destination port << 16 (host order, as in flow.L4)
  *  dns_id          gpuagg_dns_intern id (DNS verdict rows only; 0xFFFFFFFF reserved)
- * ports / dns_id may be NULL when no enabled metric reads them.
+ *  tcp_id          RetinaMetadata.TcpId: TSval on TO_NETWORK, TSecr on FROM_NETWORK,
+ *                  else 0 (packetparser_linux.go:622-628)
+ *  time_ns         the record time ToFlow receives (flow.Time; u64 nanoseconds)
+ * ports / dns_id / tcp_id / time_ns may be NULL when no enabled metric reads them
+ * (tcp_id and time_ns: the node-apiserver latency metrics).
  * ---------------------------------------------------------------------------- */
 typedef struct gpuagg_columns {
   uint32_t *src_ip;
@@ -179,6 +186,8 @@ typedef struct gpuagg_columns {
   uint32_t *meta;
   uint32_t *ports;
   uint32_t *dns_id;
+  uint32_t *tcp_id;
+  uint64_t *time_ns;
 } gpuagg_columns;
 
 /* Library-owned pinned host batch (the enricher's input ring, enricher.go:45). */
@@ -315,6 +324,33 @@ int gpuagg_state(gpuagg_ctx *ctx, gpuagg_state_desc *out);
 int gpuagg_sparse_export(gpuagg_ctx *ctx, uint64_t *dev_out, size_t cap, size_t *n_out);
 /* Inserts-and-adds n exported entries (device pointer) into this ctx's table. */
 int gpuagg_sparse_import(gpuagg_ctx *ctx, const uint64_t *dev_in, size_t n);
+
+/* ------------------------------------------------------------------------------
+ * Node-apiserver latency (pkg/module/metrics/latency.go).  Enabled by the metric names
+ * node_apiserver_latency, node_apiserver_handshake_latency and
+ * node_apiserver_no_response in gpuagg_reconcile (utils/metric_names.go:28-30); reads
+ * ports, tcp_id, time_ns and the observation point of meta.  The TTL join runs on the
+ * GPU per batch (gpuagg_latency.hip); its clock is the running maximum of the record
+ * times (the reference's cleaner runs on the wall clock), requests still pending carry
+ * over to the next batch.  With latency metrics enabled a submit waits for its batch's
+ * event count (one small device-to-host read) before sorting the events.
+ * ---------------------------------------------------------------------------- */
+/* The apiserver IP set (apiserverWatcherCallbackFn, latency.go:307-346); at most 64. */
+int gpuagg_set_apiserver_ips(gpuagg_ctx *ctx, const uint32_t *ipv4, size_t n);
+
+typedef struct gpuagg_latency_state {
+  uint32_t enabled;                 /* bit 0 latency, 1 handshake latency, 2 no_response */
+  uint64_t latency_buckets[11];     /* per bucket (not cumulative): le 0, 0.5, ..., 4.5, +Inf */
+  uint64_t latency_count;
+  int64_t latency_sum;              /* ms; observations are integers (math.Round)         */
+  uint64_t handshake_buckets[11];
+  uint64_t handshake_count;
+  int64_t handshake_sum;
+  uint64_t no_response;             /* entries that expired unanswered                   */
+  uint64_t pending;                 /* requests waiting for a reply (carried over)        */
+} gpuagg_latency_state;
+
+int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);
 
 /* ------------------------------------------------------------------------------
  * Introspection

@@ -1132,6 +1132,7 @@ struct SketchK {
   // per HLL super-window sbh u32 entries (powers of two), flushed every `round` records
   // per lane (2 or 4) as contiguous runs
   uint32_t sbc, sbh, round;
+  uint32_t sbs;  // hll_split_kernel staging ring per fine window (0: unstaged)
 };
 
 // Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
@@ -1435,10 +1436,15 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
 // super-window s and appends each entry to its fine window's list (s, b, fine window);
 // a full list applies the entry with the global CAS (exact).
 __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_lists) {
+  // LDS: [nfine] fill counters, [nfine] flushed positions, then (k.sbs) [nfine][sbs]
+  // staging rings: a round of 4096 entries is appended, then written out per fine window
+  // as contiguous runs (as in sketch_stage_kernel)
   extern __shared__ __attribute__((aligned(16))) uint32_t fcnt[];
   const uint32_t s = blockIdx.x / k.hb2, b = blockIdx.x % k.hb2;
   const uint32_t fshift = k.hsshift - k.hshift, nfine = 1u << fshift;
-  for (uint32_t i = threadIdx.x; i < nfine; i += blockDim.x) fcnt[i] = 0u;
+  uint32_t *ffl = fcnt + nfine, *ring = fcnt + 2 * nfine;
+  const uint32_t R = k.sbs;
+  for (uint32_t i = threadIdx.x; i < 2 * nfine; i += blockDim.x) fcnt[i] = 0u;
   __syncthreads();
   const size_t base2 = ((size_t)s * k.hb2 + b) * nfine;
   uint32_t *out = k.hlists2 + base2 * k.hcap2;
@@ -1447,7 +1453,8 @@ __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_l
     const uint32_t pod = (x >> psh) & pmask, wf = pod >> k.hshift;
     const uint32_t pos = atomicAdd(&fcnt[wf], 1u);
     if (pos < k.hcap2) {
-      out[(size_t)wf * k.hcap2 + pos] = x;
+      if (R && pos - ffl[wf] < R) ring[wf * R + (pos & (R - 1u))] = x;
+      else out[(size_t)wf * k.hcap2 + pos] = x;
       return;
     }
     const uint32_t slot = (s << k.hsshift) | pod;  // full list: the global CAS
@@ -1461,17 +1468,44 @@ __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_l
       old = prev;
     }
   };
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  auto flush = [&]() {
+    for (uint32_t w = wave; w < nfine; w += nwaves) {
+      const uint32_t f = ffl[w], c = min(fcnt[w], k.hcap2), e = min(c, f + R);
+      for (uint32_t p = f + lane; p < e; p += 64) out[(size_t)w * k.hcap2 + p] = ring[w * R + (p & (R - 1u))];
+      if (lane == 0) ffl[w] = c;
+    }
+  };
   for (uint32_t l = b; l < n_lists; l += k.hb2) {
-    const uint32_t cnt = k.hcounts[(size_t)l * k.hnsup + s];
+    const uint32_t cnt = k.hcounts[(size_t)l * k.hnsup + s];  // block-uniform
     const uint32_t *e = k.hlists + ((size_t)l * k.hnsup + s) * k.hcap;  // 16-byte aligned (hcap % 16 == 0)
-    const uint32_t n4 = cnt >> 2;
-    walk_u4((const uint4 *)e, n4, threadIdx.x, blockDim.x, [&](const uint4 &v) {
-      put(v.x);
-      put(v.y);
-      put(v.z);
-      put(v.w);
-    });
-    for (uint32_t j = (n4 << 2) + threadIdx.x; j < cnt; j += blockDim.x) put(e[j]);
+    if (!R) {
+      const uint32_t n4 = cnt >> 2;
+      walk_u4((const uint4 *)e, n4, threadIdx.x, blockDim.x, [&](const uint4 &v) {
+        put(v.x);
+        put(v.y);
+        put(v.z);
+        put(v.w);
+      });
+      for (uint32_t j = (n4 << 2) + threadIdx.x; j < cnt; j += blockDim.x) put(e[j]);
+      continue;
+    }
+    // rounds of 4 entries per thread (one 16-byte load), staged and flushed
+    for (uint32_t r0 = 0; r0 < cnt; r0 += 4 * blockDim.x) {
+      const uint32_t j = r0 + 4 * threadIdx.x;
+      if (j + 4 <= cnt) {
+        const uint4 v = *(const uint4 *)(e + j);
+        put(v.x);
+        put(v.y);
+        put(v.z);
+        put(v.w);
+      } else {
+        for (uint32_t q = j; q < cnt; ++q) put(e[q]);
+      }
+      __syncthreads();
+      flush();
+      __syncthreads();
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nfine; i += blockDim.x)
@@ -1658,8 +1692,17 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (a.hll_nsup && a.hll_p) {
-    hipLaunchKernelGGL(hll_split_kernel, dim3(a.hll_nsup * a.hll_b2), dim3(1024),
-                       (size_t)4 << (a.hll_sshift - a.hll_shift), st, k, a.blocks);
+    // staging rings: a round (4096 entries) over nfine windows, x 2 + 64, when they fit
+    const uint32_t nfine = 1u << (a.hll_sshift - a.hll_shift);
+    uint32_t R = 64;
+    while (R < 2 * 4096 / nfine + 64) R <<= 1;
+    if ((size_t)(2 + R) * nfine * 4 > kLdsBytes) R = 0;
+    k.sbs = R;
+    const size_t split_lds = (size_t)(2 + R) * nfine * 4;
+    if ((e = hipFuncSetAttribute((const void *)hll_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)split_lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(hll_split_kernel, dim3(a.hll_nsup * a.hll_b2), dim3(1024), split_lds, st, k, a.blocks);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t lds = (size_t)1 << (a.hll_p + a.hll_shift);
     if (lds > 64 * 1024 &&

@@ -1,0 +1,298 @@
+// Node-apiserver latency on the GPU: the TTL join of pkg/module/metrics/latency.go.
+//
+// Reference (per flow, one goroutine): ProcessFlow (:178-201) keeps TCP flows with a
+// non-zero TCP id (TSval on TO_NETWORK, TSecr on FROM_NETWORK, packetparser_linux.go:
+// 622-628) whose source or destination is an apiserver IP; calculateLatency (:256-305)
+// inserts {src, dst, sport, dport, id} -> (Time.Nanos, flags) on TO_NETWORK unless the key
+// is present, and on FROM_NETWORK looks up the mirrored key, observes round(dNanos / 1e6)
+// ms, observes the handshake latency for a SYN answered by SYN+ACK, and deletes the key;
+// entries that outlive the 500 ms TTL count one no_response (:123-131).
+//
+// Batch form (oracle/latency.py states it): the clock is the running maximum of the
+// record times; an entry expires before the first record whose clock passes its expiry.
+// The join is independent per key, so the batch is processed as
+//   1. lat_count_kernel   per-workgroup event counts and max record time;
+//   2. lat_scan_kernel    exclusive scans of both (one workgroup), batch end clock;
+//   3. lat_emit_kernel    events in record order, each with its clock (block scans);
+//      lat_carry_kernel   entries still pending from earlier batches go first;
+//   4. rocprim radix sort of the events by key hash (stable: record order per key);
+//   5. lat_walk_kernel    one lane per key runs the TTL-cache state machine over its
+//                         events and books histogram buckets / no_response with atomics;
+//                         live entries carry over to the next batch.
+// Latency traffic is a small share of a node's records; the filter pass (1, 3) streams
+// 36 B per record (src, dst, meta, ports, tcp_id, time_ns).
+#include <cstring>  // rocprim's texture iterator uses memset
+
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include "gpuagg_internal.h"
+#include "gpuagg_launch.h"
+
+namespace gpuagg {
+
+constexpr uint32_t kLatThreads = 256;
+constexpr uint32_t kRoleReq = 1, kRoleRep = 2, kRoleCarry = 3;
+
+__device__ __forceinline__ bool lat_is_api(const uint32_t *api, uint32_t n_api, uint32_t ip) {
+  bool hit = false;
+  for (uint32_t i = 0; i < n_api; ++i) hit |= api[i] == ip;
+  return hit;
+}
+
+// Event role of record i (0: not a latency event).  ToFlow gives L4 TCP for protocol 6
+// (flow_utils.go:42-62); the observation point is meta bits 30-31.
+__device__ __forceinline__ uint32_t lat_role(const LatArgs &a, const uint32_t *api, size_t i) {
+  const uint32_t m = a.meta[i];
+  if ((m & 0xFFu) != 6u || a.tcp_id[i] == 0u) return 0u;
+  const uint32_t obs = m >> 30;
+  const uint32_t role = obs == 3u ? kRoleReq : obs == 2u ? kRoleRep : 0u;
+  if (!role) return 0u;
+  return (lat_is_api(api, a.n_api, a.src[i]) || lat_is_api(api, a.n_api, a.dst[i])) ? role : 0u;
+}
+
+__device__ __forceinline__ uint64_t lat_hash(uint64_t k0, uint64_t k1) {
+  return fmix64(k0 ^ fmix64(k1 ^ 0x9E3779B97F4A7C15ULL));
+}
+
+__global__ __launch_bounds__(kLatThreads) void lat_count_kernel(LatArgs a) {
+  __shared__ uint32_t api[kLatMaxApi];
+  __shared__ uint32_t cnt_w[kLatThreads / 64];
+  __shared__ unsigned long long max_w[kLatThreads / 64];
+  if (threadIdx.x < a.n_api) api[threadIdx.x] = a.api[threadIdx.x];
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * a.chunk, hi = min(lo + a.chunk, a.n);
+  uint32_t cnt = 0;
+  unsigned long long mx = 0;
+  for (size_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    cnt += lat_role(a, api, i) != 0u;
+    mx = max(mx, (unsigned long long)a.time_ns[i]);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    cnt_w[threadIdx.x >> 6] = cnt;
+    max_w[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    unsigned long long m = 0;
+    for (uint32_t w = 0; w < kLatThreads / 64; ++w) {
+      c += cnt_w[w];
+      m = max(m, max_w[w]);
+    }
+    a.blk_cnt[blockIdx.x] = c;
+    a.blk_max[blockIdx.x] = m;
+  }
+}
+
+// One workgroup: exclusive scans over the (<= a few thousand) count workgroups.
+__global__ void lat_scan_kernel(LatArgs a) {
+  if (threadIdx.x != 0) return;
+  unsigned long long *st = a.state;
+  uint64_t base = st[kLatPending];  // carried entries occupy [0, pending)
+  unsigned long long clk = st[kLatClock];
+  for (uint32_t b = 0; b < a.blocks; ++b) {
+    a.blk_base[b] = base;
+    a.blk_clk[b] = clk;
+    base += a.blk_cnt[b];
+    clk = max(clk, a.blk_max[b]);
+  }
+  st[kLatEvents] = base;
+  st[kLatClockEnd] = clk;
+  st[kLatCarryOut] = 0ULL;
+}
+
+// Events in record order: each 256-record round is scanned in LDS (event ranks and the
+// running max of the record times) so event e carries clock = max time of records <= e.
+__global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
+  __shared__ uint32_t api[kLatMaxApi];
+  __shared__ uint32_t cnt_w[kLatThreads / 64];
+  __shared__ unsigned long long max_w[kLatThreads / 64];
+  if (threadIdx.x < a.n_api) api[threadIdx.x] = a.api[threadIdx.x];
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * a.chunk, hi = min(lo + a.chunk, a.n);
+  uint64_t base = a.blk_base[blockIdx.x];
+  unsigned long long clk = a.blk_clk[blockIdx.x];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (size_t r = lo; r < hi; r += blockDim.x) {
+    const size_t i = r + threadIdx.x;
+    const bool in = i < hi;
+    const uint32_t role = in ? lat_role(a, api, i) : 0u;
+    const unsigned long long t = in ? (unsigned long long)a.time_ns[i] : 0ULL;
+    // wave-inclusive max scan of t, wave rank of events
+    unsigned long long m = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(m, o);
+      if (lane >= (uint32_t)o) m = max(m, y);
+    }
+    const uint64_t ball = __ballot(role != 0u);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
+    if (lane == 63) {
+      cnt_w[wave] = (uint32_t)__popcll(ball);
+      max_w[wave] = m;
+    }
+    __syncthreads();
+    uint64_t off = base;
+    unsigned long long c = clk;
+    for (uint32_t w = 0; w < wave; ++w) {
+      off += cnt_w[w];
+      c = max(c, max_w[w]);
+    }
+    c = max(c, m);
+    if (role) {
+      const uint32_t s = a.src[i], d = a.dst[i], p = a.ports[i];
+      const uint64_t id = a.tcp_id[i];
+      const uint32_t sp = p & 0xFFFFu, dp = p >> 16;
+      // request key {src, dst, sport, dport, id}; a reply looks up the mirrored key
+      const uint64_t k0 = role == kRoleReq ? ((uint64_t)s | ((uint64_t)d << 32)) : ((uint64_t)d | ((uint64_t)s << 32));
+      const uint64_t k1 = role == kRoleReq ? ((uint64_t)sp | ((uint64_t)dp << 16) | (id << 32))
+                                           : ((uint64_t)dp | ((uint64_t)sp << 16) | (id << 32));
+      const uint32_t m8 = a.meta[i], verdict = (m8 >> 8) & 0xFFu, flags = (m8 >> 21) & 0x3Fu;
+      // AddTCPFlags: packetparser sets them on every TCP flow (forwarded); SYN bit 1, ACK bit 4
+      const bool has_flags = verdict == kVerdictForwarded || verdict == kVerdictRetrans;
+      const uint32_t bits = role | ((has_flags && (flags & 2u)) ? 4u : 0u) | ((has_flags && (flags & 16u)) ? 8u : 0u);
+      const uint64_t e = off + rank;
+      a.ev[e] = LatEvent{k0, k1, c, (uint32_t)((uint64_t)a.time_ns[i] % 1000000000ULL), bits};
+      a.hash_in[e] = lat_hash(k0, k1);
+      a.idx_in[e] = (uint32_t)e;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < kLatThreads / 64; ++w) {
+      base += cnt_w[w];
+      clk = max(clk, max_w[w]);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void lat_carry_kernel(LatArgs a) {
+  const uint64_t n = a.state[kLatPending];
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x) {
+    const LatEvent c = a.carry_in[e];
+    a.ev[e] = c;
+    a.hash_in[e] = lat_hash(c.k0, c.k1);
+    a.idx_in[e] = (uint32_t)e;
+  }
+}
+
+// Histogram bucket of an integer latency (LinearBuckets(0, 0.5, 10): le 0, 0.5, ..., 4.5).
+__device__ __forceinline__ uint32_t lat_bucket(int64_t v) {
+  if (v <= 0) return 0u;
+  return v >= 5 ? 10u : (uint32_t)(2 * v);
+}
+
+__global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32_t enabled) {
+  const uint64_t n = a.state[kLatEvents];
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long h = a.hash_out[i];
+  if (i > 0 && a.hash_out[i - 1] == h) return;  // not a segment start
+  uint64_t j = i + 1;
+  while (j < n && a.hash_out[j] == h) ++j;
+  const unsigned long long clk_end = a.state[kLatClockEnd];
+  unsigned long long *st = a.state;
+  // one pass per distinct exact key of the segment (a 64-bit hash collision is the only
+  // way a segment holds two); events of a key in record order (stable sort)
+  for (uint64_t p = i; p < j; ++p) {
+    const LatEvent ep = a.ev[a.idx_out[p]];
+    bool seen = false;
+    for (uint64_t q = i; q < p && !seen; ++q) {
+      const LatEvent eq = a.ev[a.idx_out[q]];
+      seen = eq.k0 == ep.k0 && eq.k1 == ep.k1;
+    }
+    if (seen) continue;
+    bool live = false, syn = false;
+    unsigned long long expires = 0;
+    uint32_t nanos = 0;
+    for (uint64_t q = p; q < j; ++q) {
+      const LatEvent e = a.ev[a.idx_out[q]];
+      if (e.k0 != ep.k0 || e.k1 != ep.k1) continue;
+      const uint32_t role = e.bits & 3u;
+      if (role == kRoleCarry) {  // pending from an earlier batch: first in order
+        live = true;
+        expires = e.clock;
+        nanos = e.nanos;
+        syn = (e.bits >> 2) & 1u;
+        continue;
+      }
+      if (live && e.clock > expires) {  // the cleaner evicted it before this record
+        live = false;
+        if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
+      }
+      if (role == kRoleReq) {
+        if (!live) {
+          live = true;
+          expires = e.clock + kLatTtlNs;
+          nanos = e.nanos;
+          syn = (e.bits >> 2) & 1u;
+        }
+      } else if (live) {  // reply: latency of the first reply, then Delete
+        const int64_t d = (int64_t)e.nanos - (int64_t)nanos;
+        const int64_t ad = d < 0 ? -d : d;
+        const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
+        const uint32_t bk = lat_bucket(lat);
+        if (enabled & 1u) {
+          atomicAdd(&st[kLatHist + bk], 1ULL);
+          atomicAdd(&st[kLatHist + 11], 1ULL);
+          atomicAdd(&st[kLatHist + 12], (unsigned long long)lat);
+        }
+        if ((enabled & 2u) && syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
+          atomicAdd(&st[kLatHandshake + bk], 1ULL);
+          atomicAdd(&st[kLatHandshake + 11], 1ULL);
+          atomicAdd(&st[kLatHandshake + 12], (unsigned long long)lat);
+        }
+        live = false;
+      }
+    }
+    if (!live) continue;
+    if (clk_end > expires) {
+      if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
+    } else {
+      const unsigned long long o = atomicAdd(&st[kLatCarryOut], 1ULL);
+      a.carry_out[o] = LatEvent{ep.k0, ep.k1, expires, nanos, kRoleCarry | (syn ? 4u : 0u)};
+    }
+  }
+}
+
+__global__ void lat_finish_kernel(unsigned long long *st) {
+  st[kLatClock] = st[kLatClockEnd];
+  st[kLatPending] = st[kLatCarryOut];
+}
+
+// ---- host side ----------------------------------------------------------------------
+hipError_t launch_latency_front(const LatArgs &a, hipStream_t st) {
+  hipLaunchKernelGGL(lat_count_kernel, dim3(a.blocks), dim3(kLatThreads), 0, st, a);
+  hipLaunchKernelGGL(lat_scan_kernel, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(lat_emit_kernel, dim3(a.blocks), dim3(kLatThreads), 0, st, a);
+  hipLaunchKernelGGL(lat_carry_kernel, dim3(64), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t latency_sort_bytes(size_t n, size_t *bytes) {
+  return rocprim::radix_sort_pairs(nullptr, *bytes, (const unsigned long long *)nullptr,
+                                   (unsigned long long *)nullptr, (const uint32_t *)nullptr,
+                                   (uint32_t *)nullptr, n, 0, 64, (hipStream_t)0);
+}
+
+hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
+                               uint32_t enabled, hipStream_t st) {
+  hipError_t e;
+  if (n_events) {
+    size_t tb = tmp_bytes;
+    if ((e = rocprim::radix_sort_pairs(tmp, tb, a.hash_in, a.hash_out, a.idx_in, a.idx_out, n_events, 0, 64,
+                                       st)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(lat_walk_kernel, dim3((uint32_t)((n_events + kLatThreads - 1) / kLatThreads)),
+                       dim3(kLatThreads), 0, st, a, enabled);
+  }
+  hipLaunchKernelGGL(lat_finish_kernel, dim3(1), dim3(1), 0, st, a.state);
+  return hipGetLastError();
+}
+
+}  // namespace gpuagg

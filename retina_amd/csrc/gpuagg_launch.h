@@ -10,6 +10,8 @@ namespace gpuagg {
 
 struct ColsView {
   const uint32_t *src_ip, *dst_ip, *bytes, *meta, *ports, *dns_id;
+  const uint32_t *tcp_id = nullptr;
+  const uint64_t *time_ns = nullptr;
 };
 
 struct SparseView {
@@ -63,6 +65,8 @@ struct LaunchArgs {
 enum RawKind : int { kRawPacket = 1, kRawDrop = 2 };
 struct OutCols {
   uint32_t *src_ip, *dst_ip, *bytes, *meta, *ports, *dns_id;  // ports / dns_id may be null
+  uint32_t *tcp_id = nullptr;   // latency columns, may be null
+  uint64_t *time_ns = nullptr;
 };
 struct DecodeArgs {
   int kind;
@@ -73,6 +77,46 @@ struct DecodeArgs {
   uint32_t n_cu;
 };
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
+
+// Node-apiserver latency join (gpuagg_latency.hip).
+struct LatEvent {
+  uint64_t k0, k1;   // request-oriented key: src | dst << 32, sport | dport << 16 | id << 32
+  uint64_t clock;    // record clock (carried entry: its expiry)
+  uint32_t nanos;    // Time.Nanos
+  uint32_t bits;     // role 1 request / 2 reply / 3 carried | SYN << 2 | ACK << 3
+};
+constexpr uint32_t kLatMaxApi = 64;
+constexpr uint64_t kLatTtlNs = 500000000ULL;  // latency.go:34
+// state words (u64): clock, pending carried entries, scratch, histograms, no_response
+enum : uint32_t {
+  kLatClock = 0, kLatPending = 1, kLatCarryOut = 2, kLatClockEnd = 3, kLatEvents = 4,
+  kLatHist = 8,        // 11 buckets (le 0, 0.5 .. 4.5, +Inf), count, sum (i64)
+  kLatHandshake = 24,  // same layout
+  kLatNoResponse = 40,
+  kLatStateWords = 48
+};
+struct LatArgs {
+  const uint32_t *src, *dst, *meta, *ports, *tcp_id;
+  const uint64_t *time_ns;
+  size_t n;
+  uint64_t chunk;
+  uint32_t blocks;
+  const uint32_t *api;
+  uint32_t n_api;
+  unsigned long long *state;
+  uint32_t *blk_cnt;
+  unsigned long long *blk_max, *blk_clk;
+  uint64_t *blk_base;
+  LatEvent *ev;
+  unsigned long long *hash_in, *hash_out;
+  uint32_t *idx_in, *idx_out;
+  const LatEvent *carry_in;
+  LatEvent *carry_out;
+};
+hipError_t launch_latency_front(const LatArgs &a, hipStream_t st);
+hipError_t latency_sort_bytes(size_t n, size_t *bytes);
+hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
+                               uint32_t enabled, hipStream_t st);
 
 // Sketch pass (count-min by window partition + HLL), after the metric kernels.
 struct SketchArgs {
