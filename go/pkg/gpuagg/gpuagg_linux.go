@@ -43,6 +43,8 @@ import (
 	kcfg "github.com/microsoft/retina/pkg/config"
 	"github.com/microsoft/retina/pkg/controllers/cache"
 	"github.com/microsoft/retina/pkg/exporter"
+	"github.com/microsoft/retina/pkg/ktime"
+	"github.com/microsoft/retina/pkg/pubsub"
 	"github.com/microsoft/retina/pkg/log"
 	"github.com/microsoft/retina/pkg/metrics"
 	"github.com/microsoft/retina/pkg/plugin/registry"
@@ -66,6 +68,8 @@ const (
 // tcpretrans.eventHandler) fill it instead of building a *flow.Flow.
 type Record struct {
 	SrcIP, DstIP, Bytes, Meta, Ports, DNSID uint32
+	TcpID  uint32 // RetinaMetadata.TcpId (latency metrics)
+	TimeNs uint64 // the time ToFlow receives (latency metrics)
 }
 
 // Raw perf-record kinds (GPUAGG_RAW_* of include/gpuagg.h): packetparser and
@@ -89,7 +93,8 @@ type device struct {
 	ctx   *C.gpuagg_ctx
 	batch *C.gpuagg_batch
 	n     int
-	cols  [6][]uint32
+	cols  [7][]uint32 // src, dst, bytes, meta, ports, dns_id, tcp_id
+	times []uint64
 }
 
 type gpuAgg struct {
@@ -199,7 +204,11 @@ func (g *gpuAgg) Init() error {
 		}
 		c := d.batch.cols
 		col := func(p *C.uint32_t) []uint32 { return unsafe.Slice((*uint32)(unsafe.Pointer(p)), batchCapacity) }
-		d.cols = [6][]uint32{col(c.src_ip), col(c.dst_ip), col(c.bytes), col(c.meta), col(c.ports), col(c.dns_id)}
+		d.cols = [7][]uint32{col(c.src_ip), col(c.dst_ip), col(c.bytes), col(c.meta), col(c.ports), col(c.dns_id),
+			col(c.tcp_id)}
+		d.times = unsafe.Slice((*uint64)(unsafe.Pointer(c.time_ns)), batchCapacity)
+		// raw records carry boot-time stamps; ToFlow adds ktime.MonotonicOffset (packetparser_linux.go:583-585)
+		C.gpuagg_set_time_offset(d.ctx, C.int64_t(ktime.MonotonicOffset.Nanoseconds()))
 		g.devs = append(g.devs, d)
 	}
 	g.stopping = false
@@ -288,7 +297,9 @@ func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
 	return nil
 }
 
-// shardOf is retina_amd/dist.py shard_of: fmix64 of the 5-tuple, mod the devices.
+// shardOf is retina_amd/dist.py shard_of: fmix64 of the direction-free 5-tuple (the
+// (ip, port) ends in order, so a request and its reply meet on one device for the
+// latency join), mod the devices.
 func shardOf(r *Record, n int) int {
 	if n == 1 {
 		return 0
@@ -301,9 +312,11 @@ func shardOf(r *Record, n int) int {
 		k ^= k >> 33
 		return k
 	}
-	lo := uint64(r.SrcIP) | uint64(r.DstIP)<<32
-	hi := uint64(r.Ports) | uint64(r.Meta&0xff)<<32
-	return int(fmix(lo^fmix(hi^0x1F2E3D4C5B6A7988)) % uint64(n))
+	a, b := uint64(r.SrcIP)<<16|uint64(r.Ports&0xffff), uint64(r.DstIP)<<16|uint64(r.Ports>>16)
+	if a > b {
+		a, b = b, a
+	}
+	return int(fmix(a^fmix(b^(uint64(r.Meta&0xff)<<48)^0x1F2E3D4C5B6A7988)) % uint64(n))
 }
 
 // Start blocks until ctx is done (PluginManager runs it in an errgroup goroutine,
@@ -376,8 +389,9 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		case r := <-g.records:
 			d := devs[shardOf(&r, len(devs))]
 			i := d.n
-			d.cols[0][i], d.cols[1][i], d.cols[2][i], d.cols[3][i], d.cols[4][i], d.cols[5][i] =
-				r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID
+			d.cols[0][i], d.cols[1][i], d.cols[2][i], d.cols[3][i], d.cols[4][i], d.cols[5][i], d.cols[6][i] =
+				r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID, r.TcpID
+			d.times[i] = r.TimeNs
 			d.n++
 			if d.n == batchCapacity {
 				if err := submit(d); err != nil {

@@ -352,6 +352,10 @@ typedef struct gpuagg_latency_state {
 
 int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);
 
+/* ktime.MonotonicOffset: added to the t_nsec / ts of raw records decoded on the GPU
+ * (ToFlow receives MonotonicOffset + T_nsec, packetparser_linux.go:583-585). */
+int gpuagg_set_time_offset(gpuagg_ctx *ctx, int64_t ns);
+
 /* ------------------------------------------------------------------------------
  * Introspection
  * ---------------------------------------------------------------------------- */

@@ -64,10 +64,14 @@ def decode_packets(raw: np.ndarray) -> Tuple[R.Batch, np.ndarray]:
     tdir = r["tdir"].astype(u)
     flags = np.where(proto == 6, r["flags"].astype(u) & u(0x3F), u(0))
     bad = tdir > 3
-    meta = R.pack_meta_np(proto, np.where(bad, u(255), u(1)), tdir, 0, flags, (r["is_reply"] != 0).astype(u), 0)
+    obs = r["obs"].astype(u)
+    meta = R.pack_meta_np(proto, np.where(bad, u(255), u(1)), tdir, 0, flags, (r["is_reply"] != 0).astype(u), 0,
+                          obs)
     ports = _swap16(r["src_port"]) | (_swap16(r["dst_port"]) << u(16))
+    # TcpId: TSval on TO_NETWORK (3), TSecr on FROM_NETWORK (2) (:622-628)
+    tcp_id = np.where(obs == 3, r["tsval"], np.where(obs == 2, r["tsecr"], 0)).astype(u)
     b = R.Batch(r["src_ip"].astype(u), r["dst_ip"].astype(u), r["bytes"].astype(u), meta, ports,
-                np.full(len(r), 0xFFFFFFFF, u))
+                np.full(len(r), 0xFFFFFFFF, u), tcp_id, r["t_nsec"].astype(np.uint64))
     return b, bad
 
 
@@ -82,8 +86,8 @@ def decode_drops(raw: np.ndarray) -> Tuple[R.Batch, np.ndarray]:
     proto = r["proto"].astype(u)
     dt = r["drop_type"].astype(u)
     bad = dt > 7
-    meta = R.pack_meta_np(proto, np.where(bad, u(255), u(2)), 1, dt, 0, 0, 0)
+    meta = R.pack_meta_np(proto, np.where(bad, u(255), u(2)), 1, dt, 0, 0, 0, 2)  # ToFlow(obs 2)
     ports = _swap16(r["src_port"]) | (_swap16(r["dst_port"]) << u(16))
     b = R.Batch(r["src_ip"].astype(u), r["dst_ip"].astype(u), r["skb_len"].astype(u), meta, ports,
-                np.full(len(r), 0xFFFFFFFF, u))
+                np.full(len(r), 0xFFFFFFFF, u), np.zeros(len(r), u), r["ts"].astype(np.uint64))
     return b, bad

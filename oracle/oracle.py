@@ -269,9 +269,11 @@ assert DROP_STRUCT.size == 32
 def decode_drop(raw: bytes) -> Flow:
     """dropReason.processRecord decode (dropreason_linux.go:345-386): HostToNetShort on
     both ports, ToFlow(..., obs 2, DROPPED), AddDropReason(drop_type), AddPacketSize(skb_len)."""
-    src, dst, sport, dport, skb_len, _ret, drop_type, proto, _infm, _ts = DROP_STRUCT.unpack(raw)
-    return drop_flow(int2ip(src), int2ip(dst), host_to_net_short(sport), host_to_net_short(dport),
-                     proto, drop_type, skb_len)
+    src, dst, sport, dport, skb_len, _ret, drop_type, proto, _infm, ts = DROP_STRUCT.unpack(raw)
+    f = drop_flow(int2ip(src), int2ip(dst), host_to_net_short(sport), host_to_net_short(dport),
+                  proto, drop_type, skb_len)
+    f.time_ns = ts  # ToFlow(MonotonicOffset + Ts) (dropreason_linux.go:358-360), offset 0 here
+    return f
 
 
 # dropReason.processRecord after the decode: obs forced to 2, DROPPED.

@@ -24,6 +24,7 @@ from . import oracle as O
 # meta word layout (restated from DESIGN.md section 3; independent of the product header)
 META_PROTO_SHIFT, META_VERDICT_SHIFT, META_TDIR_SHIFT = 0, 8, 16
 META_REASON_SHIFT, META_FLAGS_SHIFT, META_REPLY_SHIFT, META_DNSTYPE_SHIFT = 18, 21, 27, 28
+META_OBS_SHIFT = 30  # observation point 0-3 (include/gpuagg.h)
 
 
 def pack_meta(proto: int, verdict: int, tdir: int = 0, reason: int = 0, flags: int = 0,
@@ -32,16 +33,18 @@ def pack_meta(proto: int, verdict: int, tdir: int = 0, reason: int = 0, flags: i
             | ((flags & 0x3F) << 21) | ((is_reply & 1) << 27) | ((dns_type & 3) << 28))
 
 
-def pack_meta_np(proto, verdict, tdir=0, reason=0, flags=0, is_reply=0, dns_type=0) -> np.ndarray:
-    """pack_meta over numpy arrays (fields masked to their widths)."""
+def pack_meta_np(proto, verdict, tdir=0, reason=0, flags=0, is_reply=0, dns_type=0, obs=0) -> np.ndarray:
+    """pack_meta over numpy arrays (fields masked to their widths; an observation point
+    above 3 is written as 0, include/gpuagg.h)."""
     u = np.uint32
 
     def f(x, mask, shift):
         return (np.asarray(x).astype(u) & u(mask)) << u(shift)
+    obs = np.asarray(obs).astype(u)
     return (f(proto, 0xFF, META_PROTO_SHIFT) | f(verdict, 0xFF, META_VERDICT_SHIFT)
             | f(tdir, 3, META_TDIR_SHIFT) | f(reason, 7, META_REASON_SHIFT)
             | f(flags, 0x3F, META_FLAGS_SHIFT) | f(is_reply, 1, META_REPLY_SHIFT)
-            | f(dns_type, 3, META_DNSTYPE_SHIFT))
+            | f(dns_type, 3, META_DNSTYPE_SHIFT) | f(np.where(obs <= 3, obs, u(0)), 3, META_OBS_SHIFT))
 
 
 @dataclass
@@ -63,6 +66,8 @@ class Batch:
     meta: np.ndarray
     ports: Optional[np.ndarray] = None
     dns_id: Optional[np.ndarray] = None
+    tcp_id: Optional[np.ndarray] = None   # u32 (latency)
+    time_ns: Optional[np.ndarray] = None  # u64 (latency)
 
     def __len__(self) -> int:
         return int(self.src_ip.shape[0])
@@ -71,11 +76,12 @@ class Batch:
         def s(x):
             return None if x is None else x[a:b]
         return Batch(self.src_ip[a:b], self.dst_ip[a:b], self.bytes[a:b], self.meta[a:b],
-                     s(self.ports), s(self.dns_id))
+                     s(self.ports), s(self.dns_id), s(self.tcp_id), s(self.time_ns))
 
 
 def flow_from_record(src_ip: int, dst_ip: int, nbytes: int, meta: int, ports: int,
-                     dns_id: int, dns_dict: Dict[int, DnsEntry]) -> O.Flow:
+                     dns_id: int, dns_dict: Dict[int, DnsEntry], tcp_id: int = 0,
+                     time_ns: int = 0) -> O.Flow:
     proto = meta & 0xFF
     verdict = (meta >> 8) & 0xFF
     tdir = (meta >> 16) & 3
@@ -83,9 +89,11 @@ def flow_from_record(src_ip: int, dst_ip: int, nbytes: int, meta: int, ports: in
     flags = (meta >> 21) & 0x3F
     dns_type = (meta >> 28) & 3
     sport, dport = ports & 0xFFFF, (ports >> 16) & 0xFFFF
-    f = O.to_flow(O.int2ip(src_ip), O.int2ip(dst_ip), sport, dport, proto, 0, verdict)
+    obs = (meta >> 30) & 3
+    f = O.to_flow(O.int2ip(src_ip), O.int2ip(dst_ip), sport, dport, proto, obs, verdict)
     f.traffic_direction = tdir
-    meta_ext = O.RetinaMetadata(bytes=nbytes)
+    f.time_ns = time_ns
+    meta_ext = O.RetinaMetadata(bytes=nbytes, tcp_id=tcp_id)
     verdict = f.verdict  # after ToFlow's 0 -> FORWARDED (flow_utils.go:94-96)
     if verdict in (O.VERDICT_FORWARDED, O.VERDICT_RETRANSMISSION):
         O.add_tcp_flags(f, (flags & 2) >> 1, (flags & 16) >> 4, flags & 1, (flags & 4) >> 2,

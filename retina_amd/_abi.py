@@ -19,6 +19,7 @@ ERR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", ECAPACITY: 
              ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE", ENOTFOUND: "ENOTFOUND"}
 
 u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
 
 
 class Config(C.Structure):
@@ -40,7 +41,7 @@ class MetricOptions(C.Structure):
 
 class Columns(C.Structure):
     _fields_ = [("src_ip", u32p), ("dst_ip", u32p), ("bytes", u32p), ("meta", u32p),
-                ("ports", u32p), ("dns_id", u32p)]
+                ("ports", u32p), ("dns_id", u32p), ("tcp_id", u32p), ("time_ns", u64p)]
 
 
 class Batch(C.Structure):
@@ -53,6 +54,13 @@ class StateDesc(C.Structure):
                 ("cms", C.c_void_p), ("cms_len", C.c_size_t),
                 ("hll", C.c_void_p), ("hll_len", C.c_size_t),
                 ("sparse_entry_words", C.c_size_t), ("sparse_len", C.c_size_t)]
+
+
+class LatencyState(C.Structure):
+    _fields_ = [("enabled", C.c_uint32), ("latency_buckets", C.c_uint64 * 11), ("latency_count", C.c_uint64),
+                ("latency_sum", C.c_int64), ("handshake_buckets", C.c_uint64 * 11),
+                ("handshake_count", C.c_uint64), ("handshake_sum", C.c_int64), ("no_response", C.c_uint64),
+                ("pending", C.c_uint64)]
 
 
 class Stats(C.Structure):
@@ -125,6 +133,9 @@ SIGNATURES = [
     ("gpuagg_result_family", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
     ("gpuagg_result_dropped", C.c_uint64, [C.c_void_p]),
     ("gpuagg_result_render_text", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("gpuagg_set_apiserver_ips", C.c_int, [C.c_void_p, u32p, C.c_size_t]),
+    ("gpuagg_latency_read", C.c_int, [C.c_void_p, C.POINTER(LatencyState)]),
+    ("gpuagg_set_time_offset", C.c_int, [C.c_void_p, C.c_int64]),
 ]
 
 _lib = None

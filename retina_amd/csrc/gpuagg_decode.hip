@@ -38,6 +38,9 @@ __device__ __forceinline__ uint32_t swap_ports(uint32_t w) { return bswap16(w & 
 struct DecodeOut {
   uint32_t *src, *dst, *bytes, *meta, *ports, *dns;
   unsigned long long *out_of_range;
+  uint32_t *tcp_id;  // latency columns, or null
+  uint64_t *time_ns;
+  uint64_t time_offset;
 };
 
 // Out-of-range rows never come from the eBPF programs: one atomic per lane that saw any.
@@ -56,20 +59,24 @@ __device__ __forceinline__ void count_out_of_range(uint32_t cnt, unsigned long l
 // A traffic direction above 3 does not fit the 2-bit field (conntrack.c only emits
 // 0..2): the row is counted in out_of_range and gets verdict kVerdictUnencodable, which
 // no metric consumes, rather than a wrong label (the sketches still see its 5-tuple).
-__device__ __forceinline__ void packet_fields(uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5,
-                                              uint32_t w10, uint32_t w11, size_t i, const DecodeOut &o,
-                                              bool &bad) {
-  const uint32_t tdir = (w10 >> 8) & 0xFFu, proto = (w10 >> 16) & 0xFFu, flags = w10 >> 24;
+__device__ __forceinline__ void packet_fields(const uint32_t *w, size_t i, const DecodeOut &o, bool &bad) {
+  const uint32_t w10 = w[10], w11 = w[11];
+  const uint32_t obs = w10 & 0xFFu, tdir = (w10 >> 8) & 0xFFu, proto = (w10 >> 16) & 0xFFu, flags = w10 >> 24;
   const uint32_t tcp_flags = proto == 6u ? (flags & 0x3Fu) : 0u;
   bad = tdir > 3u;
+  // observation point (ToFlow, flow_utils.go:72-92) in bits 30-31: only 2 (FROM_NETWORK)
+  // and 3 (TO_NETWORK) are read (latency), other points are written as 0
   const uint32_t meta = proto | ((bad ? kVerdictUnencodable : kVerdictForwarded) << 8) | ((tdir & 3u) << 16) |
-                        (tcp_flags << 21) | ((w11 & 0xFFu) ? (1u << 27) : 0u);
-  o.src[i] = w3;
-  o.dst[i] = w4;
-  o.bytes[i] = w2;
+                        (tcp_flags << 21) | ((w11 & 0xFFu) ? (1u << 27) : 0u) | ((obs <= 3u ? obs : 0u) << 30);
+  o.src[i] = w[3];
+  o.dst[i] = w[4];
+  o.bytes[i] = w[2];
   o.meta[i] = meta;
-  if (o.ports) o.ports[i] = swap_ports(w5);
+  if (o.ports) o.ports[i] = swap_ports(w[5]);
   if (o.dns) o.dns[i] = 0xFFFFFFFFu;
+  // TcpId: TSval (w8) on TO_NETWORK, TSecr (w9) on FROM_NETWORK (:622-628); t_nsec (w0-1)
+  if (o.tcp_id) o.tcp_id[i] = obs == 3u ? w[8] : obs == 2u ? w[9] : 0u;
+  if (o.time_ns) o.time_ns[i] = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + o.time_offset;
 }
 
 __global__ __launch_bounds__(kDecodeThreads) void packet_decode_kernel(const uint4 *raw, size_t n,
@@ -96,7 +103,7 @@ __global__ __launch_bounds__(kDecodeThreads) void packet_decode_kernel(const uin
     for (uint32_t r = threadIdx.x; r < nrec; r += kDecodeThreads) {
       const uint32_t *w = tw + r * kPacketWords;
       bool bad;
-      packet_fields(w[2], w[3], w[4], w[5], w[10], w[11], r0 + r, o, bad);
+      packet_fields(w, r0 + r, o, bad);
       n_bad += bad;
     }
     __syncthreads();
@@ -124,9 +131,11 @@ __global__ __launch_bounds__(kDecodeThreads) void drop_decode_kernel(const uint4
     o.dst[i] = a.y;
     o.bytes[i] = a.w;
     o.meta[i] = proto | ((bad ? kVerdictUnencodable : kVerdictDropped) << 8) | (1u << 16) |
-                ((drop_type & 7u) << 18);
+                ((drop_type & 7u) << 18) | (2u << 30);  // ToFlow(obs 2): FROM_NETWORK
     if (o.ports) o.ports[i] = swap_ports(a.z);
     if (o.dns) o.dns[i] = 0xFFFFFFFFu;
+    if (o.tcp_id) o.tcp_id[i] = 0u;  // dropreason sets no TcpId
+    if (o.time_ns) o.time_ns[i] = ((uint64_t)b.z | ((uint64_t)b.w << 32)) + o.time_offset;
   }
   count_out_of_range(n_bad, o.out_of_range);
 }
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(kDecodeThreads) void drop_decode_kernel(const uint4
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st) {
   if (a.n == 0) return hipSuccess;
   const DecodeOut o{a.out.src_ip, a.out.dst_ip, a.out.bytes, a.out.meta, a.out.ports, a.out.dns_id,
-                    (unsigned long long *)a.out_of_range};
+                    (unsigned long long *)a.out_of_range, a.out.tcp_id, a.out.time_ns, a.time_offset};
   const uint32_t cap = a.n_cu * 8u;  // enough resident workgroups to cover HBM latency
   if (a.kind == kRawPacket) {
     const size_t tiles = (a.n + kTile - 1) / kTile;

@@ -75,6 +75,7 @@ struct DecodeArgs {
   OutCols out;
   uint64_t *out_of_range;  // device counter: fields that do not fit the meta word
   uint32_t n_cu;
+  uint64_t time_offset;    // added to the record times (ktime.MonotonicOffset)
 };
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
 

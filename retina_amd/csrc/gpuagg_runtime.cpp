@@ -137,6 +137,9 @@ struct gpuagg_result {
   std::vector<Series> series;
   std::vector<std::vector<const char *>> name_ptrs, value_ptrs;
   uint64_t dropped = 0;
+  // families rendered outside `series` (the latency histograms / no_response counter):
+  // name -> exposition text block
+  std::map<std::string, std::string> extra_text;
 };
 
 struct gpuagg_ctx {
@@ -178,6 +181,27 @@ struct gpuagg_ctx {
   // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
   uint8_t *d_ipl = nullptr;
   size_t ipl_alloc = 0;
+  // node-apiserver latency join (gpuagg_latency.hip)
+  uint32_t lat_enabled = 0;  // bit 0 latency, 1 handshake, 2 no_response
+  std::vector<uint32_t> api_ips;
+  uint32_t *d_api = nullptr;
+  unsigned long long *d_lat = nullptr;  // kLatStateWords
+  uint32_t *d_lat_blk_cnt = nullptr;
+  unsigned long long *d_lat_blk_max = nullptr, *d_lat_blk_clk = nullptr;
+  uint64_t *d_lat_blk_base = nullptr;
+  size_t lat_blk_alloc = 0;
+  LatEvent *d_lat_ev = nullptr;
+  size_t lat_ev_alloc = 0;
+  unsigned long long *d_lat_hash = nullptr;  // [2][lat_ev_alloc]: sort in, sort out
+  uint32_t *d_lat_idx = nullptr;
+  LatEvent *d_lat_carry[2] = {nullptr, nullptr};
+  size_t lat_carry_alloc = 0;
+  int lat_carry_cur = 0;
+  uint64_t lat_carry_bound = 0;  // >= entries currently carried
+  void *d_lat_tmp = nullptr;
+  size_t lat_tmp_alloc = 0;
+  uint64_t *h_lat_n = nullptr;   // pinned: the batch's event count
+  int64_t time_offset = 0;       // ktime.MonotonicOffset added to decoded record times
   uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
   size_t ipl_all_alloc = 0;
   uint32_t ipl_all_nb = 0, ipl_all_seed = 0, ipl_all_bytes = 0;
@@ -208,6 +232,8 @@ struct gpuagg_ctx {
   // copy_stream after the copy, `released` on stream after the last kernel reading it.
   struct Staging {
     uint32_t *cols[6] = {};
+    uint32_t *tcp_id = nullptr;  // latency columns
+    uint64_t *time_ns = nullptr;
     uint8_t *raw = nullptr;
     size_t raw_alloc = 0;
     hipEvent_t copied = nullptr, released = nullptr;
@@ -357,6 +383,17 @@ void ctx_values(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, 
   if (opts & OPT_PORT) out.push_back((port17 & 0x10000u) ? std::to_string(port17 & 0xFFFFu) : "unknown");
 }
 
+void free_batch_cols(gpuagg_batch *b) {
+  for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
+                       &b->cols.ports, &b->cols.dns_id, &b->cols.tcp_id})
+    if (*p) {
+      hipHostFree(*p);
+      *p = nullptr;
+    }
+  if (b->cols.time_ns) hipHostFree(b->cols.time_ns);
+  b->cols.time_ns = nullptr;
+}
+
 int ensure_staging(gpuagg_ctx *c, size_t cap) {
   if (cap <= c->staging_cap) return GPUAGG_OK;
   if (c->staging_cap) {  // in-flight copies / launches may use the old columns
@@ -366,8 +403,12 @@ int ensure_staging(gpuagg_ctx *c, size_t cap) {
   c->staging_cap = 0;
   for (auto &s : c->stg) {
     for (auto &p : s.cols) dev_free(p);
+    dev_free(s.tcp_id);
+    dev_free(s.time_ns);
     for (auto &p : s.cols)
       if (int rc = dev_alloc(c, &p, cap)) return rc;
+    if (int rc = dev_alloc(c, &s.tcp_id, cap)) return rc;
+    if (int rc = dev_alloc(c, &s.time_ns, cap)) return rc;
   }
   c->staging_cap = cap;
   return GPUAGG_OK;
@@ -647,6 +688,109 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 }
 
 
+// Latency state: `full` (reconcile) also drops the clock and the pending requests;
+// otherwise (epoch reset after a merge) only the histograms and no_response restart.
+int lat_reset(gpuagg_ctx *c, bool full) {
+  if (!c->d_lat) {
+    if (!c->lat_enabled) return GPUAGG_OK;
+    if (int rc = dev_alloc(c, &c->d_lat, kLatStateWords)) return rc;
+    full = true;
+  }
+  if (full) {
+    HIPCHK(c, hipMemsetAsync(c->d_lat, 0, kLatStateWords * 8, c->stream));
+    c->lat_carry_bound = 0;
+  } else {
+    HIPCHK(c, hipMemsetAsync(c->d_lat + kLatHist, 0, (kLatStateWords - kLatHist) * 8, c->stream));
+  }
+  return GPUAGG_OK;
+}
+
+// The TTL join over one batch (see gpuagg_latency.hip); waits for the event count.
+int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
+  int rc;
+  if (!cv.ports || !cv.tcp_id || !cv.time_ns)
+    return fail(c, GPUAGG_EINVAL, "node-apiserver latency metrics read the ports, tcp_id and time_ns columns");
+  if (!c->d_lat && (rc = lat_reset(c, true))) return rc;
+  LatArgs a{};
+  a.src = cv.src_ip;
+  a.dst = cv.dst_ip;
+  a.meta = cv.meta;
+  a.ports = cv.ports;
+  a.tcp_id = cv.tcp_id;
+  a.time_ns = cv.time_ns;
+  a.n = n;
+  a.blocks = (uint32_t)std::min<uint64_t>((uint64_t)c->n_cu * 4, (n + 4095) / 4096);
+  a.chunk = (n + a.blocks - 1) / a.blocks;
+  a.api = c->d_api;
+  a.n_api = (uint32_t)c->api_ips.size();
+  a.state = c->d_lat;
+  if ((rc = ensure_buf(c, &c->d_lat_blk_cnt, &c->lat_blk_alloc, a.blocks))) return rc;
+  if (!c->d_lat_blk_max) {
+    const size_t nb = (size_t)c->n_cu * 4;
+    if ((rc = dev_alloc(c, &c->d_lat_blk_max, nb)) || (rc = dev_alloc(c, &c->d_lat_blk_clk, nb)) ||
+        (rc = dev_alloc(c, &c->d_lat_blk_base, nb)))
+      return rc;
+    if (c->lat_blk_alloc < nb) {  // keep every per-block array the same size
+      dev_free(c->d_lat_blk_cnt);
+      c->lat_blk_alloc = 0;
+      if ((rc = ensure_buf(c, &c->d_lat_blk_cnt, &c->lat_blk_alloc, nb))) return rc;
+    }
+  }
+  a.blk_cnt = c->d_lat_blk_cnt;
+  a.blk_max = c->d_lat_blk_max;
+  a.blk_clk = c->d_lat_blk_clk;
+  a.blk_base = c->d_lat_blk_base;
+  // events: carried entries + at most one per record
+  const size_t cap = c->lat_carry_bound + n;
+  if (cap > c->lat_ev_alloc) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dev_free(c->d_lat_ev);
+    dev_free(c->d_lat_hash);
+    dev_free(c->d_lat_idx);
+    c->lat_ev_alloc = 0;
+    if ((rc = dev_alloc(c, &c->d_lat_ev, cap)) || (rc = dev_alloc(c, &c->d_lat_hash, 2 * cap)) ||
+        (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)))
+      return rc;
+    c->lat_ev_alloc = cap;
+  }
+  a.ev = c->d_lat_ev;
+  a.hash_in = c->d_lat_hash;
+  a.hash_out = c->d_lat_hash + c->lat_ev_alloc;
+  a.idx_in = c->d_lat_idx;
+  a.idx_out = c->d_lat_idx + c->lat_ev_alloc;
+  if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8, hipHostMallocDefault) != hipSuccess)
+    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(8)");
+  a.carry_in = c->d_lat_carry[c->lat_carry_cur];  // copied into the events by the front
+  HIPCHK(c, launch_latency_front(a, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_lat_n, c->d_lat + kLatEvents, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t ne = *c->h_lat_n;
+  // carry-out buffer: at most one entry per event
+  if (ne > c->lat_carry_alloc) {
+    LatEvent *keep = c->d_lat_carry[c->lat_carry_cur];  // read by this batch already (copied)
+    dev_free(c->d_lat_carry[c->lat_carry_cur ^ 1]);
+    c->d_lat_carry[c->lat_carry_cur] = nullptr;
+    dev_free(keep);
+    c->lat_carry_alloc = 0;
+    if ((rc = dev_alloc(c, &c->d_lat_carry[0], ne)) || (rc = dev_alloc(c, &c->d_lat_carry[1], ne))) return rc;
+    c->lat_carry_alloc = ne;
+  }
+  a.carry_out = c->d_lat_carry[c->lat_carry_cur ^ 1];
+  size_t tb = 0;
+  HIPCHK(c, latency_sort_bytes(ne, &tb));
+  if (tb > c->lat_tmp_alloc) {
+    if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
+    c->d_lat_tmp = nullptr;
+    c->lat_tmp_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_lat_tmp, tb));
+    c->lat_tmp_alloc = tb;
+  }
+  HIPCHK(c, launch_latency_back(a, ne, c->d_lat_tmp, c->lat_tmp_alloc, c->lat_enabled, c->stream));
+  c->lat_carry_cur ^= 1;
+  c->lat_carry_bound = ne;
+  return GPUAGG_OK;
+}
+
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
   if (n == 0) return GPUAGG_OK;
@@ -810,6 +954,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
   }
   if ((c->cms_len || c->hll_len) && (rc = launch_sketches(c, cv, n))) return rc;
+  if (c->lat_enabled && (rc = launch_latency(c, cv, n))) return rc;
   c->stats.records += n;
   c->stats.batches += 1;
   c->stats.last_kernel = a.tier1 ? GPUAGG_KERNEL_DENSE_LDS_IP
@@ -832,7 +977,7 @@ int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols
     for (auto &e : ev) HIPCHK(c, hipEventCreate(&e));
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
-  DecodeArgs a{kind, dev_raw, n, out, c->d_decode_oor, c->n_cu};
+  DecodeArgs a{kind, dev_raw, n, out, c->d_decode_oor, c->n_cu, (uint64_t)c->time_offset};
   HIPCHK(c, launch_decode(a, c->stream));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -846,10 +991,11 @@ int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols
 int decode_and_launch(gpuagg_ctx *c, gpuagg_ctx::Staging &s, int kind, const void *dev_raw, size_t n) {
   int rc;
   uint32_t *const *d = s.cols;
-  const OutCols out{d[0], d[1], d[2], d[3], (c->plan.need_ports || c->cms_len > 0) ? d[4] : nullptr,
-                    c->plan.need_dns ? d[5] : nullptr};
+  const bool lat = c->lat_enabled != 0;
+  const OutCols out{d[0], d[1], d[2], d[3], (c->plan.need_ports || c->cms_len > 0 || lat) ? d[4] : nullptr,
+                    c->plan.need_dns ? d[5] : nullptr, lat ? s.tcp_id : nullptr, lat ? s.time_ns : nullptr};
   if ((rc = decode(c, kind, dev_raw, n, out))) return rc;
-  ColsView cv{d[0], d[1], d[2], d[3], d[4], d[5]};
+  ColsView cv{d[0], d[1], d[2], d[3], d[4], d[5], s.tcp_id, s.time_ns};
   return launch(c, cv, n);
 }
 
@@ -911,14 +1057,25 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   drain_timing(c);
   for (auto *b : c->batches) {
-    for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
-                         &b->cols.ports, &b->cols.dns_id})
-      if (*p) hipHostFree(*p);
+    free_batch_cols(b);
     delete b;
   }
   dev_free(c->d_ip);
   dev_free(c->d_ipl);
   dev_free(c->d_ipl_all);
+  dev_free(c->d_api);
+  dev_free(c->d_lat);
+  dev_free(c->d_lat_blk_cnt);
+  dev_free(c->d_lat_blk_max);
+  dev_free(c->d_lat_blk_clk);
+  dev_free(c->d_lat_blk_base);
+  dev_free(c->d_lat_ev);
+  dev_free(c->d_lat_hash);
+  dev_free(c->d_lat_idx);
+  dev_free(c->d_lat_carry[0]);
+  dev_free(c->d_lat_carry[1]);
+  if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
+  if (c->h_lat_n) hipHostFree(c->h_lat_n);
   dev_free(c->d_dense_cnt);
   dev_free(c->d_dense_byt);
   dev_free(c->sv.k0);  // k1, k2, cnt, byt point into the same array
@@ -992,6 +1149,13 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
   if (c->have_opts && same_options(c->cur_opts, new_opts)) return GPUAGG_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const bool local = !c->remote;
+  // NewLatencyMetrics (latency.go:73-115): the three names it switches on
+  uint32_t lat = 0;
+  for (const auto &o : new_opts) {
+    if (o.name == "node_apiserver_latency") lat |= 1u;
+    else if (o.name == "node_apiserver_handshake_latency") lat |= 2u;
+    else if (o.name == "node_apiserver_no_response") lat |= 4u;
+  }
 
   // Module.updateMetricsContexts: registry keyed by MetricName, last writer wins.
   std::map<std::string, Instance> registry;
@@ -1183,6 +1347,8 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
   if ((rc = layout_dense(c, key_cap_for(c, c->slots.size()), false))) return rc;
   c->cur_opts = new_opts;
   c->have_opts = true;
+  c->lat_enabled = lat;
+  if ((rc = lat_reset(c, true))) return rc;  // Init: a new TTL cache (latency.go:118-122)
   return reset_state(c);
 }
 
@@ -1293,6 +1459,19 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
   dev_free(c->d_ipl_all);
+  dev_free(c->d_api);
+  dev_free(c->d_lat);
+  dev_free(c->d_lat_blk_cnt);
+  dev_free(c->d_lat_blk_max);
+  dev_free(c->d_lat_blk_clk);
+  dev_free(c->d_lat_blk_base);
+  dev_free(c->d_lat_ev);
+  dev_free(c->d_lat_hash);
+  dev_free(c->d_lat_idx);
+  dev_free(c->d_lat_carry[0]);
+  dev_free(c->d_lat_carry[1]);
+  if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
+  if (c->h_lat_n) hipHostFree(c->h_lat_n);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
@@ -1314,6 +1493,19 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_all_alloc) {
         dev_free(c->d_ipl_all);
+  dev_free(c->d_api);
+  dev_free(c->d_lat);
+  dev_free(c->d_lat_blk_cnt);
+  dev_free(c->d_lat_blk_max);
+  dev_free(c->d_lat_blk_clk);
+  dev_free(c->d_lat_blk_base);
+  dev_free(c->d_lat_ev);
+  dev_free(c->d_lat_hash);
+  dev_free(c->d_lat_idx);
+  dev_free(c->d_lat_carry[0]);
+  dev_free(c->d_lat_carry[1]);
+  if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
+  if (c->h_lat_n) hipHostFree(c->h_lat_n);
         c->ipl_all_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
         c->ipl_all_alloc = bytes;
@@ -1539,13 +1731,20 @@ int gpuagg_alloc_batch(gpuagg_ctx *c, size_t cap, gpuagg_batch **out) {
   auto *b = new gpuagg_batch();
   b->capacity = cap;
   for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
-                       &b->cols.ports, &b->cols.dns_id}) {
+                       &b->cols.ports, &b->cols.dns_id, &b->cols.tcp_id}) {
     if (hipHostMalloc((void **)p, cap * 4, hipHostMallocDefault) != hipSuccess) {
+      free_batch_cols(b);
       delete b;
       return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", cap * 4);
     }
     memset(*p, 0, cap * 4);
   }
+  if (hipHostMalloc((void **)&b->cols.time_ns, cap * 8, hipHostMallocDefault) != hipSuccess) {
+    free_batch_cols(b);
+    delete b;
+    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", cap * 8);
+  }
+  memset(b->cols.time_ns, 0, cap * 8);
   if ((rc = ensure_staging(c, cap))) return rc;
   c->batches.push_back(b);
   *out = b;
@@ -1556,9 +1755,7 @@ void gpuagg_free_batch(gpuagg_ctx *c, gpuagg_batch *b) {
   if (!c || !b) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
-                       &b->cols.ports, &b->cols.dns_id})
-    if (*p) hipHostFree(*p);
+  free_batch_cols(b);
   c->batches.erase(std::remove(c->batches.begin(), c->batches.end(), b), c->batches.end());
   delete b;
 }
@@ -1575,8 +1772,15 @@ int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
   const bool need[6] = {true, true, (bool)c->plan.need_bytes, true, c->plan.need_ports || c->cms_len > 0,
                         (bool)c->plan.need_dns};
   for (int i = 0; i < 6; ++i)
-    if (need[i]) HIPCHK(c, hipMemcpyAsync(s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
+    if (need[i] || (i == 4 && c->lat_enabled))
+      HIPCHK(c, hipMemcpyAsync(s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
   ColsView cv{s->cols[0], s->cols[1], s->cols[2], s->cols[3], s->cols[4], s->cols[5]};
+  if (c->lat_enabled) {
+    HIPCHK(c, hipMemcpyAsync(s->tcp_id, b->cols.tcp_id, n * 4, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(c, hipMemcpyAsync(s->time_ns, b->cols.time_ns, n * 8, hipMemcpyHostToDevice, c->copy_stream));
+    cv.tcp_id = s->tcp_id;
+    cv.time_ns = s->time_ns;
+  }
   return run_staged(c, *s, [&] { return launch(c, cv, n); });
 }
 
@@ -1584,7 +1788,7 @@ int gpuagg_submit_device(gpuagg_ctx *c, const gpuagg_columns *d, size_t n) {
   if (!c || !d) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  ColsView cv{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id};
+  ColsView cv{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id, d->tcp_id, d->time_ns};
   return launch(c, cv, n);
 }
 
@@ -1605,7 +1809,8 @@ int gpuagg_decode_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n,
   if (!c || !d) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  return decode(c, kind, dev_raw, n, OutCols{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id});
+  return decode(c, kind, dev_raw, n,
+                OutCols{d->src_ip, d->dst_ip, d->bytes, d->meta, d->ports, d->dns_id, d->tcp_id, d->time_ns});
 }
 
 int gpuagg_submit_raw_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n) {
@@ -1647,7 +1852,12 @@ int gpuagg_reset(gpuagg_ctx *c) {
   int rc = bind(c);
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = lat_reset(c, false))) return rc;
   return reset_state(c);
+}
+
+namespace {
+void render_latency(const gpuagg_latency_state &ls, std::map<std::string, std::string> &blocks);
 }
 
 int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
@@ -1766,6 +1976,14 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
       return rc;
     }
   }
+  if (c->lat_enabled) {
+    gpuagg_latency_state ls{};
+    if ((rc = gpuagg_latency_read(c, &ls))) {
+      gpuagg_result_free(r);
+      return rc;
+    }
+    render_latency(ls, r->extra_text);
+  }
   *out = r;
   return GPUAGG_OK;
 }
@@ -1831,6 +2049,36 @@ std::string go_float_g(double v) {
   return out;
 }
 
+// Latency families (latency.go:28-33, LinearBuckets(0, 0.5, 10)): histograms as
+// cumulative le buckets + _sum + _count, no_response once its vec child exists.
+void render_latency(const gpuagg_latency_state &ls, std::map<std::string, std::string> &blocks) {
+  auto hist = [&](const char *name, const char *help, const uint64_t *bk, uint64_t cnt, int64_t sum) {
+    std::string &o = blocks[name];
+    o += std::string("# HELP ") + name + " " + help + "\n# TYPE " + name + " histogram\n";
+    uint64_t acc = 0;
+    for (int i = 0; i < 11; ++i) {
+      acc += bk[i];
+      o += std::string(name) + "_bucket{le=\"" + (i == 10 ? std::string("+Inf") : go_float_g(0.5 * i)) + "\"} " +
+           std::to_string(acc) + "\n";
+    }
+    o += std::string(name) + "_sum " + go_float_g((double)sum) + "\n";
+    o += std::string(name) + "_count " + std::to_string(cnt) + "\n";
+  };
+  if (ls.enabled & 1u)
+    hist("networkobservability_adv_node_apiserver_latency", "Latency of node apiserver in ms",
+         ls.latency_buckets, ls.latency_count, ls.latency_sum);
+  if (ls.enabled & 2u)
+    hist("networkobservability_adv_node_apiserver_tcp_handshake_latency",
+         "Latency of node apiserver tcp handshake in ms", ls.handshake_buckets, ls.handshake_count,
+         ls.handshake_sum);
+  if ((ls.enabled & 4u) && ls.no_response) {
+    const char *name = "networkobservability_adv_node_apiserver_no_response";
+    blocks[name] = std::string("# HELP ") + name +
+                   " Number of packets that did not get a response from node apiserver\n# TYPE " + name +
+                   " counter\n" + name + "{no_response=\"no_response\"} " + go_float_g((double)ls.no_response) + "\n";
+  }
+}
+
 void escape_into(std::string &out, const std::string &s, bool quote) {  // expfmt escaping
   for (char ch : s) {
     if (ch == '\\') out += "\\\\";
@@ -1854,8 +2102,9 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
     std::stable_sort(pairs[i].begin(), pairs[i].end(),
                      [](const auto &a, const auto &b) { return a.first < b.first; });
   }
-  std::string out;
+  std::map<std::string, std::string> blocks = r->extra_text;  // family name -> text
   for (auto &kv : fam) {
+    std::string &out = blocks[kv.first];
     auto &idx = kv.second;
     std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
       const auto &pa = pairs[a], &pb = pairs[b];
@@ -1884,6 +2133,8 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
       out += '\n';
     }
   }
+  std::string out;
+  for (auto &kv : blocks) out += kv.second;  // families sorted by name (expfmt)
   *len = out.size();
   if (!buf) return GPUAGG_OK;
   if (cap < out.size() + 1) return GPUAGG_ECAPACITY;
@@ -2118,12 +2369,62 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
         if ((rc = gpuagg_sparse_import(c0, ent, m))) break;
       }
     }
+    if (c0->lat_enabled && ci->d_lat && c0->d_lat) {  // histograms / no_response: summed on the host
+      unsigned long long a0[kLatStateWords], ai[kLatStateWords];
+      if ((rc = bind(ci))) break;
+      HIPCHK(ci, hipMemcpy(ai, ci->d_lat, sizeof ai, hipMemcpyDeviceToHost));
+      if ((rc = bind(c0))) break;
+      HIPCHK(c0, hipMemcpy(a0, c0->d_lat, sizeof a0, hipMemcpyDeviceToHost));
+      for (uint32_t w = kLatHist; w < kLatStateWords; ++w) a0[w] += ai[w];
+      HIPCHK(c0, hipMemcpy(c0->d_lat, a0, sizeof a0, hipMemcpyHostToDevice));
+    }
     if ((rc = gpuagg_reset(ci))) break;
     if ((rc = bind(c0))) break;
   }
   cleanup();
   if (rc) return rc;
   HIPCHK(c0, hipStreamSynchronize(c0->stream));
+  return GPUAGG_OK;
+}
+
+int gpuagg_set_apiserver_ips(gpuagg_ctx *c, const uint32_t *ipv4, size_t n) {
+  if (!c || (n && !ipv4)) return GPUAGG_EINVAL;
+  if (n > kLatMaxApi) return fail(c, GPUAGG_ECAPACITY, "%zu apiserver IPs exceed %u", n, kLatMaxApi);
+  int rc = bind(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches read the old set
+  if (!c->d_api && (rc = dev_alloc(c, &c->d_api, kLatMaxApi))) return rc;
+  c->api_ips.assign(ipv4, ipv4 + n);
+  if (n) HIPCHK(c, hipMemcpy(c->d_api, ipv4, n * 4, hipMemcpyHostToDevice));
+  return GPUAGG_OK;
+}
+
+int gpuagg_set_time_offset(gpuagg_ctx *c, int64_t ns) {
+  if (!c) return GPUAGG_EINVAL;
+  c->time_offset = ns;
+  return GPUAGG_OK;
+}
+
+int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
+  if (!c || !out) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  *out = gpuagg_latency_state{};
+  out->enabled = c->lat_enabled;
+  if (!c->d_lat) return GPUAGG_OK;
+  unsigned long long w[kLatStateWords];
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(w, c->d_lat, sizeof w, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 11; ++i) {
+    out->latency_buckets[i] = w[kLatHist + i];
+    out->handshake_buckets[i] = w[kLatHandshake + i];
+  }
+  out->latency_count = w[kLatHist + 11];
+  out->latency_sum = (int64_t)w[kLatHist + 12];
+  out->handshake_count = w[kLatHandshake + 11];
+  out->handshake_sum = (int64_t)w[kLatHandshake + 12];
+  out->no_response = w[kLatNoResponse];
+  out->pending = w[kLatPending];
   return GPUAGG_OK;
 }
 

@@ -63,7 +63,7 @@ class HostBatch:
         self.ptr = ptr
         self.capacity = capacity
         cols = ptr.contents.cols
-        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id", "tcp_id", "time_ns"):
             p = getattr(cols, name)
             setattr(self, name, np.ctypeslib.as_array(p, shape=(capacity,)))
 
@@ -71,7 +71,7 @@ class HostBatch:
         """Copy rows [start, start+n) of an object with numpy column attributes."""
         total = len(batch.src_ip)
         n = min(self.capacity, total - start) if n is None else n
-        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id", "tcp_id", "time_ns"):
             src = getattr(batch, name, None)
             if src is not None:
                 getattr(self, name)[:n] = src[start:start + n]
@@ -249,7 +249,8 @@ class GpuAgg:
             start += n
 
     @staticmethod
-    def device_columns(src_ip, dst_ip, nbytes, meta, ports=None, dns_id=None) -> "_abi.Columns":
+    def device_columns(src_ip, dst_ip, nbytes, meta, ports=None, dns_id=None, tcp_id=None,
+                       time_ns=None) -> "_abi.Columns":
         """Columns from device tensors (torch int32/uint32, contiguous, on this device).
 
         The engine reads them on its own HIP stream, which does not wait for torch's: the
@@ -261,7 +262,25 @@ class GpuAgg:
             if t is None:
                 return None
             return C.cast(C.c_void_p(t.data_ptr()), _abi.u32p)
-        return _abi.Columns(ptr(src_ip), ptr(dst_ip), ptr(nbytes), ptr(meta), ptr(ports), ptr(dns_id))
+        t = None if time_ns is None else C.cast(C.c_void_p(time_ns.data_ptr()), _abi.u64p)
+        return _abi.Columns(ptr(src_ip), ptr(dst_ip), ptr(nbytes), ptr(meta), ptr(ports), ptr(dns_id),
+                            ptr(tcp_id), t)
+
+    # -- node-apiserver latency (gpuagg_latency.hip) ----------------------------------
+    def set_apiserver_ips(self, ips: Sequence[int]) -> None:
+        arr = (C.c_uint32 * max(1, len(ips)))(*[int(x) for x in ips])
+        self._check(self.lib.gpuagg_set_apiserver_ips(self.h, arr, len(ips)))
+
+    def set_time_offset(self, ns: int) -> None:
+        self._check(self.lib.gpuagg_set_time_offset(self.h, int(ns)))
+
+    def latency_state(self) -> dict:
+        st = _abi.LatencyState()
+        self._check(self.lib.gpuagg_latency_read(self.h, C.byref(st)))
+        return {"enabled": st.enabled, "latency_buckets": list(st.latency_buckets),
+                "latency_count": st.latency_count, "latency_sum": st.latency_sum,
+                "handshake_buckets": list(st.handshake_buckets), "handshake_count": st.handshake_count,
+                "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending}
 
     def submit_device(self, cols: "_abi.Columns", n: int) -> None:
         self._check(self.lib.gpuagg_submit_device(self.h, C.byref(cols), n))

@@ -89,6 +89,8 @@ class Records:
     ports: np.ndarray
     dns_id: np.ndarray
     dns: List[DnsPayload] = field(default_factory=list)
+    tcp_id: Optional[np.ndarray] = None   # u32, latency metrics
+    time_ns: Optional[np.ndarray] = None  # u64, latency metrics
 
     def __len__(self) -> int:
         return int(self.src_ip.shape[0])
@@ -362,3 +364,62 @@ CONFIGS = {
     "c5": dict(records=10_000_000, pods=100_000, seed=5,
                gen={"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
 }
+
+
+def gen_latency_records(n_conn: int, pods: Pods, api_ips: Sequence[int], seed: int = 0,
+                        pairs: int = 4, background: int = 0, jitter: int = 8) -> Records:
+    """Node <-> apiserver TCP traffic for the node-apiserver latency metrics (latency.go):
+    n_conn connections (node IP, apiserver IP, random source port, 443), `pairs`
+    request/reply exchanges each: TO_NETWORK requests carry TSval as tcp id, FROM_NETWORK
+    replies carry it back as TSecr (packetparser_linux.go:622-628) 0.2-6 ms later; the
+    first exchange is SYN / SYN+ACK.  Edge rows: 5 % unanswered requests, 3 % replies after
+    the 500 ms TTL, 5 % repeated requests (same TSval), 2 % replies to no request.
+    `background` pod-to-pod records (no tcp id or not apiserver traffic) are interleaved;
+    records are in time order up to local swaps of `jitter` rows."""
+    rng = np.random.Generator(np.random.PCG64(seed + 7000))
+    u = np.uint32
+    nodes = np.array([ip_le(10, 240, i >> 8, i & 255) for i in range(1, 33)], u)
+    apis = np.asarray(api_ips, u)
+    rows = []  # (time, src, dst, sport, dport, obs, flags, tcp_id)
+    t0 = 1_700_000_000_000_000_000 + int(rng.integers(0, 10**9))
+    SYN, ACK, PSH = 2, 16, 8
+    for c in range(n_conn):
+        node, api = int(rng.choice(nodes)), int(rng.choice(apis))
+        sport = int(rng.integers(32768, 61000))
+        t = t0 + int(rng.integers(0, 3 * 10**9))
+        ts = int(rng.integers(1, 2**31))
+        for k in range(pairs):
+            t += int(rng.integers(1_000_000, 200_000_000))
+            ts += int(rng.integers(1, 1000))
+            rf, pf = (SYN, SYN | ACK) if k == 0 else (ACK | PSH, ACK)
+            x = rng.random()
+            rows.append((t, node, api, sport, 443, 3, rf, ts))
+            if x < 0.05:
+                continue  # unanswered
+            if x < 0.10:  # the same request again (not stored twice, latency.go:268-275)
+                rows.append((t + int(rng.integers(10_000, 900_000)), node, api, sport, 443, 3, rf, ts))
+            lat = 600_000_000 if x > 0.97 else int(rng.integers(200_000, 6_000_000))
+            rows.append((t + lat, api, node, 443, sport, 2, pf, ts))
+            if x < 0.02:
+                rows.append((t + lat + 1000, api, node, 443, sport, 2, pf, ts + 99_999))
+    tmax = max(r[0] for r in rows)
+    for _ in range(background):
+        a, b = rng.integers(0, len(pods.ips), 2)
+        obs = int(rng.integers(0, 4))
+        rows.append((int(rng.integers(t0, tmax)), int(pods.ips[a]), int(pods.ips[b]),
+                     int(rng.integers(1024, 65535)), 80, obs, ACK, int(rng.integers(0, 2)) * int(rng.integers(1, 2**31))))
+    rows.sort(key=lambda r: r[0])
+    for i in range(0, len(rows) - 1, 2):  # local disorder: the clock is a running max
+        if rng.random() < 0.3 and jitter:
+            j = min(len(rows) - 1, i + int(rng.integers(1, jitter)))
+            rows[i], rows[j] = rows[j], rows[i]
+    n = len(rows)
+    time_ns = np.array([r[0] for r in rows], np.uint64)
+    src = np.array([r[1] for r in rows], u)
+    dst = np.array([r[2] for r in rows], u)
+    ports = np.array([r[3] | (r[4] << 16) for r in rows], u)
+    obs = np.array([r[5] for r in rows], u)
+    flags = np.array([r[6] for r in rows], u)
+    tcp_id = np.array([r[7] for r in rows], u)
+    meta = pack_meta(np.full(n, 6, u), np.full(n, 1, u), np.where(obs == 3, 2, 1), 0, flags) | (obs << u(30))
+    return Records(src, dst, np.full(n, 100, u), meta, ports, np.zeros(n, u), [], tcp_id, time_ns)

@@ -25,7 +25,8 @@ def _flow_fields(f: O.Flow):
     l4 = None if f.l4 is None else (f.l4.proto, f.l4.source_port, f.l4.destination_port, f.l4.flags)
     ext = f.extensions
     return (f.ip.source, f.ip.destination, l4, f.verdict, f.traffic_direction, ext.bytes,
-            ext.drop_reason)
+            ext.drop_reason, f.trace_observation_point if f.trace_observation_point in
+            (O.OBS_TO_NETWORK, O.OBS_FROM_NETWORK) else None, ext.tcp_id, f.time_ns)
 
 
 def _check_rows(batch: R.Batch, bad: np.ndarray, flows):
@@ -34,7 +35,8 @@ def _check_rows(batch: R.Batch, bad: np.ndarray, flows):
             assert (int(batch.meta[i]) >> 8) & 0xFF == 255
             continue
         g = R.flow_from_record(int(batch.src_ip[i]), int(batch.dst_ip[i]), int(batch.bytes[i]),
-                               int(batch.meta[i]), int(batch.ports[i]), 0, {})
+                               int(batch.meta[i]), int(batch.ports[i]), 0, {}, int(batch.tcp_id[i]),
+                               int(batch.time_ns[i]))
         assert _flow_fields(g) == _flow_fields(f), i
         if f.is_reply is not None:
             assert bool(f.is_reply) == bool((int(batch.meta[i]) >> 27) & 1), i

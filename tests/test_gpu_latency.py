@@ -1,0 +1,118 @@
+"""Node-apiserver latency on the GPU (gpuagg_latency.hip) against the restated TTL join
+(oracle/latency.py, pinned to latency_test.go's cases in tests/test_latency_oracle.py):
+device columns in one batch and in several (requests carried across batches), host-fed
+batches, the raw packetparser decode path, and the text exposition."""
+
+import numpy as np
+import pytest
+
+from oracle import latency as L
+from oracle import oracle as O
+from retina_amd import workloads as W
+
+from .helpers import make_engine
+from .latency_helpers import as_state, oracle_latency
+
+pytestmark = pytest.mark.gpu
+
+API = [W.ip_le(10, 255, 0, 1), W.ip_le(10, 255, 0, 2)]
+SPEC = [{"metric_name": "node_apiserver_latency"}, {"metric_name": "node_apiserver_handshake_latency"},
+        {"metric_name": "node_apiserver_no_response"},
+        {"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+
+
+def _dev(recs, device):
+    import torch
+    dev = torch.device("cuda", device)
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    return [t(recs.src_ip), t(recs.dst_ip), t(recs.bytes), t(recs.meta), t(recs.ports), t(recs.dns_id),
+            t(recs.tcp_id), torch.from_numpy(np.ascontiguousarray(recs.time_ns).view(np.int64)).to(dev)]
+
+
+def _engine(pods, device):
+    g = make_engine(pods, SPEC, False, device)
+    g.set_apiserver_ips(API)
+    return g
+
+
+def _state(g):
+    st = g.latency_state()
+    return {k: st[k] for k in ("latency_buckets", "latency_count", "latency_sum", "handshake_buckets",
+                               "handshake_count", "handshake_sum", "no_response", "pending")}
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 17])
+def test_device_batches_match_oracle(gpu_device, chunks):
+    from retina_amd import GpuAgg
+    pods = W.make_pods(100, seed=11)
+    recs = W.gen_latency_records(400, pods, API, seed=12, background=3000)
+    want = as_state(oracle_latency(recs, API))
+    g = _engine(pods, gpu_device)
+    try:
+        ts = _dev(recs, gpu_device)
+        n = len(recs.src_ip)
+        bounds = np.linspace(0, n, chunks + 1).astype(int)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            g.submit_device(GpuAgg.device_columns(*[x[a:] for x in ts]), int(b - a))
+        got = _state(g)
+    finally:
+        g.close()
+    assert got == want
+    assert want["latency_count"] > 0 and want["no_response"] > 0 and want["pending"] > 0
+
+
+def test_host_fed_and_text(gpu_device):
+    pods = W.make_pods(100, seed=21)
+    recs = W.gen_latency_records(200, pods, API, seed=22, background=1000)
+    m = oracle_latency(recs, API)
+    g = _engine(pods, gpu_device)
+    try:
+        n = len(recs.src_ip)
+        hb = g.alloc_batch(n)
+        hb.fill(recs)
+        g.submit(hb, n)
+        g.sync()
+        got = _state(g)
+        text = g.snapshot_text()
+    finally:
+        g.close()
+    assert got == as_state(m)
+    want_text = L.render(m)
+    for fam in want_text.split("# HELP ")[1:]:  # each latency family block appears verbatim
+        assert "# HELP " + fam in text
+    assert "networkobservability_adv_forward_count" in text
+
+
+def test_raw_packet_decode_path(gpu_device):
+    """72-byte packetparser records: TcpId from TSval / TSecr by observation point, the
+    time from t_nsec + the monotonic offset."""
+    from retina_amd import _abi
+    import torch
+    pods = W.make_pods(100, seed=31)
+    recs = W.gen_latency_records(150, pods, API, seed=32, background=500)
+    off = 123_456_789
+    n = len(recs.src_ip)
+    raw = np.zeros((n, 72), np.uint8)
+    obs = (recs.meta >> 30) & 3
+    flags = (recs.meta >> 21) & 0x3F
+    tsval = np.where(obs == 3, recs.tcp_id, 7).astype(np.uint32)
+    tsecr = np.where(obs == 2, recs.tcp_id, 9).astype(np.uint32)
+    t_nsec = (recs.time_ns - np.uint64(off)).astype(np.uint64)
+    sport, dport = recs.ports & 0xFFFF, recs.ports >> 16
+    swap = lambda x: (((x & 0xFF) << 8) | (x >> 8)).astype(np.uint16)  # noqa: E731  (LE bytes of a net-order short)
+    for i in range(n):
+        O.PACKET_STRUCT.pack_into(raw[i], 0, int(t_nsec[i]), 100, int(recs.src_ip[i]), int(recs.dst_ip[i]),
+                                  int(swap(sport[i])), int(swap(dport[i])), 0, 0, int(tsval[i]), int(tsecr[i]),
+                                  int(obs[i]), 2 if obs[i] == 3 else 1, 6, int(flags[i]), False, 0, 0, 0, 0)
+    want = as_state(oracle_latency(recs, API))
+    g = _engine(pods, gpu_device)
+    try:
+        g.set_time_offset(off)
+        d = torch.from_numpy(raw.reshape(-1)).to(torch.device("cuda", gpu_device))
+        g.submit_raw_device(_abi.RAW_PACKET, d.data_ptr(), n)
+        got = _state(g)
+    finally:
+        g.close()
+    assert got == want
