@@ -117,6 +117,55 @@ type gpuAgg struct {
 	records chan Record
 	raw     chan rawSample
 	done    chan struct{} // closed when Start returns
+
+	// node-apiserver latency (latency.go): apiserver IP set from the pubsub topic, the
+	// histograms as a collector, no_response as a counter vec
+	apiIPs     map[string]uint32
+	apiSubID   string
+	latency    *latencyCollector
+	noResponse *prometheus.CounterVec
+	noRespLast float64
+}
+
+// latencyCollector exposes the engine's latency histograms with the reference's names,
+// Help texts and buckets (latency.go:28-39, LinearBuckets(0, 0.5, 10)) as const
+// histograms built from gpuagg_latency_read.
+type latencyCollector struct {
+	mu      sync.Mutex
+	st      C.gpuagg_latency_state
+	lat, hs *prometheus.Desc
+}
+
+func newLatencyCollector() *latencyCollector {
+	ns := exporter.RetinaNamespace
+	return &latencyCollector{
+		lat: prometheus.NewDesc(ns+"_adv_node_apiserver_latency", "Latency of node apiserver in ms", nil, nil),
+		hs: prometheus.NewDesc(ns+"_adv_node_apiserver_tcp_handshake_latency",
+			"Latency of node apiserver tcp handshake in ms", nil, nil),
+	}
+}
+
+func (lc *latencyCollector) Describe(ch chan<- *prometheus.Desc) { ch <- lc.lat; ch <- lc.hs }
+
+func (lc *latencyCollector) Collect(ch chan<- prometheus.Metric) {
+	lc.mu.Lock()
+	st := lc.st
+	lc.mu.Unlock()
+	emit := func(d *prometheus.Desc, bk [11]C.uint64_t, cnt C.uint64_t, sum C.int64_t) {
+		buckets := map[float64]uint64{}
+		acc := uint64(0)
+		for i := 0; i < 10; i++ { // cumulative upper bounds 0, 0.5, ..., 4.5 (+Inf = count)
+			acc += uint64(bk[i])
+			buckets[0.5*float64(i)] = acc
+		}
+		ch <- prometheus.MustNewConstHistogram(d, uint64(cnt), float64(sum), buckets)
+	}
+	if st.enabled&1 != 0 {
+		emit(lc.lat, st.latency_buckets, st.latency_count, st.latency_sum)
+	}
+	if st.enabled&2 != 0 {
+		emit(lc.hs, st.handshake_buckets, st.handshake_count, st.handshake_sum)
+	}
 }
 
 var (
@@ -213,6 +262,11 @@ func (g *gpuAgg) Init() error {
 	}
 	g.stopping = false
 	g.spec = nil
+	g.apiIPs = map[string]uint32{}
+	if g.apiSubID == "" {
+		fn := pubsub.CallBackFunc(g.apiserverCallback)
+		g.apiSubID = pubsub.New().Subscribe(common.PubSubAPIServer, &fn)
+	}
 	return nil
 }
 
@@ -268,8 +322,62 @@ func (g *gpuAgg) Reconcile(spec *api.MetricsSpec) error {
 	g.vecs = map[string]*prometheus.GaugeVec{}
 	g.ctrs = map[string]*prometheus.CounterVec{}
 	g.ctrLast = map[string]float64{}
+	g.latency, g.noResponse, g.noRespLast = nil, nil, 0
+	for _, o := range spec.ContextOptions {
+		switch o.MetricName { // NewLatencyMetrics (latency.go:73-115)
+		case utils.NodeAPIServerLatencyName, utils.NodeAPIServerTCPHandshakeLatencyName:
+			if g.latency == nil {
+				g.latency = newLatencyCollector()
+				exporter.AdvancedRegistry.MustRegister(g.latency)
+			}
+		case utils.NoResponseFromAPIServerName:
+			g.noResponse = exporter.CreatePrometheusCounterVecForMetric(exporter.AdvancedRegistry,
+				"adv_node_apiserver_no_response", "Number of packets that did not get a response from node apiserver",
+				"no_response")
+		}
+	}
 	g.spec = spec
 	return nil
+}
+
+// apiserverCallback mirrors apiserverWatcherCallbackFn (latency.go:307-346): the
+// apiserver IP set follows the cache's add / delete events and is handed to every device.
+func (g *gpuAgg) apiserverCallback(obj interface{}) {
+	event, ok := obj.(*cache.CacheEvent)
+	if !ok || event == nil {
+		return
+	}
+	apiServer, ok := event.Obj.(*common.APIServerObject)
+	if !ok || apiServer == nil {
+		return
+	}
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	for _, ip := range apiServer.IPs() {
+		v4 := ip.To4()
+		if v4 == nil {
+			continue
+		}
+		switch event.Type {
+		case cache.EventTypeAddAPIServerIPs:
+			g.apiIPs[v4.String()] = binary.LittleEndian.Uint32(v4) // the LE u32 of the record columns
+		case cache.EventTypeDeleteAPIServerIPs:
+			delete(g.apiIPs, v4.String())
+		}
+	}
+	ips := make([]C.uint32_t, 0, len(g.apiIPs))
+	for _, v := range g.apiIPs {
+		ips = append(ips, C.uint32_t(v))
+	}
+	var p *C.uint32_t
+	if len(ips) > 0 {
+		p = &ips[0]
+	}
+	if err := g.each("gpuagg_set_apiserver_ips", func(ctx *C.gpuagg_ctx) C.int {
+		return C.gpuagg_set_apiserver_ips(ctx, p, C.size_t(len(ips)))
+	}); err != nil {
+		g.l.Error("apiserver ips", zap.Error(err))
+	}
 }
 
 // Write is what producers call per decoded record (Enricher.Write's replacement). It
@@ -485,6 +593,23 @@ func (g *gpuAgg) publish() error {
 			g.vecs[full] = vec
 		}
 		vec.WithLabelValues(lvals...).Set(float64(v))
+	}
+	if g.latency != nil || g.noResponse != nil {
+		var st C.gpuagg_latency_state
+		if err := check(ctx, C.gpuagg_latency_read(ctx, &st), "gpuagg_latency_read"); err != nil {
+			return err
+		}
+		if g.latency != nil {
+			g.latency.mu.Lock()
+			g.latency.st = st
+			g.latency.mu.Unlock()
+		}
+		if g.noResponse != nil {
+			if d := float64(st.no_response) - g.noRespLast; d > 0 {
+				g.noResponse.WithLabelValues("no_response").Add(d)
+				g.noRespLast = float64(st.no_response)
+			}
+		}
 	}
 	// the epoch is published: slots no IP maps to any more are freed (their series keep
 	// the last published value, as the reference's gauges of a deleted pod do)

@@ -37,18 +37,27 @@ def _fmix64(k: np.ndarray) -> np.ndarray:
 
 
 def shard_of(src_ip, dst_ip, ports, meta, world: int) -> np.ndarray:
-    """Rank owning each record: h(src, dst, sport, dport, proto) mod world."""
-    lo = src_ip.astype(_U64) | (dst_ip.astype(_U64) << _U64(32))
-    hi = ports.astype(_U64) | ((meta.astype(_U64) & _U64(0xFF)) << _U64(32))
-    h = _fmix64(lo ^ _fmix64(hi ^ SHARD_SEED))
+    """Rank owning each record: h(direction-free 5-tuple) mod world.  The two (ip, port)
+    ends are ordered before hashing, so a request and its reply (mirrored 5-tuples) land
+    on one rank, which the node-apiserver latency join needs (latency.go:256-305)."""
+    p = ports.astype(_U64)
+    a = (src_ip.astype(_U64) << _U64(16)) | (p & _U64(0xFFFF))
+    b = (dst_ip.astype(_U64) << _U64(16)) | (p >> _U64(16))
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    proto = (meta.astype(_U64) & _U64(0xFF)) << _U64(48)
+    h = _fmix64(lo ^ _fmix64(hi ^ proto ^ SHARD_SEED))
     return (h % _U64(world)).astype(np.int64)
 
 
 def shard_records(recs, world: int, rank: int):
     """This rank's records (a workloads.Records-like object with numpy columns)."""
     own = shard_of(recs.src_ip, recs.dst_ip, recs.ports, recs.meta, world) == rank
-    return type(recs)(*(getattr(recs, k)[own] for k in ("src_ip", "dst_ip", "bytes", "meta",
-                                                         "ports", "dns_id")), recs.dns)
+    out = type(recs)(*(getattr(recs, k)[own] for k in ("src_ip", "dst_ip", "bytes", "meta",
+                                                        "ports", "dns_id")), recs.dns)
+    for k in ("tcp_id", "time_ns"):
+        if getattr(recs, k, None) is not None:
+            setattr(out, k, getattr(recs, k)[own])
+    return out
 
 
 # ---- collectives over torch tensors (device views on GPU, CPU tensors under gloo) -------

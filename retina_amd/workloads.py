@@ -30,13 +30,13 @@ def ip_le(a: int, b: int, c: int, d: int) -> int:
     return a | (b << 8) | (c << 16) | (d << 24)
 
 
-def pack_meta(proto, verdict, tdir=0, reason=0, flags=0, is_reply=0, dns_type=0):
+def pack_meta(proto, verdict, tdir=0, reason=0, flags=0, is_reply=0, dns_type=0, obs=0):
     """meta word of include/gpuagg.h (vectorised over numpy arrays)."""
     u = np.uint32
     return (np.asarray(proto, u) & u(0xFF)) | ((np.asarray(verdict, u) & u(0xFF)) << u(8)) \
         | ((np.asarray(tdir, u) & u(3)) << u(16)) | ((np.asarray(reason, u) & u(7)) << u(18)) \
         | ((np.asarray(flags, u) & u(0x3F)) << u(21)) | ((np.asarray(is_reply, u) & u(1)) << u(27)) \
-        | ((np.asarray(dns_type, u) & u(3)) << u(28))
+        | ((np.asarray(dns_type, u) & u(3)) << u(28)) | ((np.asarray(obs, u) & u(3)) << u(30))
 
 
 @dataclass
@@ -421,5 +421,5 @@ def gen_latency_records(n_conn: int, pods: Pods, api_ips: Sequence[int], seed: i
     obs = np.array([r[5] for r in rows], u)
     flags = np.array([r[6] for r in rows], u)
     tcp_id = np.array([r[7] for r in rows], u)
-    meta = pack_meta(np.full(n, 6, u), np.full(n, 1, u), np.where(obs == 3, 2, 1), 0, flags) | (obs << u(30))
+    meta = pack_meta(np.full(n, 6, u), np.full(n, 1, u), np.where(obs == 3, 2, 1), 0, flags, obs=obs)
     return Records(src, dst, np.full(n, 100, u), meta, ports, np.zeros(n, u), [], tcp_id, time_ns)

@@ -131,3 +131,16 @@ def test_two_rank_merge_equals_single():
         assert np.array_equal(c.view(np.uint32), cms)
         assert np.array_equal(h, hll)
     assert res[0][3] == want_sparse
+
+
+def test_shard_of_is_direction_free():
+    """A request and its reply (mirrored 5-tuples) land on one rank (the latency join)."""
+    rng = np.random.default_rng(5)
+    n = 10_000
+    s, d = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32), rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sp, dp = rng.integers(0, 65536, n).astype(np.uint32), rng.integers(0, 65536, n).astype(np.uint32)
+    meta = np.full(n, 6, np.uint32)
+    for world in (2, 8):
+        a = D.shard_of(s, d, sp | (dp << np.uint32(16)), meta, world)
+        b = D.shard_of(d, s, dp | (sp << np.uint32(16)), meta, world)
+        assert np.array_equal(a, b) and len(np.unique(a)) == world

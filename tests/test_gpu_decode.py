@@ -172,7 +172,7 @@ def test_full_size_raw_roundtrip(gpu_device):
         r = W.gen_records(chunk, pods, seed=5000 + k, udp_frac=0.1, other_proto_frac=0.02)
         proto, flags = r.meta & 0xFF, (r.meta >> 21) & 0x3F
         tdir, rep = (r.meta >> 16) & 3, (r.meta >> 27) & 1
-        meta = W.pack_meta(proto, 1, tdir, 0, np.where(proto == 6, flags, 0), rep, 0)
+        meta = W.pack_meta(proto, 1, tdir, 0, np.where(proto == 6, flags, 0), rep, 0, obs=2)  # encoder: obs 2
         for t, a in zip(cols, (r.src_ip, r.dst_ip, r.bytes, meta, r.ports)):
             t[k * chunk:(k + 1) * chunk].copy_(torch.from_numpy(np.ascontiguousarray(a).view(np.int32)))
     raw = W.raw_packets_torch(*cols)
