@@ -11,6 +11,7 @@ prints one JSON line per variant with the HIP-event time per launch:
   *-hbm-ip-table  same with FLAG_NO_LDS_IP_TABLE (IP table in HBM, u64 LDS bins)
   remote    C1 remote spec (sparse table)
   c5*       C5 batch (100k pods) with the C5 spec, and with each of its metrics alone
+  c2-lat    C2 spec + node-apiserver latency metrics (the join's filter pass over 100M rows)
   raw-packet  decode of 72-byte packetparser records (C2 columns re-encoded) + C2 forward
               aggregation; decode_ms is the decode kernel, 92 B/record of HBM traffic
 """
@@ -36,13 +37,15 @@ DROP = W.LOCAL_FWD_DROP[2:]
 ONLY = set(filter(None, os.environ.get("ABLATE_ONLY", "").split(",")))
 
 
-def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, **kw):
+def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, api_ips=None, **kw):
     if ONLY and name not in ONLY:
         return
     g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
                max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags, **kw)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
+    if api_ips:
+        g.set_apiserver_ips(api_ips)
     dc = GpuAgg.device_columns(*cols)
     g.submit_device(dc, n)
     g.sync()
@@ -83,6 +86,14 @@ def main():
         run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
         del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+    if not ONLY or "c2-lat" in ONLY:  # C2 + the latency join's filter pass (no apiserver rows)
+        tcp_id = torch.zeros(n, dtype=torch.int32, device=dev)
+        t_ns = torch.arange(n, dtype=torch.int64, device=dev) * 1000
+        lat_spec = W.LOCAL_FWD_DROP + [{"metric_name": "node_apiserver_latency"},
+                                       {"metric_name": "node_apiserver_no_response"}]
+        run("c2-lat", lat_spec, pods, list(cols[:5]) + [None, tcp_id, t_ns], n,
+            api_ips=[W.ip_le(10, 255, 0, 1)])
+        del tcp_id, t_ns
     if not ONLY or any(v.startswith("c3") for v in ONLY):  # C3 sketch pass split by sketch
         del cols
         c3 = W.CONFIGS["c3"]

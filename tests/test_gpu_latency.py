@@ -116,3 +116,31 @@ def test_raw_packet_decode_path(gpu_device):
     finally:
         g.close()
     assert got == want
+
+
+def test_sharded_contexts_merge(gpu_device):
+    """Two contexts fed the direction-free shards (dist.shard_records) and merged equal one
+    context: the histograms exactly; no_response + pending as a sum (each shard's clock
+    is its own records' running max, so an entry expiring in the last milliseconds of the
+    stream may still be pending on one side)."""
+    from retina_amd import GpuAgg
+    from retina_amd import dist as D
+    pods = W.make_pods(100, seed=41)
+    recs = W.gen_latency_records(300, pods, API, seed=42, background=2000)
+    want = as_state(oracle_latency(recs, API))
+    parts = [_engine(pods, gpu_device) for _ in range(2)]
+    try:
+        for r, g in enumerate(parts):
+            sh = D.shard_records(recs, 2, r)
+            g.submit_device(GpuAgg.device_columns(*_dev(sh, gpu_device)), len(sh.src_ip))
+        parts[0].merge_from(parts[1:])
+        got = _state(parts[0])
+        rest = _state(parts[1])
+    finally:
+        for g in parts:
+            g.close()
+    for k in ("latency_buckets", "latency_count", "latency_sum", "handshake_buckets", "handshake_count",
+              "handshake_sum"):
+        assert got[k] == want[k], k
+    assert got["no_response"] + got["pending"] + rest["pending"] == want["no_response"] + want["pending"]
+    assert rest["latency_count"] == 0 and rest["no_response"] == 0  # reset after the merge
