@@ -222,7 +222,7 @@ def main():
 
     # C5's DNS series are sparse keys (one per query payload and side): a 2^24-slot table
     g = GpuAgg(device=local_rank, remote_context=False, max_slots=cfg["pods"] + 16,
-               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=23 if args.config == "c5" else 16,
+               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2={"c1": 21, "c5": 23}.get(args.config, 16),
                **sketch)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)

@@ -11,9 +11,10 @@
 // Batch form (oracle/latency.py states it): the clock is the running maximum of the
 // record times; an entry expires before the first record whose clock passes its expiry.
 // The join is independent per key, so the batch is processed as
-//   1. lat_count_kernel   per-workgroup event counts and max record time;
+//   1. lat_count_kernel   per-unit (one wave's record range) event count and max time;
 //   2. lat_scan_kernel    exclusive scans of both (one workgroup), batch end clock;
-//   3. lat_emit_kernel    events in record order, each with its clock (block scans);
+//   3. lat_emit_kernel    events in record order, each with its clock (wave scans),
+//                         only for units that hold events;
 //      lat_carry_kernel   entries still pending from earlier batches go first;
 //   4. rocprim radix sort of the events by key hash (stable: record order per key);
 //   5. lat_walk_kernel    one lane per key runs the TTL-cache state machine over its
@@ -55,16 +56,20 @@ __device__ __forceinline__ uint64_t lat_hash(uint64_t k0, uint64_t k1) {
   return fmix64(k0 ^ fmix64(k1 ^ 0x9E3779B97F4A7C15ULL));
 }
 
+// The unit of the front end is one wave over a contiguous record range (a.chunk rows):
+// the count pass reads meta, tcp_id and time for every row (src / dst only for TCP rows
+// with a TCP id at observation point 2 or 3), the scan gives each unit its first event
+// slot and incoming clock, and the emit pass revisits only units that hold events.
 __global__ __launch_bounds__(kLatThreads) void lat_count_kernel(LatArgs a) {
   __shared__ uint32_t api[kLatMaxApi];
-  __shared__ uint32_t cnt_w[kLatThreads / 64];
-  __shared__ unsigned long long max_w[kLatThreads / 64];
   if (threadIdx.x < a.n_api) api[threadIdx.x] = a.api[threadIdx.x];
   __syncthreads();
-  const size_t lo = (size_t)blockIdx.x * a.chunk, hi = min(lo + a.chunk, a.n);
+  const uint32_t u = blockIdx.x * (kLatThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (u >= a.blocks) return;
+  const size_t lo = (size_t)u * a.chunk, hi = min(lo + a.chunk, a.n);
   uint32_t cnt = 0;
   unsigned long long mx = 0;
-  for (size_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+  for (size_t i = lo + lane; i < hi; i += 64) {
     cnt += lat_role(a, api, i) != 0u;
     mx = max(mx, (unsigned long long)a.time_ns[i]);
   }
@@ -73,58 +78,67 @@ __global__ __launch_bounds__(kLatThreads) void lat_count_kernel(LatArgs a) {
     cnt += __shfl_xor(cnt, o);
     mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
   }
-  if ((threadIdx.x & 63u) == 0) {
-    cnt_w[threadIdx.x >> 6] = cnt;
-    max_w[threadIdx.x >> 6] = mx;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    unsigned long long m = 0;
-    for (uint32_t w = 0; w < kLatThreads / 64; ++w) {
-      c += cnt_w[w];
-      m = max(m, max_w[w]);
-    }
-    a.blk_cnt[blockIdx.x] = c;
-    a.blk_max[blockIdx.x] = m;
+  if (lane == 0) {
+    a.blk_cnt[u] = cnt;
+    a.blk_max[u] = mx;
   }
 }
 
-// One workgroup: exclusive scans over the (<= a few thousand) count workgroups.
-__global__ void lat_scan_kernel(LatArgs a) {
-  if (threadIdx.x != 0) return;
+// One 1024-thread workgroup: exclusive scans (event count, clock max) over the units.
+__global__ __launch_bounds__(1024) void lat_scan_kernel(LatArgs a) {
+  __shared__ uint64_t s_cnt[1024];
+  __shared__ unsigned long long s_max[1024];
   unsigned long long *st = a.state;
-  uint64_t base = st[kLatPending];  // carried entries occupy [0, pending)
-  unsigned long long clk = st[kLatClock];
-  for (uint32_t b = 0; b < a.blocks; ++b) {
-    a.blk_base[b] = base;
-    a.blk_clk[b] = clk;
-    base += a.blk_cnt[b];
-    clk = max(clk, a.blk_max[b]);
+  const uint32_t per = (a.blocks + 1023) / 1024, u0 = threadIdx.x * per, u1 = min(u0 + per, a.blocks);
+  uint64_t c = 0;
+  unsigned long long m = 0;
+  for (uint32_t u = u0; u < u1; ++u) {
+    c += a.blk_cnt[u];
+    m = max(m, a.blk_max[u]);
   }
-  st[kLatEvents] = base;
-  st[kLatClockEnd] = clk;
-  st[kLatCarryOut] = 0ULL;
+  s_cnt[threadIdx.x] = c;
+  s_max[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scans
+    const uint64_t yc = threadIdx.x >= o ? s_cnt[threadIdx.x - o] : 0;
+    const unsigned long long ym = threadIdx.x >= o ? s_max[threadIdx.x - o] : 0;
+    __syncthreads();
+    s_cnt[threadIdx.x] += yc;
+    s_max[threadIdx.x] = max(s_max[threadIdx.x], ym);
+    __syncthreads();
+  }
+  uint64_t base = st[kLatPending] + (threadIdx.x ? s_cnt[threadIdx.x - 1] : 0);  // carried entries first
+  unsigned long long clk = max((unsigned long long)st[kLatClock], threadIdx.x ? s_max[threadIdx.x - 1] : 0ULL);
+  for (uint32_t u = u0; u < u1; ++u) {
+    a.blk_base[u] = base;
+    a.blk_clk[u] = clk;
+    base += a.blk_cnt[u];
+    clk = max(clk, a.blk_max[u]);
+  }
+  __syncthreads();  // every thread has read st[kLatPending] / st[kLatClock]
+  if (threadIdx.x == 1023) {
+    st[kLatEvents] = base;
+    st[kLatClockEnd] = clk;
+    st[kLatCarryOut] = 0ULL;
+  }
 }
 
-// Events in record order: each 256-record round is scanned in LDS (event ranks and the
-// running max of the record times) so event e carries clock = max time of records <= e.
+// Events of one unit in record order, each with clock = max time of the rows up to it
+// (wave scans: max via shuffles, ranks via ballot); units without events return at once.
 __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
   __shared__ uint32_t api[kLatMaxApi];
-  __shared__ uint32_t cnt_w[kLatThreads / 64];
-  __shared__ unsigned long long max_w[kLatThreads / 64];
   if (threadIdx.x < a.n_api) api[threadIdx.x] = a.api[threadIdx.x];
   __syncthreads();
-  const size_t lo = (size_t)blockIdx.x * a.chunk, hi = min(lo + a.chunk, a.n);
-  uint64_t base = a.blk_base[blockIdx.x];
-  unsigned long long clk = a.blk_clk[blockIdx.x];
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (size_t r = lo; r < hi; r += blockDim.x) {
-    const size_t i = r + threadIdx.x;
+  const uint32_t u = blockIdx.x * (kLatThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (u >= a.blocks || a.blk_cnt[u] == 0) return;
+  const size_t lo = (size_t)u * a.chunk, hi = min(lo + a.chunk, a.n);
+  uint64_t base = a.blk_base[u];
+  unsigned long long clk = a.blk_clk[u];
+  for (size_t r = lo; r < hi; r += 64) {
+    const size_t i = r + lane;
     const bool in = i < hi;
     const uint32_t role = in ? lat_role(a, api, i) : 0u;
     const unsigned long long t = in ? (unsigned long long)a.time_ns[i] : 0ULL;
-    // wave-inclusive max scan of t, wave rank of events
     unsigned long long m = t;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -132,20 +146,9 @@ __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
       if (lane >= (uint32_t)o) m = max(m, y);
     }
     const uint64_t ball = __ballot(role != 0u);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
-    if (lane == 63) {
-      cnt_w[wave] = (uint32_t)__popcll(ball);
-      max_w[wave] = m;
-    }
-    __syncthreads();
-    uint64_t off = base;
-    unsigned long long c = clk;
-    for (uint32_t w = 0; w < wave; ++w) {
-      off += cnt_w[w];
-      c = max(c, max_w[w]);
-    }
-    c = max(c, m);
     if (role) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
+      const unsigned long long c = max(clk, m);
       const uint32_t s = a.src[i], d = a.dst[i], p = a.ports[i];
       const uint64_t id = a.tcp_id[i];
       const uint32_t sp = p & 0xFFFFu, dp = p >> 16;
@@ -157,17 +160,13 @@ __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
       // AddTCPFlags: packetparser sets them on every TCP flow (forwarded); SYN bit 1, ACK bit 4
       const bool has_flags = verdict == kVerdictForwarded || verdict == kVerdictRetrans;
       const uint32_t bits = role | ((has_flags && (flags & 2u)) ? 4u : 0u) | ((has_flags && (flags & 16u)) ? 8u : 0u);
-      const uint64_t e = off + rank;
+      const uint64_t e = base + rank;
       a.ev[e] = LatEvent{k0, k1, c, (uint32_t)((uint64_t)a.time_ns[i] % 1000000000ULL), bits};
       a.hash_in[e] = lat_hash(k0, k1);
       a.idx_in[e] = (uint32_t)e;
     }
-    __syncthreads();
-    for (uint32_t w = 0; w < kLatThreads / 64; ++w) {
-      base += cnt_w[w];
-      clk = max(clk, max_w[w]);
-    }
-    __syncthreads();
+    base += (uint64_t)__popcll(ball);
+    clk = max(clk, (unsigned long long)__shfl(m, 63));
   }
 }
 
@@ -267,9 +266,10 @@ __global__ void lat_finish_kernel(unsigned long long *st) {
 
 // ---- host side ----------------------------------------------------------------------
 hipError_t launch_latency_front(const LatArgs &a, hipStream_t st) {
-  hipLaunchKernelGGL(lat_count_kernel, dim3(a.blocks), dim3(kLatThreads), 0, st, a);
-  hipLaunchKernelGGL(lat_scan_kernel, dim3(1), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(lat_emit_kernel, dim3(a.blocks), dim3(kLatThreads), 0, st, a);
+  const uint32_t wg = (a.blocks + kLatThreads / 64 - 1) / (kLatThreads / 64);  // a.blocks = units (waves)
+  hipLaunchKernelGGL(lat_count_kernel, dim3(wg), dim3(kLatThreads), 0, st, a);
+  hipLaunchKernelGGL(lat_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(lat_emit_kernel, dim3(wg), dim3(kLatThreads), 0, st, a);
   hipLaunchKernelGGL(lat_carry_kernel, dim3(64), dim3(256), 0, st, a);
   return hipGetLastError();
 }

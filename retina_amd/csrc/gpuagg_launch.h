@@ -87,6 +87,7 @@ struct LatEvent {
   uint32_t bits;     // role 1 request / 2 reply / 3 carried | SYN << 2 | ACK << 3
 };
 constexpr uint32_t kLatMaxApi = 64;
+constexpr uint32_t kLatMaxUnits = 1u << 16;  // front-end units (one wave's contiguous rows each)
 constexpr uint64_t kLatTtlNs = 500000000ULL;  // latency.go:34
 // state words (u64): clock, pending carried entries, scratch, histograms, no_response
 enum : uint32_t {
@@ -100,8 +101,8 @@ struct LatArgs {
   const uint32_t *src, *dst, *meta, *ports, *tcp_id;
   const uint64_t *time_ns;
   size_t n;
-  uint64_t chunk;
-  uint32_t blocks;
+  uint64_t chunk;   // rows per unit
+  uint32_t blocks;  // units (one wave each)
   const uint32_t *api;
   uint32_t n_api;
   unsigned long long *state;

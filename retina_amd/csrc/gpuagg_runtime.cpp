@@ -719,14 +719,15 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.tcp_id = cv.tcp_id;
   a.time_ns = cv.time_ns;
   a.n = n;
-  a.blocks = (uint32_t)std::min<uint64_t>((uint64_t)c->n_cu * 4, (n + 4095) / 4096);
+  // units: one wave over >= 2048 contiguous rows, at most 64k units
+  a.blocks = (uint32_t)std::min<uint64_t>(kLatMaxUnits, (n + 2047) / 2048);
   a.chunk = (n + a.blocks - 1) / a.blocks;
   a.api = c->d_api;
   a.n_api = (uint32_t)c->api_ips.size();
   a.state = c->d_lat;
   if ((rc = ensure_buf(c, &c->d_lat_blk_cnt, &c->lat_blk_alloc, a.blocks))) return rc;
   if (!c->d_lat_blk_max) {
-    const size_t nb = (size_t)c->n_cu * 4;
+    const size_t nb = kLatMaxUnits;
     if ((rc = dev_alloc(c, &c->d_lat_blk_max, nb)) || (rc = dev_alloc(c, &c->d_lat_blk_clk, nb)) ||
         (rc = dev_alloc(c, &c->d_lat_blk_base, nb)))
       return rc;
