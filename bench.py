@@ -252,6 +252,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     stats = g.stats()
     kernel = g.kernel_name()
+    sketch_kernels = g.sketch_kernel_name()
     g.set_timing(False)
     if stats["sparse_dropped"]:
         raise RuntimeError("group-by table overflowed (%d updates lost)" % stats["sparse_dropped"])
@@ -265,7 +266,7 @@ def main():
     fold_ms = stats["fold_ms"] / max(1, stats["kernel_launches"])
     sk_ms = stats["sketch_ms"] / max(1, stats["sketch_launches"]) if stats["sketch_launches"] else 0.0
     if sk_ms > agg_ms:
-        dom, dom_ms, dom_bpr = "sketch_scatter_kernel+cms_fold_kernel+hll_fold_kernel", sk_ms, SKETCH_BYTES_PER_RECORD
+        dom, dom_ms, dom_bpr = sketch_kernels, sk_ms, SKETCH_BYTES_PER_RECORD
         other_ms = agg_ms + fold_ms
     else:
         dom, dom_ms, dom_bpr = kernel, agg_ms, bpr

@@ -392,6 +392,9 @@ void *gpuagg_stream(gpuagg_ctx *ctx);
  * (without "void gpuagg::" and the argument list), e.g. "dense_lds_kernel<2, true, 41u>";
  * "" before the first launch.  Lets a profile be matched to the kernel that ran. */
 const char *gpuagg_kernel_name(const gpuagg_ctx *ctx);
+/* The same for the last sketch pass: its kernels joined by "+", e.g.
+ * "sketch_stage_kernel<true>+cms_fold_kernel+hll_split_kernel+hll_fold_kernel". */
+const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *ctx);
 
 #ifdef __cplusplus
 }

@@ -1594,8 +1594,9 @@ __global__ __launch_bounds__(1024) void cms_fold_kernel(SketchK k, uint32_t n_li
   }
 }
 
-hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels) {
   if (a.n == 0) return hipSuccess;
+  std::string names;
   SketchK k{};
   k.src = a.cols.src_ip;
   k.dst = a.cols.dst_ip;
@@ -1664,6 +1665,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
       if (lds_ip) hipLaunchKernelGGL((sketch_stage_kernel<true>), dim3(a.blocks), dim3(1024), lds, st, k);
       else hipLaunchKernelGGL((sketch_stage_kernel<false>), dim3(a.blocks), dim3(1024), lds, st, k);
       if ((e = hipGetLastError()) != hipSuccess) return e;
+      names = lds_ip ? "sketch_stage_kernel<true>" : "sketch_stage_kernel<false>";
       staged = true;
       break;
     }
@@ -1681,8 +1683,10 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
   else if (lds_ip) hipLaunchKernelGGL((sketch_scatter_kernel<false, true>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   else hipLaunchKernelGGL((sketch_scatter_kernel<false, false>), dim3(a.blocks), dim3(1024), scatter_lds, st, k);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+    names = std::string("sketch_scatter_kernel<") + (vec ? "true" : "false") + ", " + (lds_ip ? "true" : "false") + ">";
   }  // unstaged
   if (a.nwin && a.cms_depth) {
+    names += "+cms_fold_kernel";
     const size_t lds = (size_t)4 << a.win_shift;
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1692,6 +1696,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (a.hll_nsup && a.hll_p) {
+    names += "+hll_split_kernel+hll_fold_kernel";
     // staging rings: a round (4096 entries) over nfine windows, x 2 + 64, when they fit
     const uint32_t nfine = 1u << (a.hll_sshift - a.hll_shift);
     uint32_t R = 64;
@@ -1712,6 +1717,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(hll_fold_kernel, dim3(a.hll_nwin), dim3(1024), lds, st, k);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  if (kernels) *kernels = names;
   return hipSuccess;
 }
 

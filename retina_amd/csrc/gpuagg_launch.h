@@ -1,6 +1,8 @@
 // Host <-> kernel launch interface (internal).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -146,7 +148,8 @@ struct SketchArgs {
   const uint8_t *ipl;               // LDS image of every pod IP for the source lookup, or null
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
 };
-hipError_t launch_sketch(const SketchArgs &a, hipStream_t st);
+// *kernels: the pass's kernels in rocprofv3 spelling joined by "+"
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels);
 
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
 // *kernel (may be null) receives the aggregation kernel's signature as rocprofv3 prints it

@@ -244,6 +244,7 @@ struct gpuagg_ctx {
   hipStream_t copy_stream = nullptr;
   std::vector<gpuagg_batch *> batches;
   std::string kernel_name;  // aggregation kernel of the last launch (rocprofv3 spelling)
+  std::string sketch_kernel_name;  // kernels of the last sketch pass, joined by "+"
 
   // stats / timing
   gpuagg_stats stats{};
@@ -678,7 +679,7 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       s.hll_lists2 = c->d_hll_lists2;
       s.hll_counts2 = c->d_hll_counts2;
     }
-    HIPCHK(c, launch_sketch(s, c->stream));
+    HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
   }
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -2449,5 +2450,6 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
 void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }
+const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *c) { return c ? c->sketch_kernel_name.c_str() : ""; }
 
 }  // extern "C"

@@ -422,5 +422,9 @@ class GpuAgg:
         """Signature of the last launch's aggregation kernel (rocprofv3 spelling)."""
         return (self.lib.gpuagg_kernel_name(self.h) or b"").decode()
 
+    def sketch_kernel_name(self) -> str:
+        """The last sketch pass's kernels (rocprofv3 spelling, joined by "+")."""
+        return (self.lib.gpuagg_sketch_kernel_name(self.h) or b"").decode()
+
     def set_timing(self, enabled: bool) -> None:
         self._check(self.lib.gpuagg_set_timing(self.h, 1 if enabled else 0))
