@@ -28,8 +28,8 @@
 namespace gpuagg {
 
 struct DevIpTable {
-  const uint64_t *slots;
-  uint32_t mask;
+  const uint64_t *slots;  // buckets of 2 entries (16 bytes)
+  uint32_t mask;          // bucket mask
   uint32_t seed;
 };
 struct DevDense {
@@ -97,17 +97,26 @@ __device__ __forceinline__ Lk lk_from(uint64_t e) {
   return Lk{(int32_t)((e >> 32) & ((1u << kSlotBits) - 1)), (uint32_t)(e >> 53) & 1u};
 }
 
-// Cuckoo lookup: both candidate entries are loaded unconditionally (independent
-// loads, no probe loop); an EMPTY entry never matches a real key because the host
-// refuses 255.255.255.255 as a pod IP.
-__device__ __forceinline__ Lk ip_pick(uint32_t ip, uint64_t e1, uint64_t e2) {
-  const uint64_t e = ((uint32_t)e1 == ip) ? e1 : (((uint32_t)e2 == ip) ? e2 : kIpEmpty);
+// Bucketized cuckoo lookup (host builder: gpuagg_set_endpoints): one 16-byte load of
+// the first bucket; the second bucket is read only when the first is full and holds
+// neither entry (~15 % of lookups at the 40 % build load).  An EMPTY entry never matches
+// a real key because the host refuses 255.255.255.255 as a pod IP.
+__device__ __forceinline__ ulonglong2 ip_bucket(const DevIpTable &t, uint32_t b) {
+  return ((const ulonglong2 *)t.slots)[b];
+}
+__device__ __forceinline__ bool ip_need2(uint32_t ip, const ulonglong2 &e) {
+  return (uint32_t)e.x != ip && (uint32_t)e.y != ip && e.x != kIpEmpty && e.y != kIpEmpty;
+}
+__device__ __forceinline__ Lk ip_pick(uint32_t ip, const ulonglong2 &e1, const ulonglong2 &e2) {
+  const uint64_t e = (uint32_t)e1.x == ip ? e1.x : (uint32_t)e1.y == ip ? e1.y
+                   : (uint32_t)e2.x == ip ? e2.x : (uint32_t)e2.y == ip ? e2.y : kIpEmpty;
   return lk_from(e);
 }
 
 __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
-  const uint64_t e1 = t.slots[ip_h1(ip, t.seed) & t.mask];
-  const uint64_t e2 = t.slots[ip_h2(ip, t.seed) & t.mask];
+  const ulonglong2 e1 = ip_bucket(t, ip_h1(ip, t.seed) & t.mask);
+  const ulonglong2 e2 = ip_need2(ip, e1) ? ip_bucket(t, ip_h2(ip, t.seed) & t.mask)
+                                         : make_ulonglong2(kIpEmpty, kIpEmpty);
   return ip_pick(ip, e1, e2);
 }
 
@@ -508,12 +517,13 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
-      uint64_t e1[8], e2[8];
+      ulonglong2 e1[8], e2[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        e1[k] = a.t.slots[ip_h1(ip[k], a.t.seed) & a.t.mask];
-        e2[k] = a.t.slots[ip_h2(ip[k], a.t.seed) & a.t.mask];
-      }
+      for (int k = 0; k < 8; ++k) e1[k] = ip_bucket(a.t, ip_h1(ip[k], a.t.seed) & a.t.mask);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        e2[k] = ip_need2(ip[k], e1[k]) ? ip_bucket(a.t, ip_h2(ip[k], a.t.seed) & a.t.mask)
+                                       : make_ulonglong2(kIpEmpty, kIpEmpty);
       Lk ls0 = ip_pick(ip[0], e1[0], e2[0]), ls1 = ip_pick(ip[1], e1[1], e2[1]);
       Lk ls2 = ip_pick(ip[2], e1[2], e2[2]), ls3 = ip_pick(ip[3], e1[3], e2[3]);
       Lk ld0 = ip_pick(ip[4], e1[4], e2[4]), ld1 = ip_pick(ip[5], e1[5], e2[5]);
@@ -1255,14 +1265,8 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
         ls[3] = lds_lookup(vs.w);
       } else if (k.p) {
         const uint32_t ip[4] = {vs.x, vs.y, vs.z, vs.w};
-        uint64_t e1[4], e2[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          e1[j] = k.t.slots[ip_h1(ip[j], k.t.seed) & k.t.mask];
-          e2[j] = k.t.slots[ip_h2(ip[j], k.t.seed) & k.t.mask];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ls[j] = ip_pick(ip[j], e1[j], e2[j]);
+        for (int j = 0; j < 4; ++j) ls[j] = ip_lookup(k.t, ip[j]);
       }
       L.record(vs.x, vd.x, vp.x, vm.x, ls[0]);
       L.record(vs.y, vd.y, vp.y, vm.y, ls[1]);

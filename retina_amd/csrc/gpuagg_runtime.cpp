@@ -597,7 +597,7 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc;
   SketchArgs s{};
   s.ip_slots = c->d_ip;
-  s.ip_mask = (uint32_t)(c->ip_cap ? c->ip_cap - 1 : 0);
+  s.ip_mask = (uint32_t)(c->ip_cap ? c->ip_cap / 2 - 1 : 0);  // bucket mask
   s.ip_seed = c->ip_seed;
   s.cms = c->d_cms;
   s.cms_depth = c->cms_len ? c->cfg.cms_depth : 0;
@@ -802,7 +802,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   if (c->plan.need_dns && !cv.dns_id) return fail(c, GPUAGG_EINVAL, "enabled DNS metrics read the dns_id column");
   LaunchArgs a{};
   a.ip_slots = c->d_ip;
-  a.ip_mask = (uint32_t)(c->ip_cap - 1);
+  a.ip_mask = (uint32_t)(c->ip_cap / 2 - 1);  // bucket mask
   a.ip_seed = c->ip_seed;
   a.plan = c->plan;
   a.dense_cnt = c->d_dense_cnt;
@@ -1406,30 +1406,46 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     if (ipv4[i] == 0xFFFFFFFFu) return fail(c, GPUAGG_ERANGE, "255.255.255.255 cannot be a pod IP");
     last[ipv4[i]] = ip_entry(ipv4[i], (uint32_t)slot[i], c->slots[slot[i]].api);
   }
-  // cuckoo build: load <= ~45%, re-seed on a failed insertion, grow after 8 seeds
-  size_t cap = 64;
-  while (cap * 45 < last.size() * 100) cap <<= 1;
+  // Bucketized cuckoo build: buckets of 2 entries (16 bytes, one load), two choices,
+  // first choice preferred; an entry moves to its second bucket only while its first is
+  // full, and a kick always refills the bucket it empties, so "key in its second bucket
+  // => first bucket full" holds and a lookup stops after the first bucket whenever that
+  // bucket has a free slot.  Load <= 40 %; re-seed on a failed insertion, grow after 8.
+  size_t cap = 64;  // entries (2 per bucket)
+  while (cap * 40 < last.size() * 100) cap <<= 1;
   std::vector<uint64_t> tab;
   uint32_t seed = 0x2545F491u;
   for (int attempt = 0;; ++attempt) {
     if (attempt && attempt % 8 == 0) cap <<= 1;
     seed = (uint32_t)fmix64((uint64_t)seed + 0x9E3779B97F4A7C15ULL * (attempt + 1));
     tab.assign(cap, kIpEmpty);
-    const uint32_t mask = (uint32_t)(cap - 1);
+    const uint32_t bmask = (uint32_t)(cap / 2 - 1);
+    uint64_t rnd = 0x9E3779B97F4A7C15ULL ^ seed;
+    auto put = [&](uint32_t b, uint64_t e) {
+      for (int k = 0; k < 2; ++k)
+        if (tab[2 * b + k] == kIpEmpty) {
+          tab[2 * b + k] = e;
+          return true;
+        }
+      return false;
+    };
     bool ok = true;
     for (const auto &kv : last) {
       uint64_t cur = kv.second;
-      uint32_t h = ip_h1((uint32_t)cur, seed) & mask;
+      const uint32_t b1 = ip_h1((uint32_t)cur, seed) & bmask, b2 = ip_h2((uint32_t)cur, seed) & bmask;
+      if (put(b1, cur) || put(b2, cur)) continue;
+      uint32_t b = b2;  // both full: kick a random entry of the second bucket
       int kicks = 0;
       for (;;) {
-        std::swap(cur, tab[h]);
-        if (cur == kIpEmpty) break;
+        rnd = rnd * 6364136223846793005ULL + 1442695040888963407ULL;
+        std::swap(cur, tab[2 * b + ((rnd >> 33) & 1)]);
+        const uint32_t c1 = ip_h1((uint32_t)cur, seed) & bmask, c2 = ip_h2((uint32_t)cur, seed) & bmask;
+        b = (b == c1) ? c2 : c1;  // the evicted key's other bucket
+        if (put(b, cur)) break;
         if (++kicks > 500) {
           ok = false;
           break;
         }
-        const uint32_t h1 = ip_h1((uint32_t)cur, seed) & mask, h2 = ip_h2((uint32_t)cur, seed) & mask;
-        h = (h == h1) ? h2 : h1;  // move the evicted key to its other choice
       }
       if (!ok) break;
     }
