@@ -107,6 +107,11 @@ GA_HD uint64_t fmix64(uint64_t k) {
 // IP table: open addressing, linear probing. Entry = ip | slot << 32 | apiserver << 53.
 constexpr uint64_t kIpEmpty = ~0ULL;
 constexpr uint32_t kSlotBits = 21;
+// Radix IP table (when the pod IPs fall in few /16s, as cluster pod CIDRs do): a 64k
+// u16 table maps the first two address octets (the low 16 bits of the LE u32) to a block
+// of 64k u32 entries indexed by the last two octets; entry = slot | apiserver << 31, or
+// kRadixEmpty.  Two loads per IP, the first to a table of a few hot lines.
+constexpr uint32_t kRadixEmpty = 0xFFFFFFFFu, kRadixNoBlock = 0xFFFFu, kRadixMaxBlocks = 64;
 constexpr uint32_t kMaxSlot = (1u << kSlotBits) - 2;  // slot ids 0..kMaxSlot
 GA_HD uint32_t ip_hash(uint32_t ip) {  // murmur3 fmix32: 2 mul + 3 xorshift
   ip ^= ip >> 16;

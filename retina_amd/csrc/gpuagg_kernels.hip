@@ -31,6 +31,8 @@ struct DevIpTable {
   const uint64_t *slots;  // buckets of 2 entries (16 bytes)
   uint32_t mask;          // bucket mask
   uint32_t seed;
+  const uint16_t *pre;    // radix table (kRadix*), or null
+  const uint32_t *blk;
 };
 struct DevDense {
   unsigned long long *cnt;
@@ -113,7 +115,15 @@ __device__ __forceinline__ Lk ip_pick(uint32_t ip, const ulonglong2 &e1, const u
   return lk_from(e);
 }
 
+__device__ __forceinline__ Lk radix_pick(uint32_t e) {
+  return e == kRadixEmpty ? Lk{-1, 0} : Lk{(int32_t)(e & ((1u << kSlotBits) - 1)), e >> 31};
+}
+__device__ __forceinline__ uint32_t radix_entry(const DevIpTable &t, uint32_t ip, uint32_t b) {
+  return b == kRadixNoBlock ? kRadixEmpty : t.blk[(b << 16) | (ip >> 16)];
+}
+
 __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
+  if (t.pre) return radix_pick(radix_entry(t, ip, t.pre[ip & 0xFFFFu]));
   const ulonglong2 e1 = ip_bucket(t, ip_h1(ip, t.seed) & t.mask);
   const ulonglong2 e2 = ip_need2(ip, e1) ? ip_bucket(t, ip_h2(ip, t.seed) & t.mask)
                                          : make_ulonglong2(kIpEmpty, kIpEmpty);
@@ -517,17 +527,28 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
-      ulonglong2 e1[8], e2[8];
+      Lk lk[8];
+      if (a.t.pre) {  // radix table: 8 prefix loads, then 8 entry loads
+        uint32_t bi[8], e[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) e1[k] = ip_bucket(a.t, ip_h1(ip[k], a.t.seed) & a.t.mask);
+        for (int k = 0; k < 8; ++k) bi[k] = a.t.pre[ip[k] & 0xFFFFu];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        e2[k] = ip_need2(ip[k], e1[k]) ? ip_bucket(a.t, ip_h2(ip[k], a.t.seed) & a.t.mask)
-                                       : make_ulonglong2(kIpEmpty, kIpEmpty);
-      Lk ls0 = ip_pick(ip[0], e1[0], e2[0]), ls1 = ip_pick(ip[1], e1[1], e2[1]);
-      Lk ls2 = ip_pick(ip[2], e1[2], e2[2]), ls3 = ip_pick(ip[3], e1[3], e2[3]);
-      Lk ld0 = ip_pick(ip[4], e1[4], e2[4]), ld1 = ip_pick(ip[5], e1[5], e2[5]);
-      Lk ld2 = ip_pick(ip[6], e1[6], e2[6]), ld3 = ip_pick(ip[7], e1[7], e2[7]);
+        for (int k = 0; k < 8; ++k) e[k] = radix_entry(a.t, ip[k], bi[k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lk[k] = radix_pick(e[k]);
+      } else {
+        ulonglong2 e1[8], e2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e1[k] = ip_bucket(a.t, ip_h1(ip[k], a.t.seed) & a.t.mask);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          e2[k] = ip_need2(ip[k], e1[k]) ? ip_bucket(a.t, ip_h2(ip[k], a.t.seed) & a.t.mask)
+                                         : make_ulonglong2(kIpEmpty, kIpEmpty);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lk[k] = ip_pick(ip[k], e1[k], e2[k]);
+      }
+      Lk ls0 = lk[0], ls1 = lk[1], ls2 = lk[2], ls3 = lk[3];
+      Lk ld0 = lk[4], ld1 = lk[5], ld2 = lk[6], ld3 = lk[7];
       uint32_t s0 = vs.x, s1 = vs.y, s2 = vs.z, s3 = vs.w, d0 = vd.x, d1 = vd.y, d2 = vd.z, d3 = vd.w;
       uint32_t b0 = vb.x, b1 = vb.y, b2 = vb.z, b3 = vb.w, m0 = vm.x, m1 = vm.y, m2 = vm.z, m3 = vm.w;
       uint32_t p0 = vp.x, p1 = vp.y, p2 = vp.z, p3 = vp.w, q0 = vq.x, q1 = vq.y, q2 = vq.z, q3 = vq.w;
@@ -1608,7 +1629,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   k.meta = a.cols.meta;
   k.n = a.n;
   k.chunk = a.chunk;
-  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed};
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk};
   k.cms = a.cms;
   k.depth = a.cms_depth;
   k.wlog2 = a.cms_wlog2;
@@ -2022,7 +2043,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.c = DevCols{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
   k.n = a.n;
   k.chunk = a.chunk;
-  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed};
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk};
   k.d = DevDense{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
   k.s = dev_sparse(a.sparse);
   k.sk = DevSketch{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};

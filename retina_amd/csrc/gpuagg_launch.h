@@ -30,6 +30,8 @@ struct LaunchArgs {
   const uint64_t *ip_slots;
   uint32_t ip_mask;
   uint32_t ip_seed;
+  const uint16_t *ip_pre;  // radix IP table (null: the bucket table above)
+  const uint32_t *ip_blk;
   Plan plan;
   uint64_t *dense_cnt, *dense_byt;
   SparseView sparse;
@@ -130,6 +132,8 @@ struct SketchArgs {
   uint32_t blocks;          // scatter workgroups (= lists per window)
   const uint64_t *ip_slots;
   uint32_t ip_mask, ip_seed;
+  const uint16_t *ip_pre;  // radix IP table (null: the bucket table above)
+  const uint32_t *ip_blk;
   uint32_t *cms;
   uint32_t cms_depth, cms_wlog2;
   uint32_t win_shift, nwin, cap;  // windows of 2^win_shift columns; nwin 0: direct atomics

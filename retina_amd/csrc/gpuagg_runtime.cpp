@@ -176,6 +176,11 @@ struct gpuagg_ctx {
 
   // IP table
   uint64_t *d_ip = nullptr;
+  // radix IP table (few /16 prefixes): prefix -> block, blocks of 64k u32 entries
+  uint16_t *d_rpre = nullptr;
+  uint32_t *d_rblk = nullptr;
+  size_t rblk_alloc = 0;
+  bool radix = false;
   size_t ip_cap = 0;  // slots
   uint32_t ip_seed = 0;
   // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
@@ -598,6 +603,8 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   SketchArgs s{};
   s.ip_slots = c->d_ip;
   s.ip_mask = (uint32_t)(c->ip_cap ? c->ip_cap / 2 - 1 : 0);  // bucket mask
+  s.ip_pre = c->radix ? c->d_rpre : nullptr;
+  s.ip_blk = c->radix ? c->d_rblk : nullptr;
   s.ip_seed = c->ip_seed;
   s.cms = c->d_cms;
   s.cms_depth = c->cms_len ? c->cfg.cms_depth : 0;
@@ -803,6 +810,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   LaunchArgs a{};
   a.ip_slots = c->d_ip;
   a.ip_mask = (uint32_t)(c->ip_cap / 2 - 1);  // bucket mask
+  a.ip_pre = c->radix ? c->d_rpre : nullptr;
+  a.ip_blk = c->radix ? c->d_rblk : nullptr;
   a.ip_seed = c->ip_seed;
   a.plan = c->plan;
   a.dense_cnt = c->d_dense_cnt;
@@ -1063,6 +1072,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
     delete b;
   }
   dev_free(c->d_ip);
+  dev_free(c->d_rpre);
+  dev_free(c->d_rblk);
   dev_free(c->d_ipl);
   dev_free(c->d_ipl_all);
   dev_free(c->d_api);
@@ -1463,6 +1474,30 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   }
   HIPCHK(c, hipMemcpy(c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
   c->ip_cap = cap;
+  // radix image when the IPs fall in at most kRadixMaxBlocks /16 prefixes (cluster pod
+  // CIDRs): L2-resident where a hash table of 100k+ IPs is not
+  {
+    std::map<uint32_t, uint32_t> blocks;  // prefix (low 16 bits of the LE u32) -> block
+    for (const auto &kv : last) blocks.emplace(kv.first & 0xFFFFu, 0u);
+    c->radix = !(c->cfg.flags & GPUAGG_FLAG_NO_RADIX_IP_TABLE) && !blocks.empty() &&
+               blocks.size() <= kRadixMaxBlocks;
+    if (c->radix) {
+      uint32_t nb = 0;
+      for (auto &kv : blocks) kv.second = nb++;
+      std::vector<uint16_t> pre(1u << 16, (uint16_t)kRadixNoBlock);
+      for (auto &kv : blocks) pre[kv.first] = (uint16_t)kv.second;
+      std::vector<uint32_t> blk((size_t)nb << 16, kRadixEmpty);
+      for (const auto &kv : last) {
+        const uint32_t sl = (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1));
+        const uint32_t api = (uint32_t)(kv.second >> 53) & 1u;
+        blk[((size_t)blocks[kv.first & 0xFFFFu] << 16) | (kv.first >> 16)] = sl | (api << 31);
+      }
+      if (!c->d_rpre && (rc = dev_alloc(c, &c->d_rpre, (size_t)1 << 16))) return rc;
+      if ((rc = ensure_buf(c, &c->d_rblk, &c->rblk_alloc, blk.size()))) return rc;
+      HIPCHK(c, hipMemcpy(c->d_rpre, pre.data(), pre.size() * 2, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(c->d_rblk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
   // LDS image: non-apiserver pods only (local context treats the apiserver pseudo pod
   // like no endpoint), u16 slot ids
   c->ipl_bytes = 0;
