@@ -358,6 +358,35 @@ int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);
 int gpuagg_set_time_offset(gpuagg_ctx *ctx, int64_t ns);
 
 /* ------------------------------------------------------------------------------
+ * Hubble-mode L3/L4 enrichment (pkg/hubble/parser/parser_linux.go:64-93,
+ * layer34/parser_linux.go:30-84, seven/parser_linux.go:28-146,
+ * common/decoder_linux.go:32-60): per record, the source / destination endpoint from the
+ * ipcache and the flow summary, as columns; the caller renders flow.Flow objects for
+ * Hubble consumers from them (labels and strings stay on the host).
+ * ---------------------------------------------------------------------------- */
+/* The ipcache image: IP -> identity (ipcache.LookupByIP) and a caller-assigned K8s
+ * metadata id (GetK8sMetadata: pod, namespace; 0xFFFFFFFF = none).  Replaces the image. */
+int gpuagg_ipcache_set(gpuagg_ctx *ctx, const uint32_t *ipv4, const uint32_t *identity,
+                       const uint32_t *meta_id, size_t n);
+
+#define GPUAGG_SUMMARY_NONE 0u  /* no summary                                        */
+#define GPUAGG_SUMMARY_TCP 1u   /* "TCP Flags: ..."; arg = flags FIN,SYN,RST,PSH,ACK,URG bits 0-5 */
+#define GPUAGG_SUMMARY_UDP 2u   /* "UDP"                                              */
+#define GPUAGG_SUMMARY_DROP 3u  /* "Drop Reason: ..."; arg = drop reason              */
+#define GPUAGG_SUMMARY_DNS 4u   /* seven.dnsSummary; arg = dns_id | DNS type << 30    */
+
+typedef struct gpuagg_hubble_cols {
+  uint32_t *src_identity, *dst_identity;  /* World (2) when the IP is not in the ipcache */
+  uint32_t *src_meta, *dst_meta;          /* metadata id, 0xFFFFFFFF = none              */
+  uint32_t *summary_kind, *summary_arg;
+} gpuagg_hubble_cols;
+
+/* Enriches n records already in device memory (src_ip, dst_ip, meta; dns_id for DNS
+ * rows) into the device output columns, async on the ctx's stream (gpuagg_sync waits). */
+int gpuagg_hubble_decode_device(gpuagg_ctx *ctx, const gpuagg_columns *in, size_t n,
+                                const gpuagg_hubble_cols *out);
+
+/* ------------------------------------------------------------------------------
  * Introspection
  * ---------------------------------------------------------------------------- */
 typedef struct gpuagg_stats {

@@ -56,6 +56,11 @@ class StateDesc(C.Structure):
                 ("sparse_entry_words", C.c_size_t), ("sparse_len", C.c_size_t)]
 
 
+class HubbleCols(C.Structure):
+    _fields_ = [("src_identity", u32p), ("dst_identity", u32p), ("src_meta", u32p), ("dst_meta", u32p),
+                ("summary_kind", u32p), ("summary_arg", u32p)]
+
+
 class LatencyState(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("latency_buckets", C.c_uint64 * 11), ("latency_count", C.c_uint64),
                 ("latency_sum", C.c_int64), ("handshake_buckets", C.c_uint64 * 11),
@@ -137,6 +142,9 @@ SIGNATURES = [
     ("gpuagg_set_apiserver_ips", C.c_int, [C.c_void_p, u32p, C.c_size_t]),
     ("gpuagg_latency_read", C.c_int, [C.c_void_p, C.POINTER(LatencyState)]),
     ("gpuagg_set_time_offset", C.c_int, [C.c_void_p, C.c_int64]),
+    ("gpuagg_ipcache_set", C.c_int, [C.c_void_p, u32p, u32p, u32p, C.c_size_t]),
+    ("gpuagg_hubble_decode_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t,
+                                              C.POINTER(HubbleCols)]),
 ]
 
 _lib = None

@@ -18,7 +18,8 @@ LIB = os.path.join(HERE, "libgpuagg.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["gpuagg_kernels.hip", "gpuagg_decode.hip", "gpuagg_latency.hip", "gpuagg_runtime.cpp"]
+SOURCES = ["gpuagg_kernels.hip", "gpuagg_decode.hip", "gpuagg_latency.hip", "gpuagg_hubble.hip",
+           "gpuagg_runtime.cpp"]
 HEADERS = ["gpuagg_internal.h", "gpuagg_launch.h", os.path.join("..", "..", "include", "gpuagg.h")]
 
 

@@ -83,6 +83,18 @@ struct DecodeArgs {
 };
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
 
+// Hubble-mode L3/L4 enrichment (gpuagg_hubble.hip).
+constexpr uint32_t kIpcEmpty = 0xFFFFFFFFu, kIpcNoMeta = 0xFFFFFFFFu, kIdentityWorld = 2;
+enum : uint32_t { kSummaryNone = 0, kSummaryTcp = 1, kSummaryUdp = 2, kSummaryDrop = 3, kSummaryDns = 4 };
+struct HubbleArgs {
+  const uint4 *table;  // (ip, identity, metadata id, 0); ip kIpcEmpty = free
+  uint32_t mask, seed, max_probe;
+  const uint32_t *src, *dst, *meta, *dns;
+  size_t n;
+  uint32_t *o_sid, *o_did, *o_smeta, *o_dmeta, *o_kind, *o_arg;
+};
+hipError_t launch_hubble(const HubbleArgs &a, uint32_t n_cu, hipStream_t st);
+
 // Node-apiserver latency join (gpuagg_latency.hip).
 struct LatEvent {
   uint64_t k0, k1;   // request-oriented key: src | dst << 32, sport | dport << 16 | id << 32

@@ -186,6 +186,10 @@ struct gpuagg_ctx {
   // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
   uint8_t *d_ipl = nullptr;
   size_t ipl_alloc = 0;
+  // Hubble ipcache image (gpuagg_hubble.hip)
+  uint4 *d_ipc = nullptr;
+  size_t ipc_cap = 0;
+  uint32_t ipc_seed = 0, ipc_max_probe = 0;
   // node-apiserver latency join (gpuagg_latency.hip)
   uint32_t lat_enabled = 0;  // bit 0 latency, 1 handshake, 2 no_response
   std::vector<uint32_t> api_ips;
@@ -1076,6 +1080,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_rblk);
   dev_free(c->d_ipl);
   dev_free(c->d_ipl_all);
+  dev_free(c->d_ipc);
   dev_free(c->d_api);
   dev_free(c->d_lat);
   dev_free(c->d_lat_blk_cnt);
@@ -1512,6 +1517,7 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
   dev_free(c->d_ipl_all);
+  dev_free(c->d_ipc);
   dev_free(c->d_api);
   dev_free(c->d_lat);
   dev_free(c->d_lat_blk_cnt);
@@ -1546,6 +1552,7 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_all_alloc) {
         dev_free(c->d_ipl_all);
+  dev_free(c->d_ipc);
   dev_free(c->d_api);
   dev_free(c->d_lat);
   dev_free(c->d_lat_blk_cnt);
@@ -2449,6 +2456,71 @@ int gpuagg_set_apiserver_ips(gpuagg_ctx *c, const uint32_t *ipv4, size_t n) {
   if (!c->d_api && (rc = dev_alloc(c, &c->d_api, kLatMaxApi))) return rc;
   c->api_ips.assign(ipv4, ipv4 + n);
   if (n) HIPCHK(c, hipMemcpy(c->d_api, ipv4, n * 4, hipMemcpyHostToDevice));
+  return GPUAGG_OK;
+}
+
+int gpuagg_ipcache_set(gpuagg_ctx *c, const uint32_t *ipv4, const uint32_t *identity, const uint32_t *meta_id,
+                       size_t n) {
+  if (!c || (n && (!ipv4 || !identity || !meta_id))) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  // open addressing, linear probing, load <= 50 %; the last entry for an IP wins
+  size_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  const uint32_t seed = 0x7F4A7C15u, mask = (uint32_t)(cap - 1);
+  std::vector<uint4> tab(cap, uint4{kIpcEmpty, 0u, 0u, 0u});
+  uint32_t max_probe = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (ipv4[i] == kIpcEmpty) return fail(c, GPUAGG_ERANGE, "255.255.255.255 cannot be an ipcache key");
+    uint32_t h = ip_h1(ipv4[i], seed) & mask, p = 0;
+    while (tab[h].x != kIpcEmpty && tab[h].x != ipv4[i]) {
+      h = (h + 1) & mask;
+      ++p;
+    }
+    tab[h] = uint4{ipv4[i], identity[i], meta_id[i], 0u};
+    max_probe = std::max(max_probe, p);
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight decodes read the old image
+  if (cap != c->ipc_cap) {
+    dev_free(c->d_ipc);
+    c->ipc_cap = 0;
+    if ((rc = dev_alloc(c, &c->d_ipc, cap))) return rc;
+    c->ipc_cap = cap;
+  }
+  HIPCHK(c, hipMemcpy(c->d_ipc, tab.data(), cap * sizeof(uint4), hipMemcpyHostToDevice));
+  c->ipc_seed = seed;
+  c->ipc_max_probe = max_probe;
+  return GPUAGG_OK;
+}
+
+int gpuagg_hubble_decode_device(gpuagg_ctx *c, const gpuagg_columns *in, size_t n, const gpuagg_hubble_cols *out) {
+  if (!c || !in || !out) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
+  if (!in->src_ip || !in->dst_ip || !in->meta || !out->src_identity || !out->dst_identity || !out->src_meta ||
+      !out->dst_meta || !out->summary_kind || !out->summary_arg)
+    return fail(c, GPUAGG_EINVAL, "hubble decode: null column");
+  if (!c->ipc_cap) {  // no image yet: every IP resolves to World
+    if ((rc = gpuagg_ipcache_set(c, nullptr, nullptr, nullptr, 0))) return rc;
+  }
+  HubbleArgs a{};
+  a.table = c->d_ipc;
+  a.mask = (uint32_t)(c->ipc_cap - 1);
+  a.seed = c->ipc_seed;
+  a.max_probe = c->ipc_max_probe;
+  a.src = in->src_ip;
+  a.dst = in->dst_ip;
+  a.meta = in->meta;
+  a.dns = in->dns_id;
+  a.n = n;
+  a.o_sid = out->src_identity;
+  a.o_did = out->dst_identity;
+  a.o_smeta = out->src_meta;
+  a.o_dmeta = out->dst_meta;
+  a.o_kind = out->summary_kind;
+  a.o_arg = out->summary_arg;
+  HIPCHK(c, launch_hubble(a, c->n_cu, c->stream));
   return GPUAGG_OK;
 }
 

@@ -282,6 +282,21 @@ class GpuAgg:
                 "handshake_buckets": list(st.handshake_buckets), "handshake_count": st.handshake_count,
                 "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending}
 
+    # -- Hubble-mode L3/L4 enrichment (gpuagg_hubble.hip) ------------------------------
+    def ipcache_set(self, ips: Sequence[int], identities: Sequence[int], meta_ids: Sequence[int]) -> None:
+        n = len(ips)
+        arr = lambda v: (C.c_uint32 * max(1, n))(*[int(x) for x in v])  # noqa: E731
+        self._check(self.lib.gpuagg_ipcache_set(self.h, arr(ips), arr(identities), arr(meta_ids), n))
+
+    def hubble_decode_device(self, cols: "_abi.Columns", n: int, out) -> None:
+        """out: six device tensors (int32): src/dst identity, src/dst meta, summary kind, arg."""
+        self._torch_sync()
+
+        def ptr(t):
+            return C.cast(C.c_void_p(t.data_ptr()), _abi.u32p)
+        hc = _abi.HubbleCols(*[ptr(t) for t in out])
+        self._check(self.lib.gpuagg_hubble_decode_device(self.h, C.byref(cols), n, C.byref(hc)))
+
     def submit_device(self, cols: "_abi.Columns", n: int) -> None:
         self._check(self.lib.gpuagg_submit_device(self.h, C.byref(cols), n))
 
