@@ -66,10 +66,26 @@ __global__ __launch_bounds__(kLatThreads) void lat_count_kernel(LatArgs a) {
   __syncthreads();
   const uint32_t u = blockIdx.x * (kLatThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (u >= a.blocks) return;
-  const size_t lo = (size_t)u * a.chunk, hi = min(lo + a.chunk, a.n);
+  const size_t lo = min((size_t)u * a.chunk, a.n), hi = min(lo + a.chunk, a.n);  // (chunks round up)
   uint32_t cnt = 0;
   unsigned long long mx = 0;
-  for (size_t i = lo + lane; i < hi; i += 64) {
+  size_t i0 = lo;
+  if (a.vec) {  // 4 rows per lane: 16-byte loads of meta / tcp_id, 2 x 16 bytes of time
+    const uint4 *m4 = (const uint4 *)a.meta, *t4 = (const uint4 *)a.tcp_id;
+    const ulonglong2 *c2 = (const ulonglong2 *)a.time_ns;
+    const size_t hi4 = lo + ((hi - lo) & ~(size_t)3);
+    for (size_t j = lo + 4 * lane; j < hi4; j += 256) {
+      const uint4 m = m4[j >> 2], t = t4[j >> 2];
+      const ulonglong2 c0 = c2[j >> 1], c1 = c2[(j >> 1) + 1];
+      mx = max(mx, max(max(c0.x, c0.y), max(c1.x, c1.y)));
+      const uint32_t mm[4] = {m.x, m.y, m.z, m.w}, tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)  // rows that can be events check the IPs (rare)
+        if ((mm[q] & 0xFFu) == 6u && tt[q] != 0u && (mm[q] >> 30) >= 2u) cnt += lat_role(a, api, j + q) != 0u;
+    }
+    i0 = hi4;
+  }
+  for (size_t i = i0 + lane; i < hi; i += 64) {
     cnt += lat_role(a, api, i) != 0u;
     mx = max(mx, (unsigned long long)a.time_ns[i]);
   }
@@ -131,7 +147,7 @@ __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
   __syncthreads();
   const uint32_t u = blockIdx.x * (kLatThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
   if (u >= a.blocks || a.blk_cnt[u] == 0) return;
-  const size_t lo = (size_t)u * a.chunk, hi = min(lo + a.chunk, a.n);
+  const size_t lo = min((size_t)u * a.chunk, a.n), hi = min(lo + a.chunk, a.n);  // (chunks round up)
   uint64_t base = a.blk_base[u];
   unsigned long long clk = a.blk_clk[u];
   for (size_t r = lo; r < hi; r += 64) {

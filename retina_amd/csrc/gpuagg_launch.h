@@ -117,8 +117,9 @@ struct LatArgs {
   const uint32_t *src, *dst, *meta, *ports, *tcp_id;
   const uint64_t *time_ns;
   size_t n;
-  uint64_t chunk;   // rows per unit
+  uint64_t chunk;   // rows per unit (a multiple of 4 when vec)
   uint32_t blocks;  // units (one wave each)
+  bool vec;         // meta / tcp_id / time_ns 16-byte aligned: vector loads in the count pass
   const uint32_t *api;
   uint32_t n_api;
   unsigned long long *state;

@@ -733,7 +733,8 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.n = n;
   // units: one wave over >= 2048 contiguous rows, at most 64k units
   a.blocks = (uint32_t)std::min<uint64_t>(kLatMaxUnits, (n + 2047) / 2048);
-  a.chunk = (n + a.blocks - 1) / a.blocks;
+  a.chunk = ((n + a.blocks - 1) / a.blocks + 3) & ~3ULL;
+  a.vec = (((uintptr_t)cv.meta | (uintptr_t)cv.tcp_id | (uintptr_t)cv.time_ns) & 15u) == 0;
   a.api = c->d_api;
   a.n_api = (uint32_t)c->api_ips.size();
   a.state = c->d_lat;
