@@ -33,8 +33,8 @@ def test_hubble_decode_matches_oracle(gpu_device):
         g.ipcache_set([ips[i] for i in sel], [int(ident[i]) for i in sel], [int(meta_id[i]) for i in sel])
         dev = torch.device("cuda", gpu_device)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)  # noqa: E731
-        cols = GpuAgg.device_columns(t(recs.src_ip), t(recs.dst_ip), t(recs.bytes), t(recs.meta), t(recs.ports),
-                                     t(recs.dns_id))
+        keep = [t(recs.src_ip), t(recs.dst_ip), t(recs.bytes), t(recs.meta), t(recs.ports), t(recs.dns_id)]
+        cols = GpuAgg.device_columns(*keep)  # (the tensors must outlive the decode)
         n = len(recs.src_ip)
         out = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(6)]
         g.hubble_decode_device(cols, n, out)
