@@ -731,8 +731,9 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.tcp_id = cv.tcp_id;
   a.time_ns = cv.time_ns;
   a.n = n;
-  // units: one wave over >= 2048 contiguous rows, at most 64k units
-  a.blocks = (uint32_t)std::min<uint64_t>(kLatMaxUnits, (n + 2047) / 2048);
+  // units: one wave over >= 8192 contiguous rows (16 waves per CU at 100M rows; the
+  // one-workgroup scan reads a dozen units per thread)
+  a.blocks = (uint32_t)std::min<uint64_t>(kLatMaxUnits, (n + 8191) / 8192);
   a.chunk = ((n + a.blocks - 1) / a.blocks + 3) & ~3ULL;
   a.vec = (((uintptr_t)cv.meta | (uintptr_t)cv.tcp_id | (uintptr_t)cv.time_ns) & 15u) == 0;
   a.api = c->d_api;
