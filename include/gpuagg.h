@@ -358,6 +358,19 @@ int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);
 int gpuagg_set_time_offset(gpuagg_ctx *ctx, int64_t ns);
 
 /* ------------------------------------------------------------------------------
+ * Enriched-flow emission, standard mode (Enricher.enrich + export, enricher.go:102-140;
+ * consumers read them through ExportReader, :189-191): per record, the endpoint that
+ * getEndpoint puts into flow.Source / flow.Destination, as the pod's slot (the slot's
+ * namespace/name is the cache key of the RetinaEndpoint whose labels and owner
+ * references the caller renders), or -1 when the IP is not a pod (service, node or not
+ * in the cache: the endpoint stays nil).  Uses the IP -> pod map installed by
+ * gpuagg_set_endpoints / gpuagg_cache_commit (GPUAGG_ESTATE before the first one).
+ * Async on the ctx's stream, ordered after earlier submits (gpuagg_sync waits).
+ * ---------------------------------------------------------------------------- */
+int gpuagg_enrich_device(gpuagg_ctx *ctx, const gpuagg_columns *in, size_t n, int32_t *src_slot,
+                         int32_t *dst_slot);
+
+/* ------------------------------------------------------------------------------
  * Hubble-mode L3/L4 enrichment (pkg/hubble/parser/parser_linux.go:64-93,
  * layer34/parser_linux.go:30-84, seven/parser_linux.go:28-146,
  * common/decoder_linux.go:32-60): per record, the source / destination endpoint from the

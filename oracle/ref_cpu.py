@@ -17,9 +17,10 @@ LIB = os.path.join(HERE, "libref_cpu.so")
 
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        tmp = "%s.%d.tmp" % (LIB, os.getpid())
         subprocess.run(["gcc", "-O2", "-std=c11", "-D_GNU_SOURCE", "-shared", "-fPIC", "-Wall", "-pthread",
-                        "-o", LIB + ".tmp", SRC], check=True)
-        os.replace(LIB + ".tmp", LIB)
+                        "-o", tmp, SRC], check=True)
+        os.replace(tmp, LIB)  # atomic: concurrent builders (spawned ranks) never see a partial file
     return LIB
 
 
@@ -51,6 +52,8 @@ def lib():
 
 
 class RefCPU:
+    h = None  # set once ref_create succeeds; close()/__del__ check it
+
     def __init__(self, spec: List[dict], endpoints, remote: bool, dns=()):
         L = lib()
         self.L = L

@@ -145,6 +145,7 @@ SIGNATURES = [
     ("gpuagg_ipcache_set", C.c_int, [C.c_void_p, u32p, u32p, u32p, C.c_size_t]),
     ("gpuagg_hubble_decode_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t,
                                               C.POINTER(HubbleCols)]),
+    ("gpuagg_enrich_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t, C.c_void_p, C.c_void_p]),
 ]
 
 _lib = None

@@ -1826,7 +1826,7 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
   }  // long lists
   __syncthreads();
-  if (stage) {  // staged: this window partial, whole, for stage_reduce_b_kernel
+  if (stage) {  // staged: this window partial, whole, for stage_reduce_kernel
     uint4 *dst = (uint4 *)(stage + ((size_t)b * W));
     for (uint32_t i = threadIdx.x; i < W / 2; i += blockDim.x) dst[i] = ((const uint4 *)win)[i];
     return;
@@ -1841,19 +1841,19 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
 }
 
-// Sums the tier-1 workgroups' staged u32 bins: blockIdx.y takes 1/gridDim.y of the
-// copies, so each bin gets gridDim.y global atomics instead of one per workgroup.
-__global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *stage, uint32_t ncopies,
-                                                             uint32_t stride, uint32_t L4, Plan p,
-                                                             DevDense d) {
-  const uint32_t bin = blockIdx.x * blockDim.x + threadIdx.x;
+// Sums the tier-1 workgroups' staged u32 bins: part `y` of `ny` takes 1/ny of the
+// copies, so each bin gets ny global atomics instead of one per workgroup.
+__device__ __forceinline__ void stage_reduce_a(const uint32_t *stage, uint32_t ncopies, uint32_t stride,
+                                               uint32_t L4, const Plan &p, const DevDense &d, uint32_t bx,
+                                               uint32_t y, uint32_t ny) {
+  const uint32_t bin = bx * 256u + threadIdx.x;
   if (bin >= L4) return;
   bool packed = false;
   for (int g = 0; g < p.ngroups; ++g)
     if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
       packed = p.g[g].family <= FAM_DROP;
-  const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * blockIdx.y) / gridDim.y);
-  const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (blockIdx.y + 1)) / gridDim.y);
+  const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * y) / ny);
+  const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (y + 1)) / ny);
   unsigned long long cnt = 0, byt = 0;
 #pragma unroll 8  // 8 independent copy loads in flight per lane
   for (uint32_t c = c0; c < c1; ++c) {
@@ -1866,11 +1866,10 @@ __global__ __launch_bounds__(256) void stage_reduce_a_kernel(const uint32_t *sta
 }
 
 // Sums the fold partials of every partition of a window (layout of spill_window_kernel).
-__global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long long *stage,
-                                                             uint32_t nwin, uint32_t nparts,
-                                                             uint32_t W, uint32_t lo0,
-                                                             uint64_t dense_len, DevDense d) {
-  const uint32_t off = blockIdx.x * blockDim.x + threadIdx.x;  // over nwin * W bins
+__device__ __forceinline__ void stage_reduce_b(const unsigned long long *stage, uint32_t nwin, uint32_t nparts,
+                                               uint32_t W, uint32_t lo0, uint64_t dense_len, const DevDense &d,
+                                               uint32_t bx) {
+  const uint32_t off = bx * 256u + threadIdx.x;  // over nwin * W bins
   const uint32_t w = off / W, i = off % W;
   if (w >= nwin || lo0 + (uint64_t)off >= dense_len) return;
   unsigned long long cnt = 0, byt = 0;
@@ -1883,6 +1882,20 @@ __global__ __launch_bounds__(256) void stage_reduce_b_kernel(const unsigned long
   }
   if (cnt) atomicAdd(&d.cnt[lo0 + off], cnt);
   if (byt) atomicAdd(&d.byt[lo0 + off], byt);
+}
+
+// Both staged reductions in one launch (they are independent: the tier-1 bins and the
+// fold partials of the spilled groups), so the step ends with one small launch instead of
+// two.  Blocks [0, na) sum the tier-1 copies (na = bin blocks x ny copy parts), the rest
+// the fold partials.
+__global__ __launch_bounds__(256) void stage_reduce_kernel(const uint32_t *stage_a, uint32_t ncopies, uint32_t stride,
+                                                           uint32_t L4, uint32_t na_x, uint32_t ny, Plan p,
+                                                           const unsigned long long *stage_b, uint32_t nwin,
+                                                           uint32_t nparts, uint32_t W, uint32_t lo0,
+                                                           uint64_t dense_len, DevDense d) {
+  const uint32_t na = stage_a ? na_x * ny : 0u;
+  if (blockIdx.x < na) stage_reduce_a(stage_a, ncopies, stride, L4, p, d, blockIdx.x % na_x, blockIdx.x / na_x, ny);
+  else stage_reduce_b(stage_b, nwin, nparts, W, lo0, dense_len, d, blockIdx.x - na);
 }
 
 // Writes every slot whole (k0 k1 = 0, k2 = pending, cnt byt pad = 0): four 16-byte
@@ -2018,6 +2031,36 @@ hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipSt
   return hipGetLastError();
 }
 
+// ---- enriched-flow emission (standard mode) ----------------------------------------
+// Enricher.enrich (enricher.go:102-135) fills flow.Source / flow.Destination from
+// Cache.GetObjByIP and exports every IPv4 flow to the output ring (export, :137-140).
+// IPv4 addresses of u32 records are never "", so every record is exported; the endpoint
+// is the pod's slot (its namespace/name key names the cache object whose labels and
+// owner references getEndpoint copies) or -1 when GetObjByIP returns no pod (service,
+// node or unknown IP: getEndpoint returns nil, :157-164).  The HBM IP table is the one
+// the aggregation kernels probe.  HBM-bound: 8 B read + 8 B written per record.
+__global__ __launch_bounds__(256) void enrich_kernel(DevIpTable t, const uint32_t *src, const uint32_t *dst,
+                                                     uint64_t n, int32_t *os, int32_t *od, uint32_t vec) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t tail = 0;
+  if (vec) {  // 4 records per lane: one 16-byte load per input column, one store per output
+    const uint64_t n4 = n >> 2;
+    for (uint64_t i = t0; i < n4; i += stride) {
+      const uint4 s = ((const uint4 *)src)[i], d = ((const uint4 *)dst)[i];
+      const Lk a0 = ip_lookup(t, s.x), a1 = ip_lookup(t, s.y), a2 = ip_lookup(t, s.z), a3 = ip_lookup(t, s.w);
+      const Lk b0 = ip_lookup(t, d.x), b1 = ip_lookup(t, d.y), b2 = ip_lookup(t, d.z), b3 = ip_lookup(t, d.w);
+      ((int4 *)os)[i] = make_int4(a0.slot, a1.slot, a2.slot, a3.slot);
+      ((int4 *)od)[i] = make_int4(b0.slot, b1.slot, b2.slot, b3.slot);
+    }
+    tail = n4 << 2;
+  }
+  for (uint64_t i = tail + t0; i < n; i += stride) {
+    os[i] = ip_lookup(t, src[i]).slot;
+    od[i] = ip_lookup(t, dst[i]).slot;
+  }
+}
+
 // ---- launch wrappers called by the host runtime ---------------------------------------
 
 static DevSparse dev_sparse(const SparseView &v) {
@@ -2126,11 +2169,19 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   }
   if (e != hipSuccess) return e;
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
-  if (a.stage_a) {
-    hipLaunchKernelGGL(stage_reduce_a_kernel, dim3((a.lds_bins + 255) / 256, 8), dim3(256), 0, st,
-                       a.stage_a, a.blocks, a.stage_a_stride, a.lds_bins, a.plan, k.d);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
+  // the tier-1 copies are summed by stage_reduce_kernel after the fold (one launch for
+  // both reductions); without a fold they get it alone
+  const uint32_t ra_x = (a.lds_bins + 255) / 256, ra_y = 8;
+  const uint32_t W = 1u << a.win_shift;
+  auto reduce = [&](bool with_b) -> hipError_t {
+    const uint32_t na = a.stage_a ? ra_x * ra_y : 0u;
+    const uint32_t nb = with_b ? (a.nwin * W + 255) / 256 : 0u;
+    if (na + nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(stage_reduce_kernel, dim3(na + nb), dim3(256), 0, st, a.stage_a, a.blocks, a.stage_a_stride,
+                       a.lds_bins, ra_x, ra_y, a.plan, (const unsigned long long *)a.stage_b, a.nwin,
+                       with_b ? a.win_blocks / a.nwin : 0u, W, a.spill_lo, a.dense_len, k.d);
+    return hipGetLastError();
+  };
   if (a.sp_lists) {
     const size_t seg_lds = (size_t)16 << a.sparse.seg_log2;
     if ((e = hipFuncSetAttribute((const void *)sparse_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2140,20 +2191,15 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
                        (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  if (!a.spill) return hipSuccess;
+  if (!a.spill) return reduce(false);
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  const uint32_t W = 1u << a.win_shift;
   hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
                      (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
                      a.spill_lo, a.dense_len, W, a.nwin, k.d, (unsigned long long *)a.stage_b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (a.stage_b)
-    hipLaunchKernelGGL(stage_reduce_b_kernel, dim3((a.nwin * W + 255) / 256), dim3(256), 0, st,
-                       (const unsigned long long *)a.stage_b, a.nwin, a.win_blocks / a.nwin, W,
-                       a.spill_lo, a.dense_len, k.d);
-  return hipGetLastError();
+  return reduce(a.stage_b != nullptr);
 }
 
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st) {
@@ -2176,6 +2222,19 @@ hipError_t launch_sparse_import(const SparseView &v, const uint64_t *in, size_t 
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(sparse_import_kernel, dim3(blocks), dim3(256), 0, st, dev_sparse(v),
                      (const unsigned long long *)in, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_enrich(const EnrichArgs &a, uint32_t n_cu, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  auto al = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+  const uint32_t vec = al(a.src) && al(a.dst) && al(a.o_src) && al(a.o_dst);
+  const uint64_t lanes = vec ? (a.n + 3) / 4 : a.n;
+  const uint64_t need = (lanes + 255) / 256;
+  const uint32_t blocks = (uint32_t)(need < (uint64_t)n_cu * 8 ? need : (uint64_t)n_cu * 8);
+  hipLaunchKernelGGL(enrich_kernel, dim3(blocks), dim3(256), 0, st,
+                     DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk}, a.src, a.dst,
+                     (uint64_t)a.n, a.o_src, a.o_dst, vec);
   return hipGetLastError();
 }
 

@@ -83,6 +83,18 @@ struct DecodeArgs {
 };
 hipError_t launch_decode(const DecodeArgs &a, hipStream_t st);
 
+// Standard-mode enriched-flow emission (enrich_kernel, gpuagg_kernels.hip).
+struct EnrichArgs {
+  const uint64_t *ip_slots;
+  uint32_t ip_mask, ip_seed;
+  const uint16_t *ip_pre;
+  const uint32_t *ip_blk;
+  const uint32_t *src, *dst;
+  size_t n;
+  int32_t *o_src, *o_dst;
+};
+hipError_t launch_enrich(const EnrichArgs &a, uint32_t n_cu, hipStream_t st);
+
 // Hubble-mode L3/L4 enrichment (gpuagg_hubble.hip).
 constexpr uint32_t kIpcEmpty = 0xFFFFFFFFu, kIpcNoMeta = 0xFFFFFFFFu, kIdentityWorld = 2;
 enum : uint32_t { kSummaryNone = 0, kSummaryTcp = 1, kSummaryUdp = 2, kSummaryDrop = 3, kSummaryDns = 4 };

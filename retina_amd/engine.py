@@ -282,6 +282,18 @@ class GpuAgg:
                 "handshake_buckets": list(st.handshake_buckets), "handshake_count": st.handshake_count,
                 "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending}
 
+    # -- enriched-flow emission, standard mode (enrich_kernel) --------------------------
+    def enrich_device(self, cols: "_abi.Columns", n: int, src_slot, dst_slot) -> None:
+        """Enricher.enrich + export (enricher.go:102-140) for n device-resident records:
+        writes each record's source / destination pod slot (-1: no endpoint) into the two
+        int32 device tensors; async on the engine's stream (sync() waits)."""
+        self._torch_sync()
+        for t in (src_slot, dst_slot):
+            if t.numel() < n or t.element_size() != 4:
+                raise ValueError("enrich_device: output tensors need n int32 elements")
+        self._check(self.lib.gpuagg_enrich_device(self.h, C.byref(cols), n, C.c_void_p(src_slot.data_ptr()),
+                                                  C.c_void_p(dst_slot.data_ptr())))
+
     # -- Hubble-mode L3/L4 enrichment (gpuagg_hubble.hip) ------------------------------
     def ipcache_set(self, ips: Sequence[int], identities: Sequence[int], meta_ids: Sequence[int]) -> None:
         n = len(ips)
