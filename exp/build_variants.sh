@@ -10,8 +10,10 @@ for v in "$@"; do
   D=""; for d in ${v//+/ }; do D="$D -D$d"; done
   ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -fPIC -std=c++17 -I $C -I include $D -c $C/gpuagg_kernels.hip -o /tmp/k_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -fPIC -std=c++17 -I $C -I include $D -c $C/gpuagg_decode.hip -o /tmp/d_$name.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -fPIC -std=c++17 -I $C -I include $D -c $C/gpuagg_latency.hip -o /tmp/l_$name.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -fPIC -std=c++17 -I $C -I include $D -c $C/gpuagg_hubble.hip -o /tmp/h_$name.o &&
     /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 -I $C -I include $D -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include -x c++ -c $C/gpuagg_runtime.cpp -o /tmp/rt_$name.o &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o exp/lib_$name.so /tmp/k_$name.o /tmp/d_$name.o /tmp/rt_$name.o -Wl,--version-script=$C/gpuagg.map ) &
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o exp/lib_$name.so /tmp/k_$name.o /tmp/d_$name.o /tmp/l_$name.o /tmp/h_$name.o /tmp/rt_$name.o -Wl,--version-script=$C/gpuagg.map ) &
 done
 wait
 ls -la exp/*.so

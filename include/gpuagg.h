@@ -369,6 +369,12 @@ int gpuagg_set_time_offset(gpuagg_ctx *ctx, int64_t ns);
  * ---------------------------------------------------------------------------- */
 int gpuagg_enrich_device(gpuagg_ctx *ctx, const gpuagg_columns *in, size_t n, int32_t *src_slot,
                          int32_t *dst_slot);
+/* Host-fed: gpuagg_submit of the batch plus its enriched endpoints, from one H2D copy.
+ * The slots (host memory, n each) are written before the call returns; the aggregation
+ * may still be running, as after gpuagg_submit.  This is what a plugin with an
+ * ExportReader / SetupChannel consumer calls instead of gpuagg_submit. */
+int gpuagg_submit_enrich(gpuagg_ctx *ctx, gpuagg_batch *batch, size_t n, int32_t *src_slot,
+                         int32_t *dst_slot);
 
 /* ------------------------------------------------------------------------------
  * Hubble-mode L3/L4 enrichment (pkg/hubble/parser/parser_linux.go:64-93,

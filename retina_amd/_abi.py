@@ -146,6 +146,7 @@ SIGNATURES = [
     ("gpuagg_hubble_decode_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t,
                                               C.POINTER(HubbleCols)]),
     ("gpuagg_enrich_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t, C.c_void_p, C.c_void_p]),
+    ("gpuagg_submit_enrich", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
 ]
 
 _lib = None

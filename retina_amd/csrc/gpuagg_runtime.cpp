@@ -268,6 +268,9 @@ struct gpuagg_ctx {
   // staged flushes: per-workgroup LDS bins (tier-1) and per-partition fold windows
   uint32_t *d_stage_a = nullptr;
   size_t stage_a_alloc = 0;
+  int32_t *d_enrich = nullptr;  // gpuagg_submit_enrich: [2][cap] endpoint slots
+  size_t enrich_alloc = 0;
+  hipEvent_t enrich_done = nullptr;
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
   // raw perf-record decode (gpuagg_decode.hip)
@@ -1057,6 +1060,10 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
       gpuagg_destroy(c.release());
       return GPUAGG_EDEVICE;
     }
+  if (hipEventCreateWithFlags(&c->enrich_done, hipEventDisableTiming) != hipSuccess) {
+    gpuagg_destroy(c.release());
+    return GPUAGG_EDEVICE;
+  }
   c->n_cu = (uint32_t)prop.multiProcessorCount;
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
@@ -1113,6 +1120,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_spill);
   dev_free(c->d_spill_count);
   dev_free(c->d_stage_a);
+  dev_free(c->d_enrich);
   dev_free(c->d_stage_b);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
@@ -1128,6 +1136,9 @@ void gpuagg_destroy(gpuagg_ctx *c) {
     dev_free(st.raw);
     if (st.copied) hipEventDestroy(st.copied);
     if (st.released) hipEventDestroy(st.released);
+  }
+  if (c->enrich_done) {
+    hipEventDestroy(c->enrich_done);
   }
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -1828,11 +1839,9 @@ void gpuagg_free_batch(gpuagg_ctx *c, gpuagg_batch *b) {
   delete b;
 }
 
-int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
-  if (!c || !b || n > b->capacity) return GPUAGG_EINVAL;
-  int rc = bind(c);
-  if (rc) return rc;
-  if (n == 0) return GPUAGG_OK;
+// Enqueues the H2D copies of the columns the plan reads into the next staging buffer.
+int stage_batch(gpuagg_ctx *c, const gpuagg_batch *b, size_t n, gpuagg_ctx::Staging **out, ColsView *cv) {
+  int rc;
   if ((rc = ensure_staging(c, b->capacity))) return rc;
   gpuagg_ctx::Staging *s;
   if ((rc = acquire_staging(c, &s))) return rc;
@@ -1842,14 +1851,68 @@ int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
   for (int i = 0; i < 6; ++i)
     if (need[i] || (i == 4 && c->lat_enabled))
       HIPCHK(c, hipMemcpyAsync(s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
-  ColsView cv{s->cols[0], s->cols[1], s->cols[2], s->cols[3], s->cols[4], s->cols[5]};
+  *cv = ColsView{s->cols[0], s->cols[1], s->cols[2], s->cols[3], s->cols[4], s->cols[5]};
   if (c->lat_enabled) {
     HIPCHK(c, hipMemcpyAsync(s->tcp_id, b->cols.tcp_id, n * 4, hipMemcpyHostToDevice, c->copy_stream));
     HIPCHK(c, hipMemcpyAsync(s->time_ns, b->cols.time_ns, n * 8, hipMemcpyHostToDevice, c->copy_stream));
-    cv.tcp_id = s->tcp_id;
-    cv.time_ns = s->time_ns;
+    cv->tcp_id = s->tcp_id;
+    cv->time_ns = s->time_ns;
   }
+  *out = s;
+  return GPUAGG_OK;
+}
+
+int enrich_launch(gpuagg_ctx *c, const uint32_t *src, const uint32_t *dst, size_t n, int32_t *os, int32_t *od) {
+  EnrichArgs a{};
+  a.ip_slots = c->d_ip;
+  a.ip_mask = (uint32_t)(c->ip_cap / 2 - 1);  // bucket mask
+  a.ip_pre = c->radix ? c->d_rpre : nullptr;
+  a.ip_blk = c->radix ? c->d_rblk : nullptr;
+  a.ip_seed = c->ip_seed;
+  a.src = src;
+  a.dst = dst;
+  a.n = n;
+  a.o_src = os;
+  a.o_dst = od;
+  HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
+  return GPUAGG_OK;
+}
+
+int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
+  if (!c || !b || n > b->capacity) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
+  gpuagg_ctx::Staging *s;
+  ColsView cv{};
+  if ((rc = stage_batch(c, b, n, &s, &cv))) return rc;
   return run_staged(c, *s, [&] { return launch(c, cv, n); });
+}
+
+int gpuagg_submit_enrich(gpuagg_ctx *c, gpuagg_batch *b, size_t n, int32_t *src_slot, int32_t *dst_slot) {
+  if (!c || !b || n > b->capacity || !src_slot || !dst_slot) return GPUAGG_EINVAL;
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
+  if (!c->ip_cap) return fail(c, GPUAGG_ESTATE, "gpuagg_set_endpoints was never called");
+  if ((rc = ensure_buf(c, &c->d_enrich, &c->enrich_alloc, 2 * b->capacity))) return rc;
+  gpuagg_ctx::Staging *s;
+  ColsView cv{};
+  if ((rc = stage_batch(c, b, n, &s, &cv))) return rc;
+  rc = run_staged(c, *s, [&] {
+    // the endpoints first, so the host copy does not wait for the aggregation
+    int r = enrich_launch(c, cv.src_ip, cv.dst_ip, n, c->d_enrich, c->d_enrich + n);
+    if (r) return r;
+    HIPCHK(c, hipMemcpyAsync(src_slot, c->d_enrich, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dst_slot, c->d_enrich + n, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if ((r = launch(c, cv, n))) return r;
+    // the slots are the caller's on return (the aggregation may still run)
+    HIPCHK(c, hipEventRecord(c->enrich_done, c->stream));
+    return GPUAGG_OK;
+  });
+  if (rc) return rc;
+  HIPCHK(c, hipEventSynchronize(c->enrich_done));
+  return GPUAGG_OK;
 }
 
 int gpuagg_submit_device(gpuagg_ctx *c, const gpuagg_columns *d, size_t n) {
@@ -2541,19 +2604,7 @@ int gpuagg_enrich_device(gpuagg_ctx *c, const gpuagg_columns *in, size_t n, int3
   if (!in->src_ip || !in->dst_ip || !src_slot || !dst_slot)
     return fail(c, GPUAGG_EINVAL, "enrich: null column");
   if (!c->ip_cap) return fail(c, GPUAGG_ESTATE, "gpuagg_set_endpoints was never called");
-  EnrichArgs a{};
-  a.ip_slots = c->d_ip;
-  a.ip_mask = (uint32_t)(c->ip_cap / 2 - 1);  // bucket mask
-  a.ip_pre = c->radix ? c->d_rpre : nullptr;
-  a.ip_blk = c->radix ? c->d_rblk : nullptr;
-  a.ip_seed = c->ip_seed;
-  a.src = in->src_ip;
-  a.dst = in->dst_ip;
-  a.n = n;
-  a.o_src = src_slot;
-  a.o_dst = dst_slot;
-  HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
-  return GPUAGG_OK;
+  return enrich_launch(c, in->src_ip, in->dst_ip, n, src_slot, dst_slot);
 }
 
 int gpuagg_set_time_offset(gpuagg_ctx *c, int64_t ns) {

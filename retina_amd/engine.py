@@ -232,6 +232,13 @@ class GpuAgg:
     def submit(self, batch: HostBatch, n: int) -> None:
         self._check(self.lib.gpuagg_submit(self.h, batch.ptr, n))
 
+    def submit_enrich(self, batch: HostBatch, n: int):
+        """gpuagg_submit + the batch's enriched endpoints (src, dst slot arrays, -1: none)."""
+        src = np.empty(n, np.int32)
+        dst = np.empty(n, np.int32)
+        self._check(self.lib.gpuagg_submit_enrich(self.h, batch.ptr, n, src.ctypes.data, dst.ctypes.data))
+        return src, dst
+
     def submit_numpy(self, batch, chunk: int = 1 << 22) -> None:
         """Host-fed path: streams a numpy column batch through pinned buffers."""
         total = len(batch.src_ip)

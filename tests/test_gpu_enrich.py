@@ -112,3 +112,28 @@ def test_enrich_requires_endpoints(gpu_device):
             g.enrich_device(cols, 64, z, z)
     finally:
         g.close()
+
+
+def test_submit_enrich_host_fed(gpu_device):
+    """gpuagg_submit_enrich: the host-fed batch is aggregated (series equal the oracle's)
+    and its endpoints come back equal to the device-side emission."""
+    import torch
+    from .helpers import oracle_series
+    pods = W.make_pods(800, seed=75)
+    recs = W.gen_records(30_001, pods, seed=76, drop_frac=0.1)
+    spec = W.LOCAL_FWD_DROP
+    g = make_engine(pods, spec, False, gpu_device, recs)
+    try:
+        n = len(recs.src_ip)
+        hb = g.alloc_batch(n)
+        for name in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+            getattr(hb, name)[:n] = getattr(recs, name)
+        s_host, d_host = g.submit_enrich(hb, n)
+        g.sync()
+        got = g.snapshot()
+        dev = _run(g, recs, torch.device("cuda", gpu_device))
+    finally:
+        g.close()
+    np.testing.assert_array_equal(s_host, dev[0])
+    np.testing.assert_array_equal(d_host, dev[1])
+    assert got == oracle_series(recs, pods, spec, remote=False)
