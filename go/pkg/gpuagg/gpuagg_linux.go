@@ -36,6 +36,7 @@ import (
 	"time"
 	"unsafe"
 
+	"github.com/cilium/cilium/api/v1/flow"
 	v1 "github.com/cilium/cilium/pkg/hubble/api/v1"
 	api "github.com/microsoft/retina/crd/api/v1alpha1"
 	"github.com/microsoft/retina/crd/api/v1alpha1/validations"
@@ -51,6 +52,7 @@ import (
 	"github.com/microsoft/retina/pkg/utils"
 	"github.com/prometheus/client_golang/prometheus"
 	"go.uber.org/zap"
+	"google.golang.org/protobuf/types/known/wrapperspb"
 )
 
 const (
@@ -114,6 +116,15 @@ type gpuAgg struct {
 	version  uint64
 	stopping bool
 
+	// enriched-flow emission (SetupChannel): the consumer channel, the cache's endpoint
+	// per slot (what getEndpoint copies, enricher.go:142-183), the DNS payload per dns_id
+	// (AddDNSInfo's arguments) and the per-batch endpoint slots from gpuagg_submit_enrich
+	external  chan *v1.Event
+	slotEP    map[int32]*common.RetinaEndpoint
+	dnsByID   map[uint32]dnsPayload
+	enrichSrc []int32
+	enrichDst []int32
+
 	records chan Record
 	raw     chan rawSample
 	done    chan struct{} // closed when Start returns
@@ -125,6 +136,14 @@ type gpuAgg struct {
 	latency    *latencyCollector
 	noResponse *prometheus.CounterVec
 	noRespLast float64
+}
+
+type dnsPayload struct {
+	rcode      uint32
+	qtypes     []string
+	query      string
+	ips        []string
+	numAnswers uint32
 }
 
 // latencyCollector exposes the engine's latency histograms with the reference's names,
@@ -198,10 +217,82 @@ func (g *gpuAgg) Name() string                       { return name }
 func (g *gpuAgg) Generate(ctx context.Context) error { return nil }
 func (g *gpuAgg) Compile(ctx context.Context) error  { return nil }
 
-// SetupChannel: the engine aggregates on the GPU and emits no per-flow Hubble events
-// (the enricher's ExportReader contract, enricher.go:138-140,189-191, is not kept for
-// individual flows; see INTEGRATION.md).
-func (g *gpuAgg) SetupChannel(c chan *v1.Event) error { return nil }
+// SetupChannel registers a consumer of the enriched flows (packetparser's external
+// channel, packetparser_linux.go:335-338,642-651; the enricher's export to ExportReader,
+// enricher.go:137-140,189-191).  From then on every batch is submitted with
+// gpuagg_submit_enrich, whose per-record endpoint slots become flow.Source /
+// flow.Destination; sends never block, a full channel counts a lost event.
+func (g *gpuAgg) SetupChannel(c chan *v1.Event) error {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	g.external = c
+	if c != nil && g.enrichSrc == nil {
+		g.enrichSrc = make([]int32, batchCapacity)
+		g.enrichDst = make([]int32, batchCapacity)
+	}
+	return nil
+}
+
+// endpointLocked is getEndpoint for a slot (-1: the IP is not a pod, the endpoint stays nil).
+func (g *gpuAgg) endpointLocked(slot int32) *flow.Endpoint {
+	ep := g.slotEP[slot]
+	if slot < 0 || ep == nil {
+		return nil
+	}
+	var wl []*flow.Workload
+	if refs := ep.OwnerRefs(); refs != nil {
+		wl = make([]*flow.Workload, 0, len(refs))
+		for _, r := range refs {
+			wl = append(wl, &flow.Workload{Name: r.Name, Kind: r.Kind})
+		}
+	}
+	return &flow.Endpoint{Namespace: ep.Namespace(), PodName: ep.Name(), Labels: ep.FormattedLabels(), Workloads: wl}
+}
+
+// emitLocked rebuilds the producer's flow.Flow of each of the device's n records (the
+// fields packetparser / dropreason / dns / tcpretrans set, packetparser_linux.go:583-628)
+// with the enriched endpoints and sends it to the external channel.
+func (g *gpuAgg) emitLocked(d *device, n int) {
+	for i := 0; i < n; i++ {
+		m := d.cols[3][i]
+		ports := d.cols[4][i]
+		verdict := flow.Verdict((m >> 8) & 0xff)
+		fl := utils.ToFlow(g.l, int64(d.times[i]), utils.Int2ip(d.cols[0][i]).To4(), utils.Int2ip(d.cols[1][i]).To4(),
+			ports&0xffff, ports>>16, uint8(m&0xff), uint8(m>>30), verdict)
+		if fl == nil {
+			continue
+		}
+		fl.IsReply = &wrapperspb.BoolValue{Value: (m>>27)&1 == 1}
+		fl.TrafficDirection = flow.TrafficDirection((m >> 16) & 3)
+		meta := &utils.RetinaMetadata{}
+		utils.AddPacketSize(meta, d.cols[2][i])
+		f := uint16((m >> 21) & 0x3f) // FIN, SYN, RST, PSH, ACK, URG
+		utils.AddTCPFlags(fl, (f>>1)&1, (f>>4)&1, f&1, (f>>2)&1, (f>>3)&1, (f>>5)&1)
+		if verdict == flow.Verdict_DROPPED {
+			utils.AddDropReason(fl, meta, uint16((m>>18)&7))
+		}
+		if id := d.cols[6][i]; id != 0 {
+			utils.AddTCPID(meta, uint64(id))
+		}
+		if t := (m >> 28) & 3; t != 0 {
+			if p, ok := g.dnsByID[d.cols[5][i]]; ok {
+				qr := "Q"
+				if t == 2 {
+					qr = "R"
+				}
+				utils.AddDNSInfo(fl, meta, qr, p.rcode, p.query, p.qtypes, int(p.numAnswers), p.ips)
+			}
+		}
+		utils.AddRetinaMetadata(fl, meta)
+		fl.Source = g.endpointLocked(g.enrichSrc[i])
+		fl.Destination = g.endpointLocked(g.enrichDst[i])
+		select {
+		case g.external <- &v1.Event{Event: fl, Timestamp: fl.GetTime()}:
+		default:
+			metrics.LostEventsCounter.WithLabelValues(utils.ExternalChannel, name).Inc()
+		}
+	}
+}
 
 func lastError(ctx *C.gpuagg_ctx) string { return C.GoString(C.gpuagg_last_error(ctx)) }
 
@@ -454,6 +545,17 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		if err := g.commitLocked(); err != nil {
 			return err
 		}
+		if g.external != nil {
+			// one H2D copy for both: the aggregation and the records' endpoint slots
+			err := check(d.ctx, C.gpuagg_submit_enrich(d.ctx, d.batch, C.size_t(d.n),
+				(*C.int32_t)(unsafe.Pointer(&g.enrichSrc[0])), (*C.int32_t)(unsafe.Pointer(&g.enrichDst[0]))),
+				"gpuagg_submit_enrich")
+			if err == nil {
+				g.emitLocked(d, d.n)
+			}
+			d.n = 0
+			return err
+		}
 		// returns once the H2D copy is done: the batch may be refilled while the GPU
 		// aggregates (double-buffered staging, include/gpuagg.h)
 		err := check(d.ctx, C.gpuagg_submit(d.ctx, d.batch, C.size_t(d.n)), "gpuagg_submit")
@@ -658,6 +760,12 @@ func (g *gpuAgg) InternDNS(rcode uint32, qtypes []string, query string, ips []st
 	err := g.each("gpuagg_dns_intern", func(ctx *C.gpuagg_ctx) C.int {
 		return C.gpuagg_dns_intern(ctx, C.uint32_t(rcode), qt, q, ip, C.uint32_t(numAnswers), &id)
 	})
+	if err == nil {
+		if g.dnsByID == nil {
+			g.dnsByID = make(map[uint32]dnsPayload)
+		}
+		g.dnsByID[uint32(id)] = dnsPayload{rcode, qtypes, query, ips, numAnswers}
+	}
 	return uint32(id), err
 }
 
@@ -733,9 +841,22 @@ func (t *CacheTee) UpdateRetinaEndpoint(ep *common.RetinaEndpoint) error {
 			defer C.free(unsafe.Pointer(kind))
 			defer C.free(unsafe.Pointer(wname))
 		}
-		return g.each("gpuagg_cache_update_endpoint", func(ctx *C.gpuagg_ctx) C.int {
+		if err := g.each("gpuagg_cache_update_endpoint", func(ctx *C.gpuagg_ctx) C.int {
 			return C.gpuagg_cache_update_endpoint(ctx, ns, pod, kind, wname, (*C.uint32_t)(unsafe.Pointer(&v4[0])), C.size_t(len(v4)))
-		})
+		}); err != nil {
+			return err
+		}
+		// the slot the update interned (same identity -> same slot), for emitted flows
+		var slot C.int32_t
+		if err := check(g.devs[0].ctx, C.gpuagg_slot_intern(g.devs[0].ctx, ns, pod, kind, wname, &slot),
+			"gpuagg_slot_intern"); err != nil {
+			return err
+		}
+		if g.slotEP == nil {
+			g.slotEP = make(map[int32]*common.RetinaEndpoint)
+		}
+		g.slotEP[int32(slot)] = ep
+		return nil
 	})
 }
 
