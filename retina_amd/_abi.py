@@ -29,6 +29,7 @@ class Config(C.Structure):
                 ("cms_width_log2", C.c_uint32), ("hll_precision", C.c_uint32),
                 ("flags", C.c_uint32)]
 FLAG_NO_LDS_IP_TABLE = 1
+FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 
 
 class MetricOptions(C.Structure):

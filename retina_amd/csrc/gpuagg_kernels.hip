@@ -86,8 +86,19 @@ struct KArgs {
   unsigned long long *sp_lists;
   uint32_t *sp_counts;
   uint32_t sp_nwin, sp_cap;
+  // deferred folds: the lists already hold earlier launches' entries, so this launch's
+  // LDS fill counters start from spill_count / sp_counts instead of 0
+  uint32_t accum;
   Plan p;
 };
+
+// This workgroup's fill counter of list w at launch start (deferred folds append after
+// the entries earlier launches left).
+__device__ __forceinline__ uint32_t spill_ctr0(const KArgs &a, uint32_t w) {
+  if (!a.accum) return 0u;
+  const uint32_t c = a.spill_count[blockIdx.x * a.nwin + w];
+  return c < a.spill_cap ? c : a.spill_cap;
+}
 
 struct Lk {
   int32_t slot;  // -1: not a pod (flow.Endpoint stays nil)
@@ -578,7 +589,10 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
 
 // LDS setup and the once-per-workgroup flush shared by both aggregation kernels.
 __device__ __forceinline__ DenseSink dense_sink_init(const KArgs &a, unsigned long long *lds) {
-  for (uint32_t i = threadIdx.x; i < a.lds_bins + kLdsExtraWords; i += blockDim.x) lds[i] = 0ULL;
+  for (uint32_t i = threadIdx.x; i < a.lds_bins + 64; i += blockDim.x) lds[i] = 0ULL;
+  unsigned int *ctr = (unsigned int *)&lds[a.lds_bins + 64];
+  for (uint32_t w = threadIdx.x; w < kMaxSpillWindows; w += blockDim.x)
+    ctr[w] = a.spill && w < a.nwin ? spill_ctr0(a, w) : 0u;
   __syncthreads();
   return make_sink(a, lds, a.lds_bins, (unsigned int *)&lds[a.lds_bins + 64]);
 }
@@ -603,7 +617,10 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
   // LDS: dense bins + extras, then the segment-list fill counters
   uint32_t *sctr = (uint32_t *)&lds[a.lds_bins + kLdsExtraWords];
-  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) sctr[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
+    const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
+    sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
+  }
   const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr too)
   DevSparse s = a.s;
   if (a.sp_lists) {
@@ -1011,7 +1028,9 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const uint32_t L4 = a.lds_bins;
   for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
     ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
-  for (uint32_t i = threadIdx.x; i < L4 + 64 + kMaxSpillWindows; i += blockDim.x) bins[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < L4 + 64; i += blockDim.x) bins[i] = 0u;
+  for (uint32_t w = threadIdx.x; w < kMaxSpillWindows; w += blockDim.x)
+    bins[L4 + 64 + w] = a.spill && w < a.nwin ? spill_ctr0(a, w) : 0u;
   __syncthreads();
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const L4Ctx l4{bins, L4 + lane, a.d};
@@ -2107,6 +2126,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.sp_counts = a.sp_counts;
   k.sp_nwin = a.sp_lists ? a.sp_nwin : 0u;
   k.sp_cap = a.sp_cap;
+  k.accum = a.accum ? 1u : 0u;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
@@ -2169,6 +2189,19 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   }
   if (e != hipSuccess) return e;
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
+  if (a.defer_folds) {  // lists folded later (launch_folds); the tier-1 copies now
+    LaunchArgs r = a;
+    r.spill = nullptr;
+    r.stage_b = nullptr;
+    r.sp_lists = nullptr;
+    return launch_folds(r, st);
+  }
+  return launch_folds(a, st);
+}
+
+hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
+  hipError_t e;
+  const DevDense dd{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
   // the tier-1 copies are summed by stage_reduce_kernel after the fold (one launch for
   // both reductions); without a fold they get it alone
   const uint32_t ra_x = (a.lds_bins + 255) / 256, ra_y = 8;
@@ -2179,7 +2212,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     if (na + nb == 0) return hipSuccess;
     hipLaunchKernelGGL(stage_reduce_kernel, dim3(na + nb), dim3(256), 0, st, a.stage_a, a.blocks, a.stage_a_stride,
                        a.lds_bins, ra_x, ra_y, a.plan, (const unsigned long long *)a.stage_b, a.nwin,
-                       with_b ? a.win_blocks / a.nwin : 0u, W, a.spill_lo, a.dense_len, k.d);
+                       with_b ? a.win_blocks / a.nwin : 0u, W, a.spill_lo, a.dense_len, dd);
     return hipGetLastError();
   };
   if (a.sp_lists) {
@@ -2187,7 +2220,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     if ((e = hipFuncSetAttribute((const void *)sparse_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)seg_lds)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(sparse_fold_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, k.s,
+    hipLaunchKernelGGL(sparse_fold_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, dev_sparse(a.sparse),
                        (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
@@ -2197,7 +2230,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
                      (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.spill_lo, a.dense_len, W, a.nwin, k.d, (unsigned long long *)a.stage_b);
+                     a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return reduce(a.stage_b != nullptr);
 }

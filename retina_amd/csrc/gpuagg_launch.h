@@ -63,7 +63,15 @@ struct LaunchArgs {
   uint64_t *sp_lists;       // [blocks][sp_nwin][sp_cap] keys
   uint32_t *sp_counts;      // [blocks][sp_nwin]
   uint32_t sp_nwin, sp_cap;
+  // deferred folds (gpuagg_runtime.cpp: Pending): accum = the lists hold earlier
+  // launches' entries; defer_folds = launch_aggregate leaves the list folds to
+  // launch_folds (the tier-1 copies are still summed per launch)
+  bool accum;
+  bool defer_folds;
 };
+// The list folds of (possibly several deferred) launches with geometry a: the compact
+// segment fold, the spill-window fold and its partial reduction.
+hipError_t launch_folds(const LaunchArgs &a, hipStream_t st);
 
 // Raw perf-record decode (gpuagg_decode.hip); kinds match GPUAGG_RAW_* of gpuagg.h.
 enum RawKind : int { kRawPacket = 1, kRawDrop = 2 };

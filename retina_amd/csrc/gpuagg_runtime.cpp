@@ -268,6 +268,17 @@ struct gpuagg_ctx {
   // staged flushes: per-workgroup LDS bins (tier-1) and per-partition fold windows
   uint32_t *d_stage_a = nullptr;
   size_t stage_a_alloc = 0;
+  // Deferred list folds: the spill / segment lists of consecutive launches with one
+  // geometry accumulate and are folded once (fold_pending) -- per scrape epoch rather
+  // than per batch, so C5's fixed 128 MiB table pass is paid once per sync.
+  struct Pending {
+    bool active = false;
+    LaunchArgs a{};         // geometry and lists of the launches waiting for their fold
+    uint64_t budget = 0;    // records per workgroup the lists were sized for
+    uint64_t rpb = 0;       // records per workgroup appended so far
+  } pend;
+  bool defer_folds = true;
+  std::vector<std::array<hipEvent_t, 2>> pending_fold;  // deferred fold start, end
   int32_t *d_enrich = nullptr;  // gpuagg_submit_enrich: [2][cap] endpoint slots
   size_t enrich_alloc = 0;
   hipEvent_t enrich_done = nullptr;
@@ -453,7 +464,39 @@ int run_staged(gpuagg_ctx *c, gpuagg_ctx::Staging &s, F &&launch_fn) {
   return rc;
 }
 
+// Timing-only events: recording one with the default system-scope fence writes back and
+// invalidates the caches between kernels (measured ~5.5 us of idle GPU per event at C2,
+// profiles/round2/r4a_*); results are published by gpuagg_sync's stream sync, not by
+// these events.
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+
+// Folds the lists of the deferred launches (no-op when none are waiting).  Every reader
+// of the counters or the group-by table calls it first: gpuagg_sync (and through it the
+// snapshot), state export, merge, slot retirement and dense re-layout.
+int fold_pending(gpuagg_ctx *c) {
+  if (!c->pend.active) return GPUAGG_OK;
+  c->pend.active = false;
+  LaunchArgs f = c->pend.a;
+  f.stage_a = nullptr;  // summed per launch
+  f.defer_folds = false;
+  std::array<hipEvent_t, 2> ev{};
+  if (c->timing) {
+    for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+  }
+  HIPCHK(c, launch_folds(f, c->stream));
+  if (c->timing) {
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->pending_fold.push_back(ev);
+  }
+  return GPUAGG_OK;
+}
+
+// The state is being cleared: the waiting lists are discarded with it.
+void drop_pending(gpuagg_ctx *c) { c->pend.active = false; }
+
 int reset_state(gpuagg_ctx *c) {
+  drop_pending(c);
   if (c->dense_len) {
     HIPCHK(c, hipMemsetAsync(c->d_dense_cnt, 0, c->dense_len * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_dense_byt, 0, c->dense_len * 8, c->stream));
@@ -502,6 +545,11 @@ uint32_t key_cap_for(const gpuagg_ctx *c, size_t n) {
 // -- a group's bins are key-major, so its old bins are the prefix of its new ones -- else
 // the new state is zero.
 int layout_dense(gpuagg_ctx *c, uint32_t key_cap, bool keep) {
+  if (keep) {  // the waiting spill lists address the current dense arrays
+    if (int rc = fold_pending(c)) return rc;
+  } else {
+    drop_pending(c);
+  }
   uint64_t total = 0;
   std::vector<uint64_t> base(c->groups.size(), 0), old_base(c->groups.size(), 0), old_nbins(c->groups.size(), 0);
   for (size_t g = 0; g < c->groups.size(); ++g) {
@@ -565,12 +613,6 @@ int layout_dense(gpuagg_ctx *c, uint32_t key_cap, bool keep) {
   return GPUAGG_OK;
 }
 
-// Timing-only events: recording one with the default system-scope fence writes back and
-// invalidates the caches between kernels (measured ~5.5 us of idle GPU per event at C2,
-// profiles/round2/r4a_*); results are published by gpuagg_sync's stream sync, not by
-// these events.
-constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
-
 void drain_timing(gpuagg_ctx *c) {
   for (auto &ev : c->pending_events) {
     float ms = 0.f, fold = 0.f;
@@ -601,6 +643,13 @@ void drain_timing(gpuagg_ctx *c) {
     for (hipEvent_t e : ev) hipEventDestroy(e);
   }
   c->pending_sketch.clear();
+  for (auto &ev : c->pending_fold) {
+    float ms = 0.f;
+    if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess)
+      c->stats.fold_ms += ms;
+    for (hipEvent_t e : ev) hipEventDestroy(e);
+  }
+  c->pending_fold.clear();
 }
 
 // Count-min windows: 2^15 columns (128 KiB of LDS in the fold); at most 4096 windows
@@ -815,6 +864,9 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   return GPUAGG_OK;
 }
 
+// Launches whose list folds may wait for one fold_pending (see Pending).
+constexpr uint64_t kDeferLaunches = 8;
+
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
   if (n == 0) return GPUAGG_OK;
@@ -927,45 +979,100 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         return rc;
       a.stage_a = c->d_stage_a;
     }
-    if (c->dense_len > a.lds_bins) {
-      // bins past the LDS window: per-workgroup spill lists bucketed by fold window
-      const uint64_t rem = c->dense_len - a.lds_bins;
-      const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
-      // overflow falls back to global atomics; a multiple of 4 keeps lists 16-byte aligned
-      const uint64_t cap = ((2 * a.chunk / nwin + 4096) + 3) & ~3ULL;
-      if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
-        a.spill_cap = (uint32_t)cap;
-        const size_t need = (size_t)a.blocks * nwin * a.spill_cap;
-        if ((rc = ensure_buf(c, &c->d_spill, &c->spill_alloc, need))) return rc;
-        if ((rc = ensure_buf(c, &c->d_spill_count, &c->spill_count_alloc, (size_t)a.blocks * nwin)))
-          return rc;
-        a.spill = c->d_spill;
-        a.spill_count = c->d_spill_count;
-        a.nwin = nwin;
-        a.spill_lo = a.lds_bins;
-        a.win_shift = kFoldWindowShift;
-        a.win_blocks = nwin * std::max<uint32_t>(1u, 2u * c->n_cu / nwin);  // one wave of 2 per CU
-        // fold partials are stored (not atomically added) and summed by a reduce pass
-        const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
-        if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
-        a.stage_b = c->d_stage_b;
+    // List geometry for `budget` records per workgroup: spill lists per fold window for
+    // the bins past the LDS window (overflow falls back to global atomics; a multiple of 4
+    // keeps lists 16-byte aligned), compact-key lists per table segment (at most one
+    // insert per record, hashed evenly: budget / nwin per list + 25 % + 64; a full list
+    // inserts in place, exact).
+    struct Geom {
+      uint32_t nwin = 0, spill_cap = 0, win_blocks = 0, sp_nwin = 0, sp_cap = 0;
+      bool operator==(const Geom &o) const {
+        return nwin == o.nwin && spill_cap == o.spill_cap && win_blocks == o.win_blocks && sp_nwin == o.sp_nwin &&
+               sp_cap == o.sp_cap;
       }
+    };
+    auto geom = [&](uint64_t budget) {
+      Geom g;
+      if (c->dense_len > a.lds_bins) {
+        const uint64_t rem = c->dense_len - a.lds_bins;
+        const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
+        const uint64_t cap = ((2 * budget / nwin + 4096) + 3) & ~3ULL;
+        if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
+          g.nwin = nwin;
+          g.spill_cap = (uint32_t)cap;
+          g.win_blocks = nwin * std::max<uint32_t>(1u, 2u * c->n_cu / nwin);  // one wave of 2 per CU
+        }
+      }
+      if (sp_lists) {
+        const uint64_t mean = budget / sp_nwin;
+        g.sp_nwin = (uint32_t)sp_nwin;
+        g.sp_cap = (uint32_t)((mean + mean / 4 + 64 + 1) & ~1ULL);  // even: 16-byte key pairs
+      }
+      return g;
+    };
+    auto geom_of = [](const LaunchArgs &x) {
+      Geom g;
+      if (x.spill) {
+        g.nwin = x.nwin;
+        g.spill_cap = x.spill_cap;
+        g.win_blocks = x.win_blocks;
+      }
+      if (x.sp_lists) {
+        g.sp_nwin = x.sp_nwin;
+        g.sp_cap = x.sp_cap;
+      }
+      return g;
+    };
+    // Deferred folds: while the geometry holds, launches keep appending to the same lists
+    // (their counters start from the stored fill) for up to kDeferLaunches launches' worth
+    // of records per workgroup, and fold_pending folds them once.
+    const bool lists = c->dense_len > a.lds_bins || sp_lists;
+    const bool defer = c->defer_folds && lists;
+    uint64_t budget = defer ? std::max<uint64_t>(a.chunk, std::min<uint64_t>(kMaxRecordsPerBlock,
+                                                                             kDeferLaunches * a.chunk))
+                            : a.chunk;
+    bool accum = false;
+    if (c->pend.active) {
+      const LaunchArgs &q = c->pend.a;
+      const Geom pg = geom(c->pend.budget);
+      accum = defer && c->pend.rpb + a.chunk <= c->pend.budget && pg == geom_of(q) && q.blocks == a.blocks &&
+              q.lds_bins == a.lds_bins && q.dense_len == c->dense_len && q.dense_cnt == c->d_dense_cnt &&
+              q.dense_byt == c->d_dense_byt && q.sparse.k0 == c->sv.k0;
+      if (accum) budget = c->pend.budget;
+      else if ((rc = fold_pending(c))) return rc;
+    }
+    const Geom g = geom(budget);
+    if (g.nwin) {
+      if ((rc = ensure_buf(c, &c->d_spill, &c->spill_alloc, (size_t)a.blocks * g.nwin * g.spill_cap))) return rc;
+      if ((rc = ensure_buf(c, &c->d_spill_count, &c->spill_count_alloc, (size_t)a.blocks * g.nwin))) return rc;
+      a.spill_cap = g.spill_cap;
+      a.spill = c->d_spill;
+      a.spill_count = c->d_spill_count;
+      a.nwin = g.nwin;
+      a.spill_lo = a.lds_bins;
+      a.win_shift = kFoldWindowShift;
+      a.win_blocks = g.win_blocks;
+      // fold partials are stored (not atomically added) and summed by a reduce pass
+      const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
+      if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
+      a.stage_b = c->d_stage_b;
     }
     a.sp_lists = nullptr;
     a.sp_counts = nullptr;
     a.sp_nwin = 0;
-    if (sp_lists) {
-      // at most one compact (DNS) insert per record; hashed keys spread evenly over the
-      // segments: chunk / nwin per list + 25 % + 64 (a full list inserts in place, exact)
-      const uint64_t mean = a.chunk / sp_nwin;
-      const uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
-      if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc, (size_t)a.blocks * sp_nwin * cap))) return rc;
-      if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * sp_nwin))) return rc;
+    if (g.sp_nwin) {
+      if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc, (size_t)a.blocks * g.sp_nwin * g.sp_cap)))
+        return rc;
+      if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * g.sp_nwin))) return rc;
       a.sp_lists = c->d_sp_lists;
       a.sp_counts = c->d_sp_counts;
-      a.sp_nwin = (uint32_t)sp_nwin;
-      a.sp_cap = (uint32_t)cap;
+      a.sp_nwin = g.sp_nwin;
+      a.sp_cap = g.sp_cap;
     }
+    a.accum = accum;
+    a.defer_folds = defer && (a.spill || a.sp_lists);
+    a.dense_cnt = c->d_dense_cnt;
+    a.dense_byt = c->d_dense_byt;
     std::array<hipEvent_t, 3> ev{};
     if (c->timing) {
       for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
@@ -974,6 +1081,12 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     const char *kname = nullptr;
     HIPCHK(c, launch_aggregate(a, c->stream, c->timing ? ev[1] : nullptr, &kname));
     if (kname) c->kernel_name = kname;
+    if (a.defer_folds) {
+      c->pend.rpb = (accum ? c->pend.rpb : 0) + a.chunk;
+      c->pend.budget = budget;
+      c->pend.a = a;
+      c->pend.active = true;
+    }
     if (c->timing) {
       HIPCHK(c, hipEventRecord(ev[2], c->stream));
       c->pending_events.push_back(ev);
@@ -1065,6 +1178,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
     return GPUAGG_EDEVICE;
   }
   c->n_cu = (uint32_t)prop.multiProcessorCount;
+  c->defer_folds = !(cfg->flags & GPUAGG_FLAG_FOLD_PER_BATCH);
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
     if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) {
@@ -1714,6 +1828,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
   if (n_retired) *n_retired = 0;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   std::vector<char> live(c->slots.size(), 0);
   for (const auto &e : c->installed) live[e.second] = 1;
@@ -1927,6 +2042,7 @@ int gpuagg_sync(gpuagg_ctx *c) {
   if (!c) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   drain_timing(c);
   if (c->d_decode_oor)
@@ -2355,6 +2471,11 @@ int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
 // ---- multi-GPU merge hooks -----------------------------------------------------------
 int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   if (!c || !o) return GPUAGG_EINVAL;
+  if (c->pend.active) {  // the arrays below are read by the caller: fold what is waiting
+    int rc = bind(c);
+    if (rc || (rc = fold_pending(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   o->dense_count = c->d_dense_cnt;
   o->dense_bytes = c->d_dense_byt;
   o->dense_len = c->dense_len;
@@ -2373,6 +2494,7 @@ int gpuagg_sparse_export(gpuagg_ctx *c, uint64_t *dev_out, size_t cap, size_t *n
   if (!c->sparse_slots) return GPUAGG_OK;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 8, c->stream));
   HIPCHK(c, launch_sparse_export(c->sv, c->sparse_slots, dev_out, cap, c->d_counter, c->stream));
   uint64_t n = 0;
@@ -2438,6 +2560,7 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
   for (size_t i = 0; i < n; ++i) {
     gpuagg_ctx *ci = ctxs[i];
     if ((rc = bind(ci))) return rc;
+    if ((rc = fold_pending(ci))) return rc;
     if (ci->key_cap < cap && (rc = layout_dense(ci, (uint32_t)cap, true))) return rc;
     HIPCHK(ci, hipStreamSynchronize(ci->stream));
     HIPCHK(ci, hipStreamSynchronize(ci->copy_stream));

@@ -107,3 +107,54 @@ def test_packed_field_overflow_exact(gpu_device, flags):
     g.close()
     del cols
     assert got == want, diff_series(got, want)
+
+
+DEFER = [
+    ("c2", W.LOCAL_FWD_DROP, 10_000, {}),
+    ("c5", W.C5_SPEC, 100_000, {"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
+]
+
+
+@pytest.mark.parametrize("cid,sp,npods,gen", DEFER, ids=[d[0] for d in DEFER])
+def test_deferred_folds_exact(gpu_device, cid, sp, npods, gen):
+    """Spill / segment lists of consecutive launches are folded once (gpuagg_sync or any
+    state read).  20 batches of unequal sizes: growing chunks change the list geometry,
+    more than kDeferLaunches equal ones exhaust the budget, and a snapshot in the middle
+    folds early -- every case equals the C port and the engine folding after each batch."""
+    from retina_amd import GpuAgg, _abi
+    from .helpers import to_device
+    pods = W.make_pods(npods, seed=8)
+    recs = W.gen_records(2_000_000, pods, seed=81, **gen)
+    sizes = [30_000, 30_000, 250_000, 20_000] + [60_000] * 12 + [400_000, 10_007, 333_333]
+    bounds = np.concatenate([[0], np.cumsum(sizes)])
+    assert bounds[-1] <= len(recs)
+    n_mid, n = int(bounds[10]), int(bounds[-1])
+
+    def run(flags):
+        g = make_engine(pods, sp, False, gpu_device, recs, sparse_capacity_log2=23, flags=flags)
+        try:
+            ts = to_device(recs, gpu_device)
+            mid = None
+            for k, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+                g.submit_device(GpuAgg.device_columns(*[x[int(a):] for x in ts]), int(b - a))
+                if k == 9:
+                    mid = g.snapshot()
+            return mid, g.snapshot()
+        finally:
+            g.close()
+
+    def port(m):
+        part = W.Records(recs.src_ip[:m], recs.dst_ip[:m], recs.bytes[:m], recs.meta[:m], recs.ports[:m],
+                         recs.dns_id[:m])
+        r = RefCPU(sp, pods.endpoints, False, recs.dns)
+        r.process(part)
+        s = r.series()
+        r.close()
+        return s
+
+    mid, end = run(0)
+    mid1, end1 = run(_abi.FLAG_FOLD_PER_BATCH)
+    assert mid == mid1 and end == end1
+    want_mid, want = port(n_mid), port(n)
+    assert values_only(mid) == want_mid, diff_series(values_only(mid), want_mid)
+    assert values_only(end) == want, diff_series(values_only(end), want)
