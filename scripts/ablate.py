@@ -41,7 +41,8 @@ def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, api_ips=None,
     if ONLY and name not in ONLY:
         return
     g = GpuAgg(device=0, remote_context=remote, max_slots=len(pods.endpoints) + 16,
-               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24, flags=flags, **kw)
+               max_ips=2 * len(pods.endpoints) + 16, sparse_capacity_log2=24,
+               flags=flags | int(os.environ.get("ABLATE_FLAGS", "0")), **kw)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     if api_ips:
@@ -61,6 +62,7 @@ def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, api_ips=None,
     fold = st["fold_ms"] / max(1, st["kernel_launches"])
     sk = st["sketch_ms"] / max(1, st["sketch_launches"])
     print(json.dumps({"lib": os.path.basename(os.environ.get("GPUAGG_LIB", "")), "variant": name, "records": n,
+                      "flags": flags | int(os.environ.get("ABLATE_FLAGS", "0")),
                       "launch_ms": ms, "fold_ms": fold, "sketch_ms": sk, "wall_ms": wall * 1e3,
                       "grec_s": n / max(ms, 1e-9) / 1e6, "hbm_frac_16B": 16 * n / (max(ms, 1e-9) * 1e-3) / 8e12}),
           flush=True)
