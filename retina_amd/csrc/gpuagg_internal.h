@@ -205,6 +205,9 @@ constexpr uint32_t sig_group(uint32_t fam, bool inl) { return (fam + 1) | (inl ?
 constexpr uint32_t kSigFwdLds = sig_group(0, true);                                  // FAM_FWD
 constexpr uint32_t kSigFwdLdsDropLds = kSigFwdLds | sig_group(1, true) << 4;         // + FAM_DROP
 constexpr uint32_t kSigFwdLdsDropSpill = kSigFwdLds | sig_group(1, false) << 4;
+// C5: tcpflags + retransmissions spilled, DNS request / response compact (dense_local_kernel)
+constexpr uint32_t kSigC5 = sig_group(2, false) | sig_group(3, false) << 4 | sig_group(4, false) << 8 |
+                            sig_group(5, false) << 12;
 constexpr uint32_t kL4CountShift = 20;
 constexpr uint32_t kL4BytesMask = (1u << kL4CountShift) - 1;
 constexpr uint32_t kL4ByteLimit = 1u << kL4CountShift;

@@ -163,6 +163,36 @@ __device__ __forceinline__ void sparse_add_compact(const DevSparse &s, uint64_t 
   atomicAdd(s.dropped, 1ULL);
 }
 
+// The compact plan's aggregation side: a key goes to its table segment's list (LDS fill
+// counter, one 8-byte store); a full list adds in place.  Only the fields this needs, so
+// kernels that use it keep few scalar registers live.
+struct CompactLists {
+  unsigned long long *lists;  // this workgroup's [nseg][lcap] keys
+  uint32_t *lctr;             // LDS fill counters
+  uint32_t lcap;
+  unsigned long long *k0, *dropped;
+  uint32_t mask, seg_log2;
+  __device__ __forceinline__ void insert(uint64_t key) const {
+    const uint32_t h = (uint32_t)fmix64(key ^ 0x243F6A8885A308D3ULL) & mask;  // compact_home
+    const uint32_t w = h >> seg_log2;
+    const uint32_t pos = atomicAdd(&lctr[w], 1u);
+    if (pos < lcap) {
+      lists[(size_t)w * lcap + pos] = key;
+      return;
+    }
+    const uint32_t smask = (1u << seg_log2) - 1u, seg = h & ~smask;  // full list: in place (exact)
+    for (uint32_t probe = 0; probe <= smask; ++probe) {
+      unsigned long long *slot = k0 + 2ull * (seg | ((h + probe) & smask));
+      const unsigned long long cur = atomicCAS(&slot[0], 0ULL, (unsigned long long)key);
+      if (cur == 0ULL || cur == key) {
+        atomicAdd(&slot[1], 1ULL);
+        return;
+      }
+    }
+    atomicAdd(dropped, 1ULL);
+  }
+};
+
 // Insert-or-add into the sparse table. No lane ever waits for another: a lane that
 // meets a slot whose key is still being published moves on, so a key may occupy
 // more than one slot; the host sums duplicates when it renders series.
@@ -689,30 +719,50 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
 }
 
 // Dense local-context fast path: every group is endpoint-keyed (forward / drop /
-// tcpflags / tcpretrans with namespace|podname|workload|service options).  The NG
-// group descriptors are compile-time indexed, so they live in SGPRs for the whole
-// kernel; bin arithmetic is 32-bit.
-template <int NG, bool kVec>
+// tcpflags / tcpretrans with namespace|podname|workload|service options) or, with kDns,
+// a DNS group of the compact plan (its key fits 64 bits: group|side|slot|dns id, appended
+// to the table segment's list as the generic kernel does).  The NG group descriptors are
+// compile-time indexed, so they live in SGPRs for the whole kernel; bin arithmetic is
+// 32-bit.  kDns keeps C5 (tcpflags + retransmissions + DNS at 100k pods) off the generic
+// kernel's per-group dispatch.
+template <int NG, bool kVec, bool kDns, uint32_t SIG = 0>
 __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
-  const DenseSink ds = dense_sink_init(a, lds);
+  uint32_t *sctr = (uint32_t *)&lds[a.lds_bins + kLdsExtraWords];
+  CompactLists cl{};
+  if (kDns) {  // segment-list fill counters after the dense bins (aggregate_kernel's layout)
+    for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
+      const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
+      sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
+    }
+    cl = CompactLists{a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap, sctr, a.sp_cap, a.s.k0,
+                      a.s.dropped, a.s.mask, a.s.seg_log2};
+  }
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr too)
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t dummy = a.lds_bins + lane;  // absorbs predicated-off updates, never flushed
   const int ng = a.p.ngroups;
-  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG];
+  uint32_t fam[NG], base[NG], nsub[NG], keyed[NG], sopts[NG];
   bool inl[NG];
   bool any_flags = false;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    fam[g] = g < ng ? a.p.g[g].family : (uint32_t)FAM_COUNT;
+    if (SIG) {  // family and LDS residency fixed at compile time (see tier1_signature)
+      const uint32_t code = (SIG >> (4 * g)) & 7u;
+      fam[g] = code ? code - 1 : (uint32_t)FAM_COUNT;
+      inl[g] = (SIG >> (4 * g + 3)) & 1u;
+    } else {
+      fam[g] = g < ng ? a.p.g[g].family : (uint32_t)FAM_COUNT;
+      inl[g] = a.p.g[g].dense_base + a.p.g[g].nbins <= a.lds_bins;  // whole group in the LDS window
+    }
     base[g] = (uint32_t)a.p.g[g].dense_base;
     nsub[g] = a.p.g[g].nsub;
     keyed[g] = a.p.g[g].key_mode;
-    inl[g] = base[g] + a.p.g[g].nbins <= a.lds_bins;  // whole group in the LDS window
+    sopts[g] = a.p.g[g].src_opts;
     any_flags |= fam[g] == FAM_TCPFLAGS;
   }
-  for_each_record<kVec>(a, false, false,
-                        [&](uint32_t, uint32_t, uint32_t nb, uint32_t meta, uint32_t, uint32_t,
+  for_each_record<kVec>(a, false, kDns,
+                        [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t, uint32_t dns,
                             const Lk &ls, const Lk &ld, bool) {
     const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
     const bool s_ok = ls.slot >= 0 && !ls.api;  // getLocalCtxValues (types.go:379-416)
@@ -724,6 +774,16 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
     for (int g = 0; g < NG; ++g) {
       const uint32_t f = fam[g];
       if (f == FAM_COUNT) continue;
+      if (kDns && (f == FAM_DNS_REQ || f == FAM_DNS_RESP)) {
+        // dns.go:506-540: exactly one update; both sides -> pick by TrafficDirection.
+        // Compact plan: no ip / port option, so the side tuple is the endpoint only.
+        if (sopts[g] == 0) continue;
+        const bool hit = verdict == kVerdictDns && meta_dnstype(meta) == (f == FAM_DNS_REQ ? kDnsQuery : kDnsResponse);
+        const uint32_t side = (s_ok && d_ok) ? (meta_tdir(meta) == 1 ? 0u : 1u) : (d_ok ? 0u : 1u);
+        const SideKey k = side == 0 ? side_key(sopts[g], dip, ld, 0u, proto) : side_key(sopts[g], sip, ls, 0u, proto);
+        if (hit && (s_ok || d_ok)) cl.insert(key0((uint32_t)g, side, k.slot1, k.ip) | (uint64_t)dns);
+        continue;
+      }
       const uint32_t kd = keyed[g] ? (uint32_t)ld.slot : 0u, ks = keyed[g] ? (uint32_t)ls.slot : 0u;
       // slots < 2^16, nsub <= 64: 24-bit multiplies (full rate)
       const uint32_t row_d = base[g] + mul_u24(kd * 2u, nsub[g]);        // side 0: ingress (dst)
@@ -767,7 +827,10 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
       }
     }
   });
-  dense_flush(a, ds);
+  dense_flush(a, ds);  // (starts with a barrier)
+  if (kDns)
+    for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
+      a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
 }
 
 // ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
@@ -2133,7 +2196,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
                              : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4;
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
-  int variant = a.tier1 ? 100 + (int)a.dense_ng : (int)a.dense_ng;
+  int variant = a.tier1 ? 100 + (int)a.dense_ng : (a.dns_compact && a.dense_ng ? 300 : 0) + (int)a.dense_ng;
+  if (variant == 304 && a.sig == kSigC5) variant = 305;
   if (a.tier1) {
     if (a.sig == kSigFwdLdsDropSpill) variant = 200;
     else if (a.sig == kSigFwdLdsDropLds) variant = 201;
@@ -2150,7 +2214,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
       snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu>", variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng,
                a.vec ? "true" : "false", variant >= 200 ? a.sig : 0u);
     else if (a.dense_ng)
-      snprintf(name, sizeof name, "dense_local_kernel<%u, %s>", a.dense_ng, a.vec ? "true" : "false");
+      snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu>", a.dense_ng, a.vec ? "true" : "false",
+               a.dns_compact ? "true" : "false", variant == 305 ? a.sig : 0u);
     else
       snprintf(name, sizeof name, "aggregate_kernel<%s, %s>", a.vec ? "true" : "false", sketch ? "true" : "false");
     *kernel = name;
@@ -2171,14 +2236,25 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
                         : launch_k(dense_lds_kernel<2, false, kSigFwdLdsDropLds>, k, B, T, lds, st); break;
     case 202: e = a.vec ? launch_k(dense_lds_kernel<1, true, kSigFwdLds>, k, B, T, lds, st)
                         : launch_k(dense_lds_kernel<1, false, kSigFwdLds>, k, B, T, lds, st); break;
-    case 1: e = a.vec ? launch_k(dense_local_kernel<1, true>, k, B, T, lds, st)
-                      : launch_k(dense_local_kernel<1, false>, k, B, T, lds, st); break;
-    case 2: e = a.vec ? launch_k(dense_local_kernel<2, true>, k, B, T, lds, st)
-                      : launch_k(dense_local_kernel<2, false>, k, B, T, lds, st); break;
-    case 4: e = a.vec ? launch_k(dense_local_kernel<4, true>, k, B, T, lds, st)
-                      : launch_k(dense_local_kernel<4, false>, k, B, T, lds, st); break;
-    case 8: e = a.vec ? launch_k(dense_local_kernel<8, true>, k, B, T, lds, st)
-                      : launch_k(dense_local_kernel<8, false>, k, B, T, lds, st); break;
+    case 1: e = a.vec ? launch_k(dense_local_kernel<1, true, false>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<1, false, false>, k, B, T, lds, st); break;
+    case 2: e = a.vec ? launch_k(dense_local_kernel<2, true, false>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<2, false, false>, k, B, T, lds, st); break;
+    case 4: e = a.vec ? launch_k(dense_local_kernel<4, true, false>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<4, false, false>, k, B, T, lds, st); break;
+    case 8: e = a.vec ? launch_k(dense_local_kernel<8, true, false>, k, B, T, lds, st)
+                      : launch_k(dense_local_kernel<8, false, false>, k, B, T, lds, st); break;
+    // with the compact plan's DNS groups (segment lists)
+    case 301: e = a.vec ? launch_k(dense_local_kernel<1, true, true>, k, B, T, lds, st)
+                        : launch_k(dense_local_kernel<1, false, true>, k, B, T, lds, st); break;
+    case 302: e = a.vec ? launch_k(dense_local_kernel<2, true, true>, k, B, T, lds, st)
+                        : launch_k(dense_local_kernel<2, false, true>, k, B, T, lds, st); break;
+    case 304: e = a.vec ? launch_k(dense_local_kernel<4, true, true>, k, B, T, lds, st)
+                        : launch_k(dense_local_kernel<4, false, true>, k, B, T, lds, st); break;
+    case 305: e = a.vec ? launch_k(dense_local_kernel<4, true, true, kSigC5>, k, B, T, lds, st)
+                        : launch_k(dense_local_kernel<4, false, true, kSigC5>, k, B, T, lds, st); break;
+    case 308: e = a.vec ? launch_k(dense_local_kernel<8, true, true>, k, B, T, lds, st)
+                        : launch_k(dense_local_kernel<8, false, true>, k, B, T, lds, st); break;
     default:
       if (a.vec)
         e = sketch ? launch_k(aggregate_kernel<true, true>, k, B, T, lds, st)

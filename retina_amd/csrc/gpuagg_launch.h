@@ -51,6 +51,7 @@ struct LaunchArgs {
   uint32_t win_shift, nwin, win_blocks;  // fold windows of 2^win_shift bins
   uint32_t spill_lo;    // first spilled dense bin (fold windows start here)
   uint32_t dense_ng;    // 0: generic kernel; 1/2/4/8: dense local-context kernel
+  bool dns_compact;     // dense kernel also inserts the compact plan's DNS keys (segment lists)
   bool tier1;           // dense kernel with the IP table and u32 bins in LDS
   uint32_t sig;         // tier-1 group signature (kSig*), 0 when the plan has none
   const uint8_t *ipl;

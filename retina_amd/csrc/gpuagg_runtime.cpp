@@ -896,9 +896,20 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.hll_p = 0;
   // dense local-context fast path: every group dense, no sketches
   a.dense_ng = 0;
+  a.dns_compact = false;
   if (c->plan.local && c->plan.ngroups > 0 && !a.cms_depth && !a.hll_p) {
+    // every group dense, or -- compact plan -- dense and DNS (keys of 64 bits, inserted
+    // through the segment lists by the dense kernel)
     bool all_dense = true;
-    for (int g = 0; g < c->plan.ngroups; ++g) all_dense &= !c->plan.g[g].sparse;
+    for (int g = 0; g < c->plan.ngroups; ++g) {
+      const bool dns = c->plan.g[g].family == FAM_DNS_REQ || c->plan.g[g].family == FAM_DNS_RESP;
+      if (c->plan.g[g].sparse && c->sv.compact && dns && c->sparse_slots &&
+          (c->sparse_slots >> c->sv.seg_log2) <= kSparseMaxSegLists && !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH))
+        a.dns_compact = true;
+      else
+        all_dense &= !c->plan.g[g].sparse;
+    }
+    if (!all_dense) a.dns_compact = false;
     if (all_dense)
       for (uint32_t ng : {1u, 2u, 4u, 8u})
         if ((uint32_t)c->plan.ngroups <= ng) {
@@ -922,7 +933,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   };
   // compact group-by keys (generic kernel) go through per-segment lists whose fill
   // counters take LDS words from the dense window
-  const bool generic = !a.dense_ng;
+  const bool generic = !a.dense_ng || a.dns_compact;  // kernels that take compact-key lists
   const uint64_t sp_nwin = c->sparse_slots ? c->sparse_slots >> c->sv.seg_log2 : 0;
   const bool sp_lists = generic && c->sv.compact && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
                         !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH);
@@ -930,7 +941,15 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
   a.sig = 0;
-  if (a.dense_ng && c->ipl_bytes && !spans.empty() &&
+  if (a.dense_ng && a.dns_compact && c->plan.ngroups <= 8) {  // dense_local_kernel's signature
+    uint32_t sig = 0;
+    for (int g = 0; g < c->plan.ngroups; ++g)
+      sig |= sig_group(c->plan.g[g].family, !c->plan.g[g].sparse &&
+                                                c->plan.g[g].dense_base + c->plan.g[g].nbins <= a.lds_bins)
+             << (4 * g);
+    a.sig = sig;
+  }
+  if (a.dense_ng && !a.dns_compact && c->ipl_bytes && !spans.empty() &&
       c->ipl_bytes + kL4ExtraBytes < kLdsBytes) {
     // (with no group in LDS every update spills, but the IP probes still stay on-chip)
     const uint32_t L4 = prefix((kLdsBytes - c->ipl_bytes - kL4ExtraBytes) / 4);
