@@ -547,8 +547,15 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
 // wave-uniform -- lanes past the end read the last element and pass an inactive record
 // (no endpoint, an unmatched verdict) -- so f may use cross-lane operations.
 constexpr uint32_t kInactiveMeta = kVerdictUnencodable << 8;
-template <bool kVec, class F>
-__device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f) {
+struct NoRounds {
+  __device__ __forceinline__ void operator()() const {}
+};
+// kRounds: the vector loop is block-uniform (waves past the end process inactive lanes)
+// and calls round_end() after every step, so the caller can flush LDS staging between
+// barriers.
+template <bool kVec, bool kRounds = false, class F, class RE = NoRounds>
+__device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f,
+                                                RE &&round_end = RE{}) {
   const bool need_bytes = a.p.need_bytes;  // no forward / drop group: the column is not read
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -560,7 +567,8 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
     const uint4 *s4 = (const uint4 *)a.c.src, *d4 = (const uint4 *)a.c.dst;
     const uint4 *b4 = (const uint4 *)a.c.bytes, *m4 = (const uint4 *)a.c.meta;
     const uint4 *p4 = (const uint4 *)a.c.ports, *q4 = (const uint4 *)a.c.dns;
-    for (uint64_t vw = v0 + wave0; vw < vend; vw += blockDim.x) {
+    for (uint64_t vblk = v0; kRounds ? vblk < vend : vblk + wave0 < vend; vblk += blockDim.x) {
+      const uint64_t vw = vblk + wave0;
       const bool act = vw + lane < vend;
       const uint64_t v = act ? vw + lane : vlast;
       const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
@@ -605,6 +613,7 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
         p0 = p1; p1 = p2; p2 = p3; q0 = q1; q1 = q2; q2 = q3;
         ls0 = ls1; ls1 = ls2; ls2 = ls3; ld0 = ld1; ld1 = ld2; ld2 = ld3;
       }
+      if (kRounds) round_end();
     }
     tail = start + ((end - start) & ~3ULL);
   }
@@ -725,7 +734,7 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
 // compile-time indexed, so they live in SGPRs for the whole kernel; bin arithmetic is
 // 32-bit.  kDns keeps C5 (tcpflags + retransmissions + DNS at 100k pods) off the generic
 // kernel's per-group dispatch.
-template <int NG, bool kVec, bool kDns, uint32_t SIG = 0>
+template <int NG, bool kVec, bool kDns, uint32_t SIG = 0, bool kStage = false>
 __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
   uint32_t *sctr = (uint32_t *)&lds[a.lds_bins + kLdsExtraWords];
@@ -738,9 +747,50 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
     cl = CompactLists{a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap, sctr, a.sp_cap, a.s.k0,
                       a.s.dropped, a.s.mask, a.s.seg_log2};
   }
-  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr too)
+  // kStage: spill appends are staged in per-window LDS rings (after the segment
+  // counters: [nwin] flushed positions, then [nwin][kSpillRing] entries) and written out
+  // once per step as contiguous runs -- C5's ~1.4 appends per record to 220 windows were
+  // scattered 4-byte stores (PMC: 3.2x the list bytes written).
+  uint32_t *sfl = sctr + (kDns ? a.sp_nwin : 0u);
+  uint32_t *ring = sfl + a.nwin;
+  if (kStage)
+    for (uint32_t w = threadIdx.x; w < a.nwin; w += blockDim.x) sfl[w] = spill_ctr0(a, w);
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and sfl too)
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t dummy = a.lds_bins + lane;  // absorbs predicated-off updates, never flushed
+  auto spill = [&](uint32_t bin, uint32_t nbytes) {
+    if (!kStage) {
+      ds.spill_add(bin, nbytes);
+      return;
+    }
+    const uint32_t w = ds.window(bin);
+    const uint32_t pos = atomicAdd(&ds.ctr[w], 1u);
+    if (pos < ds.spill_cap) {
+      const uint32_t e = ds.entry(bin, nbytes);
+      if (pos - sfl[w] < kSpillRing) ring[w * kSpillRing + (pos & (kSpillRing - 1u))] = e;
+      else ds.spill[mul_u24(w, ds.spill_cap) + pos] = e;  // ring full: direct
+      return;
+    }
+    atomicAdd(&a.d.cnt[bin], 1ULL);  // list full (exact fallback)
+    if (nbytes) atomicAdd(&a.d.byt[bin], (unsigned long long)nbytes);
+  };
+  // write each window's staged run [flushed, min(filled, flushed + ring)) (all threads,
+  // between barriers; positions past the ring were stored directly)
+  auto flush = [&]() {
+    const uint32_t wv = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    for (uint32_t w = wv; w < a.nwin; w += nwaves) {
+      const uint32_t f = sfl[w], c = min(ds.ctr[w], ds.spill_cap), e = min(c, f + kSpillRing);
+      uint32_t *dst = ds.spill + mul_u24(w, ds.spill_cap);
+      for (uint32_t p = f + lane; p < e; p += 64) dst[p] = ring[w * kSpillRing + (p & (kSpillRing - 1u))];
+      if (lane == 0) sfl[w] = c;
+    }
+  };
+  auto round_end = [&]() {
+    __syncthreads();
+    flush();
+    __syncthreads();
+  };
+
   const int ng = a.p.ngroups;
   uint32_t fam[NG], base[NG], nsub[NG], keyed[NG], sopts[NG];
   bool inl[NG];
@@ -761,7 +811,7 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
     sopts[g] = a.p.g[g].src_opts;
     any_flags |= fam[g] == FAM_TCPFLAGS;
   }
-  for_each_record<kVec>(a, false, kDns,
+  for_each_record<kVec, kStage>(a, false, kDns,
                         [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t, uint32_t dns,
                             const Lk &ls, const Lk &ld, bool) {
     const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta), reason = meta_reason(meta);
@@ -801,8 +851,8 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
         } else {
           for (; m; m &= m - 1) {
             const uint32_t bit = (uint32_t)__builtin_ctz(m);
-            if (d_ok) ds.spill_add(row_d + bit, 0);
-            if (s_ok) ds.spill_add(row_s + bit, 0);
+            if (d_ok) spill(row_d + bit, 0);
+            if (s_ok) spill(row_s + bit, 0);
           }
         }
         continue;
@@ -822,11 +872,15 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
           if (s_ok) atomicAdd(&a.d.byt[row_s + sub], (unsigned long long)add_b);
         }
       } else if (hit) {
-        if (d_ok) ds.spill_add(row_d + sub, add_b);
-        if (s_ok) ds.spill_add(row_s + sub, add_b);
+        if (d_ok) spill(row_d + sub, add_b);
+        if (s_ok) spill(row_s + sub, add_b);
       }
     }
-  });
+  }, round_end);
+  if (kStage) {  // the tail records' staged entries
+    __syncthreads();
+    flush();
+  }
   dense_flush(a, ds);  // (starts with a barrier)
   if (kDns)
     for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
@@ -2198,6 +2252,11 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (a.dns_compact && a.dense_ng ? 300 : 0) + (int)a.dense_ng;
   if (variant == 304 && a.sig == kSigC5) variant = 305;
+  size_t lds_used = lds;
+  if (variant == 305 && a.spill && lds + (size_t)a.nwin * (1 + kSpillRing) * 4 <= kLdsBytes) {
+    variant = 306;  // spill appends staged in LDS rings
+    lds_used = lds + (size_t)a.nwin * (1 + kSpillRing) * 4;
+  }
   if (a.tier1) {
     if (a.sig == kSigFwdLdsDropSpill) variant = 200;
     else if (a.sig == kSigFwdLdsDropLds) variant = 201;
@@ -2214,8 +2273,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
       snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu>", variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng,
                a.vec ? "true" : "false", variant >= 200 ? a.sig : 0u);
     else if (a.dense_ng)
-      snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu>", a.dense_ng, a.vec ? "true" : "false",
-               a.dns_compact ? "true" : "false", variant == 305 ? a.sig : 0u);
+      snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu%s>", a.dense_ng, a.vec ? "true" : "false",
+               a.dns_compact ? "true" : "false", variant >= 305 ? a.sig : 0u, variant == 306 ? ", true" : "");
     else
       snprintf(name, sizeof name, "aggregate_kernel<%s, %s>", a.vec ? "true" : "false", sketch ? "true" : "false");
     *kernel = name;
@@ -2253,6 +2312,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
                         : launch_k(dense_local_kernel<4, false, true>, k, B, T, lds, st); break;
     case 305: e = a.vec ? launch_k(dense_local_kernel<4, true, true, kSigC5>, k, B, T, lds, st)
                         : launch_k(dense_local_kernel<4, false, true, kSigC5>, k, B, T, lds, st); break;
+    case 306: e = a.vec ? launch_k(dense_local_kernel<4, true, true, kSigC5, true>, k, B, T, lds_used, st)
+                        : launch_k(dense_local_kernel<4, false, true, kSigC5, true>, k, B, T, lds_used, st); break;
     case 308: e = a.vec ? launch_k(dense_local_kernel<8, true, true>, k, B, T, lds, st)
                         : launch_k(dense_local_kernel<8, false, true>, k, B, T, lds, st); break;
     default:
