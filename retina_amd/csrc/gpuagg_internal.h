@@ -112,6 +112,7 @@ constexpr uint32_t kSlotBits = 21;
 // of 64k u32 entries indexed by the last two octets; entry = slot | apiserver << 31, or
 // kRadixEmpty.  Two loads per IP, the first to a table of a few hot lines.
 constexpr uint32_t kRadixEmpty = 0xFFFFFFFFu, kRadixNoBlock = 0xFFFFu, kRadixMaxBlocks = 64;
+constexpr uint32_t kRadixSmall = 8;  // prefixes resolved by compares (DevIpTable::rp)
 constexpr uint32_t kMaxSlot = (1u << kSlotBits) - 2;  // slot ids 0..kMaxSlot
 GA_HD uint32_t ip_hash(uint32_t ip) {  // murmur3 fmix32: 2 mul + 3 xorshift
   ip ^= ip >> 16;

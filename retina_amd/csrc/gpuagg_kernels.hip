@@ -33,7 +33,24 @@ struct DevIpTable {
   uint32_t seed;
   const uint16_t *pre;    // radix table (kRadix*), or null
   const uint32_t *blk;
+  // radix table with at most kRadixSmall /16 prefixes (the usual pod CIDRs): the
+  // prefixes themselves, block j's in 16 bits of rp[j / 2]; the block of an address is
+  // found by compares instead of a load from `pre` (one dependent gather per lookup
+  // instead of two).  rpn = 0: use `pre`.
+  uint32_t rpn;
+  uint32_t rp[kRadixSmall / 2];
 };
+
+// Radix block of ip: compares against the few prefixes, else the `pre` table.
+__device__ __forceinline__ uint32_t radix_block(const DevIpTable &t, uint32_t ip) {
+  if (!t.rpn) return t.pre[ip & 0xFFFFu];
+  const uint32_t lo = ip & 0xFFFFu;
+  uint32_t b = kRadixNoBlock;
+#pragma unroll
+  for (uint32_t j = 0; j < kRadixSmall; ++j)
+    b = (j < t.rpn && lo == ((t.rp[j >> 1] >> ((j & 1u) * 16u)) & 0xFFFFu)) ? j : b;
+  return b;
+}
 struct DevDense {
   unsigned long long *cnt;
   unsigned long long *byt;
@@ -134,7 +151,7 @@ __device__ __forceinline__ uint32_t radix_entry(const DevIpTable &t, uint32_t ip
 }
 
 __device__ __forceinline__ Lk ip_lookup(const DevIpTable &t, uint32_t ip) {
-  if (t.pre) return radix_pick(radix_entry(t, ip, t.pre[ip & 0xFFFFu]));
+  if (t.pre) return radix_pick(radix_entry(t, ip, radix_block(t, ip)));
   const ulonglong2 e1 = ip_bucket(t, ip_h1(ip, t.seed) & t.mask);
   const ulonglong2 e2 = ip_need2(ip, e1) ? ip_bucket(t, ip_h2(ip, t.seed) & t.mask)
                                          : make_ulonglong2(kIpEmpty, kIpEmpty);
@@ -580,7 +597,7 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       if (a.t.pre) {  // radix table: 8 prefix loads, then 8 entry loads
         uint32_t bi[8], e[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) bi[k] = a.t.pre[ip[k] & 0xFFFFu];
+        for (int k = 0; k < 8; ++k) bi[k] = radix_block(a.t, ip[k]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) e[k] = radix_entry(a.t, ip[k], bi[k]);
 #pragma unroll
@@ -1765,7 +1782,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   k.meta = a.cols.meta;
   k.n = a.n;
   k.chunk = a.chunk;
-  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk};
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk, 0u, {}};
   k.cms = a.cms;
   k.depth = a.cms_depth;
   k.wlog2 = a.cms_wlog2;
@@ -2222,7 +2239,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.c = DevCols{a.cols.src_ip, a.cols.dst_ip, a.cols.bytes, a.cols.meta, a.cols.ports, a.cols.dns_id};
   k.n = a.n;
   k.chunk = a.chunk;
-  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk};
+  k.t = DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk, a.ip_rpn, {}};
+  for (uint32_t j = 0; j < kRadixSmall / 2; ++j) k.t.rp[j] = a.ip_rp[j];
   k.d = DevDense{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
   k.s = dev_sparse(a.sparse);
   k.sk = DevSketch{a.cms, a.cms_depth, a.cms_wlog2, (uint32_t *)a.hll, a.hll_p};
@@ -2403,7 +2421,7 @@ hipError_t launch_enrich(const EnrichArgs &a, uint32_t n_cu, hipStream_t st) {
   const uint64_t need = (lanes + 255) / 256;
   const uint32_t blocks = (uint32_t)(need < (uint64_t)n_cu * 8 ? need : (uint64_t)n_cu * 8);
   hipLaunchKernelGGL(enrich_kernel, dim3(blocks), dim3(256), 0, st,
-                     DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk}, a.src, a.dst,
+                     DevIpTable{a.ip_slots, a.ip_mask, a.ip_seed, a.ip_pre, a.ip_blk, 0u, {}}, a.src, a.dst,
                      (uint64_t)a.n, a.o_src, a.o_dst, vec);
   return hipGetLastError();
 }

@@ -32,6 +32,8 @@ struct LaunchArgs {
   uint32_t ip_seed;
   const uint16_t *ip_pre;  // radix IP table (null: the bucket table above)
   const uint32_t *ip_blk;
+  uint32_t ip_rpn;                       // radix prefixes resolved by compares (0: use ip_pre)
+  uint32_t ip_rp[kRadixSmall / 2];
   Plan plan;
   uint64_t *dense_cnt, *dense_byt;
   SparseView sparse;

@@ -181,6 +181,8 @@ struct gpuagg_ctx {
   uint32_t *d_rblk = nullptr;
   size_t rblk_alloc = 0;
   bool radix = false;
+  uint32_t radix_n = 0;                   // prefixes (blocks) of the radix table
+  uint32_t radix_pfx[kRadixSmall / 2] = {};  // their values when radix_n <= kRadixSmall
   size_t ip_cap = 0;  // slots
   uint32_t ip_seed = 0;
   // LDS image of the IP table for the tier-1 dense kernel (empty: not available)
@@ -865,7 +867,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 }
 
 // Launches whose list folds may wait for one fold_pending (see Pending).
-constexpr uint64_t kDeferLaunches = 8;
+constexpr uint64_t kDeferLaunches = 16;
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
@@ -879,6 +881,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.ip_mask = (uint32_t)(c->ip_cap / 2 - 1);  // bucket mask
   a.ip_pre = c->radix ? c->d_rpre : nullptr;
   a.ip_blk = c->radix ? c->d_rblk : nullptr;
+  a.ip_rpn = c->radix && c->radix_n <= kRadixSmall ? c->radix_n : 0u;
+  for (uint32_t j = 0; j < kRadixSmall / 2; ++j) a.ip_rp[j] = c->radix_pfx[j];
   a.ip_seed = c->ip_seed;
   a.plan = c->plan;
   a.dense_cnt = c->d_dense_cnt;
@@ -1043,7 +1047,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       return g;
     };
     // Deferred folds: while the geometry holds, launches keep appending to the same lists
-    // (their counters start from the stored fill) for up to kDeferLaunches launches' worth
+    // (their counters start from the stored fill) for up to kDeferLaunches (16) launches' worth
     // of records per workgroup, and fold_pending folds them once.
     const bool lists = c->dense_len > a.lds_bins || sp_lists;
     const bool defer = c->defer_folds && lists;
@@ -1641,6 +1645,10 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     if (c->radix) {
       uint32_t nb = 0;
       for (auto &kv : blocks) kv.second = nb++;
+      c->radix_n = nb;
+      for (auto &p : c->radix_pfx) p = 0;
+      for (auto &kv : blocks)
+        if (kv.second < kRadixSmall) c->radix_pfx[kv.second / 2] |= kv.first << (16 * (kv.second & 1));
       std::vector<uint16_t> pre(1u << 16, (uint16_t)kRadixNoBlock);
       for (auto &kv : blocks) pre[kv.first] = (uint16_t)kv.second;
       std::vector<uint32_t> blk((size_t)nb << 16, kRadixEmpty);
