@@ -1049,7 +1049,11 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     // Deferred folds: while the geometry holds, launches keep appending to the same lists
     // (their counters start from the stored fill) for up to kDeferLaunches (16) launches' worth
     // of records per workgroup, and fold_pending folds them once.
-    const bool lists = c->dense_len > a.lds_bins || sp_lists;
+    // Only plans with compact-key lists defer: their fold pays a fixed pass over the
+    // group-by table.  Spill-only plans (C2, C4) fold per batch -- their fold is
+    // proportional to the entries, and appending past earlier launches' entries measured
+    // ~2 % slower in the tier-1 kernel (profiles/round2/r4f_*).
+    const bool lists = sp_lists;
     const bool defer = c->defer_folds && lists;
     uint64_t budget = defer ? std::max<uint64_t>(a.chunk, std::min<uint64_t>(kMaxRecordsPerBlock,
                                                                              kDeferLaunches * a.chunk))
