@@ -36,7 +36,8 @@ METRIC = "flow records/sec aggregated (node, 1/2/4/8 GPU); % of HBM peak GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Algorithmic bytes per record: the columns the enabled metrics read.
 # C5's metrics (tcpflags, retransmits, DNS) count records only: src, dst, meta, dns_id.
-BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c4-src": 16, "c5": 16}
+BYTES_PER_RECORD = {"c1": 16, "c2": 16, "c3": 20, "c4": 16, "c4-src": 16, "c4-remote": 16, "c5": 16}
+REMOTE_CONFIGS = {"c4-remote"}  # remote context: source and destination label tuples
 # the sketch pass reads src, dst, ports, meta (proto)
 SKETCH_BYTES_PER_RECORD = 16
 
@@ -52,6 +53,9 @@ def bench_spec(name: str):
             "C3: " + c2txt + " + count-min d=4 w=2^20 over the 5-tuple + HLL p=14 distinct dst per source pod")
     if name == "c4":
         return W.LOCAL_FWD_DROP, {}, "C4: Zipf(1.2) 5-tuple ranks over 10^7 flows, " + c2txt
+    if name == "c4-remote":
+        return W.C1_REMOTE, {}, ("C4 remote context: Zipf(1.2) 5-tuple ranks over 10^7 flows, forward + drop "
+                                 "[ip, namespace, podname, workload] on both sides (sparse group-by keys)")
     if name == "c4-src":
         return W.LOCAL_FWD_DROP, {}, "C4 (round-1 form): Zipf(1.2) source pods, " + c2txt
     if name == "c5":
@@ -98,7 +102,7 @@ def _cpu_info():
 
 
 def cpu_baseline(cfg_name: str, pods, spec, seed: int, gen_kw, go_sample: int, tuned_sample: int,
-                 runs: int = 5):
+                 runs: int = 5, remote: bool = False):
     """The C port of the reference path (oracle/ref_cpu.c) timed on this host, in the two
     modes of SURVEY.md 8d / BASELINE.md, 1 warm-up + `runs` timed runs each, median:
       go-shaped: dotted-string IPs, string-keyed cache and label maps, enrich + every
@@ -116,7 +120,7 @@ def cpu_baseline(cfg_name: str, pods, spec, seed: int, gen_kw, go_sample: int, t
     def timed(fn, n):
         rates = []
         for i in range(runs + 1):
-            r = RefCPU(spec, pods.endpoints, False, recs.dns)
+            r = RefCPU(spec, pods.endpoints, remote, recs.dns)
             dt = fn(r)
             r.close()
             if i:  # run 0 is the warm-up
@@ -221,9 +225,10 @@ def main():
     log("rank %d: %d records resident in HBM (%.1f s)" % (rank, n, time.time() - t0))
 
     # C5's DNS series are sparse keys (one per query payload and side): a 2^24-slot table
-    g = GpuAgg(device=local_rank, remote_context=False, max_slots=cfg["pods"] + 16,
-               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2={"c1": 21, "c5": 23}.get(args.config, 16),
-               **sketch)
+    remote = args.config in REMOTE_CONFIGS
+    g = GpuAgg(device=local_rank, remote_context=remote, max_slots=cfg["pods"] + 16,
+               max_ips=2 * cfg["pods"] + 16,
+               sparse_capacity_log2={"c1": 21, "c5": 23, "c4-remote": 25}.get(args.config, 16), **sketch)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     for p in last.dns:
@@ -313,7 +318,8 @@ def main():
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         go_s, tu_s = (400_000, 4_000_000) if args.config == "c5" else (args.cpu_sample // 8, args.cpu_sample)
-        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s)
+        result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s,
+                                              remote=remote)
         if sketch:
             result["cpu_baseline"]["sample"] += " (metrics only: the sketches have no reference CPU path)"
     g.close()

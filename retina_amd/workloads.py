@@ -359,6 +359,11 @@ CONFIGS = {
     # pods are Zipf-skewed too: the hottest flow carries ~18 % of the records)
     "c4": dict(records=100_000_000, pods=10_000, seed=4,
                gen={"flows": 10_000_000, "flow_zipf": 1.2, "n_dst": 1_000_000}),
+    # C4 through the remote context (C1_REMOTE: ip/namespace/podname/workload on both
+    # sides): every update is a sparse group-by key, hot keys repeat within a wave, so this
+    # is the contention case of the wave key de-duplication before the table's atomics
+    "c4-remote": dict(records=100_000_000, pods=10_000, seed=4,
+                      gen={"flows": 10_000_000, "flow_zipf": 1.2, "n_dst": 1_000_000}),
     # round-1 C4: Zipf(1.2) source pods only, independent destinations
     "c4-src": dict(records=100_000_000, pods=10_000, seed=4, gen={"zipf": 1.2}),
     "c5": dict(records=10_000_000, pods=100_000, seed=5,
