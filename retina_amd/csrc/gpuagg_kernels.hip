@@ -1668,11 +1668,18 @@ __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_l
       for (uint32_t j = (n4 << 2) + threadIdx.x; j < cnt; j += blockDim.x) put(e[j]);
       continue;
     }
-    // rounds of 4 entries per thread (one 16-byte load), staged and flushed
+    // rounds of 4 entries per thread (one 16-byte load), staged and flushed; the next
+    // round's load is issued before this round's appends and flush, so the list reads
+    // stay in flight across the barriers
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (4 * threadIdx.x + 4 <= cnt) nxt = *(const uint4 *)(e + 4 * threadIdx.x);
     for (uint32_t r0 = 0; r0 < cnt; r0 += 4 * blockDim.x) {
       const uint32_t j = r0 + 4 * threadIdx.x;
+      const uint4 cur = nxt;
+      const uint32_t jn = j + 4 * blockDim.x;
+      if (jn + 4 <= cnt) nxt = *(const uint4 *)(e + jn);
       if (j + 4 <= cnt) {
-        const uint4 v = *(const uint4 *)(e + j);
+        const uint4 v = cur;
         put(v.x);
         put(v.y);
         put(v.z);
