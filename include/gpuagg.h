@@ -68,6 +68,7 @@ typedef struct gpuagg_config {
 #define GPUAGG_FLAG_NO_LDS_IP_TABLE 1u /* keep the IP table in HBM/L2 only (diagnostics) */
 #define GPUAGG_FLAG_DIRECT_SKETCH 2u   /* sketch updates as global atomics, no window lists (diagnostics) */
 #define GPUAGG_FLAG_NO_RADIX_IP_TABLE 4u /* HBM lookups through the bucket hash table only (diagnostics) */
+#define GPUAGG_FLAG_NO_HOT_KEYS 16u    /* no LDS hot-key cache in front of the group-by table (diagnostics) */
 #define GPUAGG_FLAG_FOLD_PER_BATCH 8u  /* fold the spill / segment lists after every batch instead of
                                           once per gpuagg_sync or state read (diagnostics) */
 

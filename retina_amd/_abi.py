@@ -30,6 +30,7 @@ class Config(C.Structure):
                 ("flags", C.c_uint32)]
 FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
+FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table
 
 
 class MetricOptions(C.Structure):

@@ -146,7 +146,9 @@ constexpr uint32_t kLdsBytes = 160 * 1024;
 // 256 windows x 2^13 bins: dense spaces up to ~2M bins beyond the LDS prefix (C5's
 // 100k-pod tcpflags + retransmit groups) still fold in LDS instead of global atomics
 constexpr uint32_t kMaxSpillWindows = 256;
-constexpr uint32_t kSpillRing = 128;  // staged spill appends per window (dense_local_kernel kStage)
+constexpr uint32_t kSpillRing = 128;
+constexpr uint32_t kHotKeyBytes = 48;    // LDS hot-key cache entry (aggregate_kernel)
+constexpr uint32_t kHotKeys = 2048;      // entries when the plan has HBM-table keys  // staged spill appends per window (dense_local_kernel kStage)
 constexpr uint32_t kLdsExtraWords = 64 + kMaxSpillWindows / 2;  // 64 dummies + u32 spill-window counters
 constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
 constexpr uint32_t kLdsCountShift = 44;

@@ -66,7 +66,51 @@ struct DevSparse {
   unsigned long long *lists;
   uint32_t *lctr;
   uint32_t lcap;
+  // per-workgroup LDS cache of hot group-by keys (aggregate_kernel; null: none)
+  struct HotKey *hot;
+  uint32_t hot_n;  // entries, a power of two
 };
+
+// One cached key: tag 0 free, 1 being claimed, 2 published (key words final).
+struct HotKey {
+  unsigned long long tag, k0, k1, k2, cnt, byt;
+};
+static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp");
+
+// Adds (c, b) to key (k0, k1, k2) in this workgroup's LDS hot-key cache if the key is
+// there or a free entry can be claimed (two candidate entries); false: the caller adds
+// to the HBM table.  No lane ever waits: an entry being claimed by another lane is
+// skipped.  Under skew (C4's Zipf flows) the hot keys then cost LDS atomics instead of
+// memory-side atomics serialised on one table slot; the cache is added to the table
+// once per workgroup at the end (hot_flush).
+__device__ __forceinline__ bool hot_add(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
+                                        uint64_t b) {
+  const uint32_t h = (uint32_t)key_hash(k0, k1, k2);
+#pragma unroll
+  for (uint32_t q = 0; q < 2; ++q) {
+    HotKey *e = &s.hot[(h + q * 0x9E37u) & (s.hot_n - 1u)];
+    unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t == 0ULL) {
+      t = atomicCAS(&e->tag, 0ULL, 1ULL);
+      if (t == 0ULL) {  // claimed: write the key and the first update, then publish
+        e->k0 = k0;
+        e->k1 = k1;
+        e->k2 = k2;
+        e->cnt = c;
+        e->byt = b;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&e->tag, 2ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
+    }
+    if (t == 2ULL && e->k0 == k0 && e->k1 == k1 && e->k2 == k2) {
+      atomicAdd(&e->cnt, (unsigned long long)c);
+      if (b) atomicAdd(&e->byt, (unsigned long long)b);
+      return true;
+    }
+  }
+  return false;
+}
 struct DevSketch {
   uint32_t *cms;
   uint32_t depth;
@@ -106,6 +150,7 @@ struct KArgs {
   // deferred folds: the lists already hold earlier launches' entries, so this launch's
   // LDS fill counters start from spill_count / sp_counts instead of 0
   uint32_t accum;
+  uint32_t hot_n;  // LDS hot-key cache entries of aggregate_kernel (0: none)
   Plan p;
 };
 
@@ -436,7 +481,7 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
       }
     }
   }
-  if (keep) sparse_add(s, k0, k1, k2, c, b);
+  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b))) sparse_add(s, k0, k1, k2, c, b);
 }
 
 // One record through every metric group.  Converged: every lane of the wave runs it
@@ -677,12 +722,19 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
     const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
     sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
   }
-  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr too)
+  // hot-key cache after the segment counters (8-byte aligned)
+  HotKey *hot = (HotKey *)&lds[a.lds_bins + kLdsExtraWords + (a.sp_nwin + 1) / 2];
+  for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and the tags too)
   DevSparse s = a.s;
   if (a.sp_lists) {
     s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap;
     s.lctr = sctr;
     s.lcap = a.sp_cap;
+  }
+  if (a.hot_n) {
+    s.hot = hot;
+    s.hot_n = a.hot_n;
   }
   for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
                         [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports,
@@ -693,6 +745,13 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   dense_flush(a, ds);  // (starts with a barrier)
   for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
     a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+  if (a.hot_n) {  // the cached keys, once per workgroup (dense_flush's barrier precedes)
+    DevSparse g = a.s;
+    for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) {
+      const HotKey e = hot[i];
+      if (e.tag == 2ULL) sparse_add(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
+    }
+  }
 }
 
 // Workgroup w folds table segment w: its 2^seg_log2 (key, count) slots are loaded into
@@ -2269,10 +2328,12 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.sp_nwin = a.sp_lists ? a.sp_nwin : 0u;
   k.sp_cap = a.sp_cap;
   k.accum = a.accum ? 1u : 0u;
+  k.hot_n = a.hot_n;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
-                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4;
+                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4 +
+                                   (a.hot_n ? 4 + (size_t)a.hot_n * kHotKeyBytes : 0);
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (a.dns_compact && a.dense_ng ? 300 : 0) + (int)a.dense_ng;

@@ -71,6 +71,7 @@ struct LaunchArgs {
   // launch_folds (the tier-1 copies are still summed per launch)
   bool accum;
   bool defer_folds;
+  uint32_t hot_n;  // aggregate_kernel's LDS hot-key cache entries (0: none)
 };
 // The list folds of (possibly several deferred) launches with geometry a: the compact
 // segment fold, the spill-window fold and its partial reduction.

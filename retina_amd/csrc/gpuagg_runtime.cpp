@@ -941,7 +941,12 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   const uint64_t sp_nwin = c->sparse_slots ? c->sparse_slots >> c->sv.seg_log2 : 0;
   const bool sp_lists = generic && c->sv.compact && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
                         !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH);
-  a.lds_bins = prefix(kLdsMaxBins - (sp_lists ? (uint32_t)(sp_nwin + 1) / 2 : 0u));
+  // plans with HBM-table keys (remote context, ip / port options): an LDS cache of the
+  // hot keys per workgroup in front of the table (hot_add in gpuagg_kernels.hip)
+  const bool hot = generic && c->sparse_slots && !c->sv.compact && !(c->cfg.flags & GPUAGG_FLAG_NO_HOT_KEYS);
+  a.hot_n = hot ? kHotKeys : 0u;
+  a.lds_bins = prefix(kLdsMaxBins - (sp_lists ? (uint32_t)(sp_nwin + 1) / 2 : 0u) -
+                      (hot ? kHotKeys * kHotKeyBytes / 8 + 1 : 0u));
   // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
   a.sig = 0;

@@ -158,3 +158,24 @@ def test_deferred_folds_exact(gpu_device, cid, sp, npods, gen):
     want_mid, want = port(n_mid), port(n)
     assert values_only(mid) == want_mid, diff_series(values_only(mid), want_mid)
     assert values_only(end) == want, diff_series(values_only(end), want)
+
+
+@pytest.mark.parametrize("gen", [dict(W.CONFIGS["c4"]["gen"]), {"flows": 64, "flow_zipf": 1.2, "n_dst": 64}],
+                         ids=["zipf-1e7-flows", "64-flows"])
+def test_hot_key_cache_exact(gpu_device, gen):
+    """The LDS hot-key cache in front of the group-by table (remote context, C4's Zipf
+    flows and a 64-flow extreme where every key is hot in every workgroup) equals the
+    table-only path and the C port."""
+    from retina_amd import _abi
+    pods = W.make_pods(10_000, seed=9)
+    recs = W.gen_records(1_500_000, pods, seed=91, **gen)
+    a = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
+                                  sparse_capacity_log2=23))
+    b = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
+                                  sparse_capacity_log2=23, flags=_abi.FLAG_NO_HOT_KEYS))
+    assert a == b, diff_series(a, b)
+    r = RefCPU(W.C1_REMOTE, pods.endpoints, True, recs.dns)
+    r.process(recs)
+    want = r.series()
+    r.close()
+    assert a == want, diff_series(a, want)
