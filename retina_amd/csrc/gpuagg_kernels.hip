@@ -78,19 +78,24 @@ struct HotKey {
 static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp");
 
 // Adds (c, b) to key (k0, k1, k2) in this workgroup's LDS hot-key cache if the key is
-// there or a free entry can be claimed (two candidate entries); false: the caller adds
+// there or a free entry can be claimed (two candidate entries; only a key seen more
+// than once in the wave claims); false: the caller adds
 // to the HBM table.  No lane ever waits: an entry being claimed by another lane is
 // skipped.  Under skew (C4's Zipf flows) the hot keys then cost LDS atomics instead of
 // memory-side atomics serialised on one table slot; the cache is added to the table
 // once per workgroup at the end (hot_flush).
 __device__ __forceinline__ bool hot_add(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
                                         uint64_t b) {
+  // only keys that occur more than once in the wave (the de-dup count) claim an entry:
+  // under skew those are the hot ones; uniform keys (C1) then cost two tag reads
+  const bool may_claim = c > 1;
   const uint32_t h = (uint32_t)key_hash(k0, k1, k2);
 #pragma unroll
   for (uint32_t q = 0; q < 2; ++q) {
     HotKey *e = &s.hot[(h + q * 0x9E37u) & (s.hot_n - 1u)];
     unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (t == 0ULL) {
+      if (!may_claim) continue;
       t = atomicCAS(&e->tag, 0ULL, 1ULL);
       if (t == 0ULL) {  // claimed: write the key and the first update, then publish
         e->k0 = k0;
