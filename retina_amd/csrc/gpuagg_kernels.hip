@@ -1387,6 +1387,7 @@ struct SketchK {
   // per lane (2 or 4) as contiguous runs
   uint32_t sbc, sbh, round;
   uint32_t sbs;  // hll_split_kernel staging ring per fine window (0: unstaged)
+  uint32_t sbs_every;  // hll_split_kernel: rounds between flushes of the rings
 };
 
 // Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
@@ -1717,6 +1718,7 @@ __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_l
     }
   };
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  uint32_t rounds = 0;  // block-uniform
   auto flush = [&]() {
     for (uint32_t w = wave; w < nfine; w += nwaves) {
       const uint32_t f = ffl[w], c = min(fcnt[w], k.hcap2), e = min(c, f + R);
@@ -1757,12 +1759,18 @@ __global__ __launch_bounds__(1024) void hll_split_kernel(SketchK k, uint32_t n_l
       } else {
         for (uint32_t q = j; q < cnt; ++q) put(e[q]);
       }
-      __syncthreads();
-      flush();
-      __syncthreads();
+      if (++rounds % k.sbs_every == 0) {
+        __syncthreads();
+        flush();
+        __syncthreads();
+      }
     }
   }
   __syncthreads();
+  if (R) {  // what the last rounds staged
+    flush();
+    __syncthreads();
+  }
   for (uint32_t i = threadIdx.x; i < nfine; i += blockDim.x)
     k.hcounts2[base2 + i] = fcnt[i] < k.hcap2 ? fcnt[i] : k.hcap2;
 }
@@ -1952,12 +1960,17 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   }
   if (a.hll_nsup && a.hll_p) {
     names += "+hll_split_kernel+hll_fold_kernel";
-    // staging rings: a round (4096 entries) over nfine windows, x 2 + 64, when they fit
+    // staging rings: a round (4096 entries) over nfine windows, x 2 + 64, when they fit;
+    // larger rings where LDS allows, flushed every few rounds (each flush is a barrier
+    // pair for the workgroup): C3's 128 fine windows take 256-entry rings, every 3 rounds
     const uint32_t nfine = 1u << (a.hll_sshift - a.hll_shift);
+    const uint32_t per_round = 2 * 4096 / nfine;  // twice the mean appends per window
     uint32_t R = 64;
-    while (R < 2 * 4096 / nfine + 64) R <<= 1;
+    while (R < per_round + 64) R <<= 1;
     if ((size_t)(2 + R) * nfine * 4 > kLdsBytes) R = 0;
+    while (R && R < 256 && (size_t)(2 + 2 * R) * nfine * 4 <= kLdsBytes) R <<= 1;
     k.sbs = R;
+    k.sbs_every = R ? std::max<uint32_t>(1u, (R - 64) / std::max<uint32_t>(1u, per_round)) : 1u;
     const size_t split_lds = (size_t)(2 + R) * nfine * 4;
     if ((e = hipFuncSetAttribute((const void *)hll_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)split_lds)) != hipSuccess)
