@@ -614,6 +614,16 @@ __device__ __forceinline__ void sketch_update(const DevSketch &sk, uint32_t sip,
 // wave-uniform -- lanes past the end read the last element and pass an inactive record
 // (no endpoint, an unmatched verdict) -- so f may use cross-lane operations.
 constexpr uint32_t kInactiveMeta = kVerdictUnencodable << 8;
+// Record-stream loads: every column element is read once per launch, so they are
+// non-temporal -- the stream does not evict the spill lists, IP tables and staged copies
+// that the folds read back from L2 (C2 fold 0.043 -> 0.035 ms, C5 kernel 0.208 ->
+// 0.200 ms, profiles/round2/r6c*_*).
+__device__ __forceinline__ uint4 rec_ld(const uint4 *p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load((const v4u *)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 struct NoRounds {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -638,10 +648,10 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       const uint64_t vw = vblk + wave0;
       const bool act = vw + lane < vend;
       const uint64_t v = act ? vw + lane : vlast;
-      const uint4 vs = s4[v], vd = d4[v], vm = m4[v];
+      const uint4 vs = rec_ld(&s4[v]), vd = rec_ld(&d4[v]), vm = rec_ld(&m4[v]);
       const uint4 vb = need_bytes ? b4[v] : make_uint4(0, 0, 0, 0);
       const uint4 vp = need_ports ? p4[v] : make_uint4(0, 0, 0, 0);
-      const uint4 vq = need_dns ? q4[v] : make_uint4(0, 0, 0, 0);
+      const uint4 vq = need_dns ? rec_ld(&q4[v]) : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       Lk lk[8];
       if (a.t.pre) {  // radix table: 8 prefix loads, then 8 entry loads
@@ -1264,15 +1274,15 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t vwave = v0 + (threadIdx.x & ~63u);
     const uint64_t vlast = vend - 1;  // vn >= 1
     uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
-    uint4 ns = s4[vl], nd = d4[vl], nbv = b4[vl], nm = m4[vl];
+    uint4 ns = rec_ld(&s4[vl]), nd = rec_ld(&d4[vl]), nbv = rec_ld(&b4[vl]), nm = rec_ld(&m4[vl]);
     for (uint64_t vw = vwave; vw < vend; vw += blockDim.x) {
       const bool act = vw + lane < vend;
       const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
       vl = vw + blockDim.x + lane < vend ? vw + blockDim.x + lane : vlast;  // clamped: no branch
-      ns = s4[vl];
-      nd = d4[vl];
-      nbv = b4[vl];
-      nm = m4[vl];
+      ns = rec_ld(&s4[vl]);
+      nd = rec_ld(&d4[vl]);
+      nbv = rec_ld(&b4[vl]);
+      nm = rec_ld(&m4[vl]);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t j[8];
 #pragma unroll
