@@ -1642,10 +1642,10 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
     uint4 ns = z4, nd = z4, nm = z4, np = z4;
     if (v0 + threadIdx.x < vend) {
       const uint64_t v = v0 + threadIdx.x;
-      ns = s4[v];
-      nd = d4[v];
-      nm = m4[v];
-      np = need_ports ? p4[v] : z4;
+      ns = rec_ld(&s4[v]);
+      nd = rec_ld(&d4[v]);
+      nm = rec_ld(&m4[v]);
+      np = need_ports ? rec_ld(&p4[v]) : z4;
     }
     // block-uniform trip count: every thread reaches the flush barriers
     for (uint64_t vb = v0; vb < vend; vb += blockDim.x) {
@@ -1654,10 +1654,10 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
       const uint4 vs = ns, vd = nd, vm = nm, vp = np;
       const uint64_t vn = v + blockDim.x;
       if (vn < vend) {
-        ns = s4[vn];
-        nd = d4[vn];
-        nm = m4[vn];
-        np = need_ports ? p4[vn] : z4;
+        ns = rec_ld(&s4[vn]);
+        nd = rec_ld(&d4[vn]);
+        nm = rec_ld(&m4[vn]);
+        np = need_ports ? rec_ld(&p4[vn]) : z4;
       }
       if (act) {
         const Lk l0 = lookup(vs.x), l1 = lookup(vs.y);
