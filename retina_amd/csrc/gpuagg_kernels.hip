@@ -876,10 +876,10 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
       if (lane == 0) sfl[w] = c;
     }
   };
-  // flush every kStageSteps steps: ~75 appends per window on average into the 128-entry
-  // rings (the excess of a busy window is stored directly); every step / 2 / 3 steps
-  // measured 0.231 / 0.207 / 0.201 ms at C5 (profiles/round2/r5f_*)
-  constexpr uint32_t kStageSteps = 3;
+  // flush every kStageSteps steps: ~100 appends per window on average into the 128-entry
+  // rings (the excess of a busy window is stored directly); every 1 / 2 / 3 / 4 / 6 steps
+  // measured 0.231 / 0.207 / 0.201 / 0.196 / 0.199 ms at C5 (profiles/round2/r5f_*, r6f_*)
+  constexpr uint32_t kStageSteps = 4;
   uint32_t steps = 0;  // block-uniform
   auto round_end = [&]() {
     if (++steps % kStageSteps) return;
