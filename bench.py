@@ -141,9 +141,11 @@ def cpu_baseline(cfg_name: str, pods, spec, seed: int, gen_kw, go_sample: int, t
                                     "runs": go_all}}}
 
 
-def pmc_traffic(cfg_name: str, kernel: str):
+def pmc_traffic(cfg_name: str, kernel: str, build_id: str):
     """HBM bytes per launch from profiles/pmc_<config>.json, only if that file profiles
-    the kernel that ran (its `kernel` list holds rocprofv3 names containing `kernel`)."""
+    the kernel that ran (its `kernel` list holds rocprofv3 names containing `kernel`) AND
+    was collected from the same library build (its `build_id` equals gpuagg_build_id(),
+    a hash of retina_amd/csrc/*): counters of older code are never reported."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg_name)
     if not os.path.exists(path):
         return None, "no %s" % os.path.relpath(path, ROOT)
@@ -156,6 +158,9 @@ def pmc_traffic(cfg_name: str, kernel: str):
     parts = [p for p in (kernel or "").split("+") if p]
     if not parts or not all(any(p in k for k in names) for p in parts):
         return None, "%s profiles %s, not %s: refused" % (os.path.relpath(path, ROOT), names, kernel)
+    if pmc.get("build_id") != build_id:
+        return None, "%s is from build %s, this library is %s: refused" % (
+            os.path.relpath(path, ROOT), pmc.get("build_id"), build_id)
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 
 
@@ -277,7 +282,8 @@ def main():
         dom, dom_ms, dom_bpr = kernel, agg_ms, bpr
         other_ms = fold_ms + sk_ms
     achieved = dom_bpr * n / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.config, dom)
+    build_id = g.lib.gpuagg_build_id().decode()
+    traffic, traffic_src = pmc_traffic(args.config, dom, build_id)
 
     result = {
         "metric": METRIC,
@@ -313,6 +319,7 @@ def main():
             "bytes_per_record": dom_bpr,
             "step_bytes_per_record": bpr,
         },
+        "build_id": build_id,
     }
     if rank == 0 and world == 1 and not args.no_host_fed:
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)

@@ -447,6 +447,9 @@ const char *gpuagg_kernel_name(const gpuagg_ctx *ctx);
 /* The same for the last sketch pass: its kernels joined by "+", e.g.
  * "sketch_stage_kernel<true>+cms_fold_kernel+hll_split_kernel+hll_fold_kernel". */
 const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *ctx);
+/* Hash of the sources this library was built from (retina_amd/build.py): profiles under
+ * profiles/ carry it, and bench.py uses a profile's counters only for the same build. */
+const char *gpuagg_build_id(void);
 
 #ifdef __cplusplus
 }

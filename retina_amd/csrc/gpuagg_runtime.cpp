@@ -28,6 +28,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "gpuagg_build_id.h"
 #include "gpuagg_internal.h"
 #include "ipl_build.h"
 #include "gpuagg_launch.h"
@@ -1685,21 +1686,6 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
-  dev_free(c->d_ipl_all);
-  dev_free(c->d_ipc);
-  dev_free(c->d_api);
-  dev_free(c->d_lat);
-  dev_free(c->d_lat_blk_cnt);
-  dev_free(c->d_lat_blk_max);
-  dev_free(c->d_lat_blk_clk);
-  dev_free(c->d_lat_blk_base);
-  dev_free(c->d_lat_ev);
-  dev_free(c->d_lat_hash);
-  dev_free(c->d_lat_idx);
-  dev_free(c->d_lat_carry[0]);
-  dev_free(c->d_lat_carry[1]);
-  if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
-  if (c->h_lat_n) hipHostFree(c->h_lat_n);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
@@ -1721,20 +1707,6 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_all_alloc) {
         dev_free(c->d_ipl_all);
-  dev_free(c->d_ipc);
-  dev_free(c->d_api);
-  dev_free(c->d_lat);
-  dev_free(c->d_lat_blk_cnt);
-  dev_free(c->d_lat_blk_max);
-  dev_free(c->d_lat_blk_clk);
-  dev_free(c->d_lat_blk_base);
-  dev_free(c->d_lat_ev);
-  dev_free(c->d_lat_hash);
-  dev_free(c->d_lat_idx);
-  dev_free(c->d_lat_carry[0]);
-  dev_free(c->d_lat_carry[1]);
-  if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
-  if (c->h_lat_n) hipHostFree(c->h_lat_n);
         c->ipl_all_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
         c->ipl_all_alloc = bytes;
@@ -2814,6 +2786,7 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
 
 void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+const char *gpuagg_build_id(void) { return GPUAGG_BUILD_ID; }
 const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }
 const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *c) { return c ? c->sketch_kernel_name.c_str() : ""; }
 

@@ -57,7 +57,8 @@ for s in $STEPS; do
         [ $rc -ne 0 ] && exit $rc
       done
       python scripts/pmc_summary.py "$OUT/${TAG}_pmc_${cfg}.json" "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" roofline.kernel)" \
-        "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" config.records_per_gpu)" "$OUT"/${TAG}_pmc_${cfg}_[0-9]* > /dev/null 2>> "$OUT/${TAG}_pmc_${cfg}_1.log" ;;
+        "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" config.records_per_gpu)" \
+        "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" build_id)" "$OUT"/${TAG}_pmc_${cfg}_[0-9]* > /dev/null 2>> "$OUT/${TAG}_pmc_${cfg}_1.log" ;;
     ablate)
       ABLATE_ONLY="$arg" timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
       rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;

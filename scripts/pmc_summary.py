@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc passes into per-launch HBM traffic for one kernel (or pass).
 
-    python scripts/pmc_summary.py OUT.json KERNEL RECORDS PASS_DIR...
+    python scripts/pmc_summary.py OUT.json KERNEL RECORDS BUILD_ID PASS_DIR...
 
 KERNEL is the signature bench.py reports in roofline.kernel (e.g.
 "dense_lds_kernel<2, true, 41u>"); a pass of several kernels is written "a+b" and its
@@ -19,7 +19,7 @@ from collections import defaultdict
 
 
 def main():
-    out, kernel, records, dirs = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4:]
+    out, kernel, records, build_id, dirs = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5:]
     parts = [p for p in kernel.split("+") if p]
     vals = {p: defaultdict(list) for p in parts}
     names = set()
@@ -37,6 +37,7 @@ def main():
             avg[k] += sum(v) / len(v)
             disp["%s:%s" % (p, k)] = len(v)
     res = {"kernel": sorted(names), "kernel_signature": kernel, "records_per_launch": records,
+           "build_id": build_id,
            "counters_avg_per_dispatch": dict(avg), "dispatches": disp}
     if "FETCH_SIZE" in avg:
         rd = 2.0 * avg["FETCH_SIZE"] * 1024

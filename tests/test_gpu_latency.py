@@ -144,3 +144,41 @@ def test_sharded_contexts_merge(gpu_device):
         assert got[k] == want[k], k
     assert got["no_response"] + got["pending"] + rest["pending"] == want["no_response"] + want["pending"]
     assert rest["latency_count"] == 0 and rest["no_response"] == 0  # reset after the merge
+
+
+def test_apiserver_and_ipcache_before_endpoints(gpu_device):
+    """The Go agent's order: the apiserver IPs and the Hubble ipcache are set before the
+    IP cache commits its first endpoints, and the endpoint set then grows (the LDS IP
+    images are rebuilt larger).  Latency batches and a Hubble decode after the growth
+    must still use live buffers and match the oracle."""
+    import torch
+    from retina_amd import GpuAgg
+    small = W.make_pods(50, seed=71)
+    big = W.make_pods(3000, seed=71)
+    recs = W.gen_latency_records(300, big, API, seed=72, background=2000)
+    want = as_state(oracle_latency(recs, API))
+    g = GpuAgg(device=gpu_device, max_slots=len(big.endpoints) + 64, max_ips=len(big.ips) + 64,
+               sparse_capacity_log2=20, cms_depth=2, cms_width_log2=12, hll_precision=10)
+    try:
+        g.reconcile(SPEC)
+        g.set_apiserver_ips(API)
+        ips = big.ips.tolist()
+        g.ipcache_set(ips, [1000 + i for i in range(len(ips))], list(range(len(ips))))
+        g.load_endpoints(small.endpoints, version=1)  # first commit: the images are built
+        g.load_endpoints(big.endpoints, version=2)    # growth: the images are reallocated
+        ts = _dev(recs, gpu_device)
+        n = len(recs.src_ip)
+        half = n // 2
+        g.submit_device(GpuAgg.device_columns(*ts), half)
+        g.submit_device(GpuAgg.device_columns(*[x[half:] for x in ts]), n - half)
+        got = _state(g)
+        out = [torch.empty(n, dtype=torch.int32, device=ts[0].device) for _ in range(6)]
+        g.hubble_decode_device(GpuAgg.device_columns(*ts), n, out)
+        g.sync()
+        sid = out[0].cpu().numpy().view(np.uint32)
+    finally:
+        g.close()
+    assert got == want
+    pos = {ip: i for i, ip in enumerate(ips)}
+    exp = np.array([1000 + pos[int(s)] if int(s) in pos else 2 for s in recs.src_ip], np.uint32)
+    assert np.array_equal(sid, exp)
