@@ -233,7 +233,7 @@ def main():
     remote = args.config in REMOTE_CONFIGS
     g = GpuAgg(device=local_rank, remote_context=remote, max_slots=cfg["pods"] + 16,
                max_ips=2 * cfg["pods"] + 16,
-               sparse_capacity_log2={"c1": 21, "c5": 23, "c4-remote": 25}.get(args.config, 16), **sketch)
+               sparse_capacity_log2={"c1": 21, "c5": 23, "c4-remote": 24}.get(args.config, 16), **sketch)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     for p in last.dns:

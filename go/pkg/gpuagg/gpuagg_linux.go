@@ -659,6 +659,11 @@ func (g *gpuAgg) publish() error {
 		g.l.Warn("group-by table full: series undercount", zap.Uint64("lost_updates", lost))
 	}
 	n := int(C.gpuagg_result_count(r))
+	// counter series of this snapshot: what was already added per label tuple.  Tuples
+	// missing from the snapshot are dropped (their slots were retired), and a value below
+	// the last one means the engine restarted the series (a retired slot reused by a pod
+	// of the same namespace/name): the whole value is new.
+	ctrNext := make(map[string]float64, len(g.ctrLast))
 	for i := 0; i < n; i++ {
 		var metric, typ, help *C.char
 		var nl C.uint32_t
@@ -683,10 +688,15 @@ func (g *gpuAgg) publish() error {
 			}
 			// the engine's values are cumulative since reconcile: add the increment
 			key := full + "\x00" + strings.Join(lvals, "\x00")
-			if d := float64(v) - g.ctrLast[key]; d > 0 {
-				vec.WithLabelValues(lvals...).Add(d)
-				g.ctrLast[key] = float64(v)
+			last, seen := g.ctrLast[key]
+			d := float64(v) - last
+			if !seen || float64(v) < last {
+				d = float64(v)
 			}
+			if d > 0 {
+				vec.WithLabelValues(lvals...).Add(d)
+			}
+			ctrNext[key] = float64(v)
 			continue
 		}
 		vec, ok := g.vecs[full]
@@ -696,6 +706,7 @@ func (g *gpuAgg) publish() error {
 		}
 		vec.WithLabelValues(lvals...).Set(float64(v))
 	}
+	g.ctrLast = ctrNext
 	if g.latency != nil || g.noResponse != nil {
 		var st C.gpuagg_latency_state
 		if err := check(ctx, C.gpuagg_latency_read(ctx, &st), "gpuagg_latency_read"); err != nil {

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GPUAGG_ABI_VERSION 1u
+#define GPUAGG_ABI_VERSION 2u  /* 2: columns tcp_id/time_ns, stats, state latency words */
 
 /* error codes */
 #define GPUAGG_OK 0
@@ -71,6 +71,8 @@ typedef struct gpuagg_config {
 #define GPUAGG_FLAG_NO_HOT_KEYS 16u    /* no LDS hot-key cache in front of the group-by table (diagnostics) */
 #define GPUAGG_FLAG_FOLD_PER_BATCH 8u  /* fold the spill / segment lists after every batch instead of
                                           once per gpuagg_sync or state read (diagnostics) */
+#define GPUAGG_FLAG_NO_WIDE_LISTS 32u  /* 192-bit group-by keys straight into the table with memory-side
+                                          atomics, not through per-segment lists (diagnostics) */
 
 int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out);
 /* Number of gfx950 devices visible to this process (one ctx per device). */
@@ -320,6 +322,9 @@ typedef struct gpuagg_state_desc {
   size_t sparse_entry_words;                    /* u64 words per exported entry */
   size_t sparse_len;                            /* group-by table slots (0: none): an
                                                    upper bound on exported entries */
+  uint64_t *latency;       size_t latency_len;  /* node-apiserver latency histograms, counts,
+                                                   sums and no_response: sum u64 (NULL / 0
+                                                   when latency metrics are off)          */
 } gpuagg_state_desc;
 
 int gpuagg_state(gpuagg_ctx *ctx, gpuagg_state_desc *out);
@@ -352,6 +357,11 @@ typedef struct gpuagg_latency_state {
   int64_t handshake_sum;
   uint64_t no_response;             /* entries that expired unanswered                   */
   uint64_t pending;                 /* requests waiting for a reply (carried over)        */
+  uint64_t peak_pending;            /* most requests carried across a batch boundary since
+                                       the last reconcile: a lower bound of the live peak.
+                                       The reference's TTL cache holds at most 100000
+                                       (latency.go:35,121); past that its results differ
+                                       (it drops entries), this engine keeps them all     */
 } gpuagg_latency_state;
 
 int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);

@@ -13,7 +13,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPUAGG_LIB") or os.path.join(HERE, "libgpuagg.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE, ENOTFOUND = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ERR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", ECAPACITY: "ECAPACITY",
              ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE", ENOTFOUND: "ENOTFOUND"}
@@ -31,6 +31,7 @@ class Config(C.Structure):
 FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table
+FLAG_NO_WIDE_LISTS = 32  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
 
 
 class MetricOptions(C.Structure):
@@ -55,7 +56,8 @@ class StateDesc(C.Structure):
                 ("dense_bytes", C.c_void_p),
                 ("cms", C.c_void_p), ("cms_len", C.c_size_t),
                 ("hll", C.c_void_p), ("hll_len", C.c_size_t),
-                ("sparse_entry_words", C.c_size_t), ("sparse_len", C.c_size_t)]
+                ("sparse_entry_words", C.c_size_t), ("sparse_len", C.c_size_t),
+                ("latency", C.c_void_p), ("latency_len", C.c_size_t)]
 
 
 class HubbleCols(C.Structure):
@@ -67,7 +69,7 @@ class LatencyState(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("latency_buckets", C.c_uint64 * 11), ("latency_count", C.c_uint64),
                 ("latency_sum", C.c_int64), ("handshake_buckets", C.c_uint64 * 11),
                 ("handshake_count", C.c_uint64), ("handshake_sum", C.c_int64), ("no_response", C.c_uint64),
-                ("pending", C.c_uint64)]
+                ("pending", C.c_uint64), ("peak_pending", C.c_uint64)]
 
 
 class Stats(C.Structure):

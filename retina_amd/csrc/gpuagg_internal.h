@@ -220,9 +220,10 @@ GA_HD uint64_t ip_entry(uint32_t ip, uint32_t slot, uint32_t api) {
   return (uint64_t)ip | ((uint64_t)slot << 32) | ((uint64_t)(api & 1) << 53);
 }
 
-// Sparse table slots are interleaved: k0 k1 k2 cnt byt + 3 pad words = one 64-byte
-// line per slot, so an insert's CAS / publish / adds touch one line, not five.
-constexpr uint32_t kSparseSlotWords = 8;
+// Sparse table slots are interleaved: k0 k1 k2 cnt byt (40 bytes), so an insert's CAS /
+// publish / adds touch one or two lines, and a segment of slots is one contiguous run
+// that the wide-key fold loads into LDS with coalesced reads.
+constexpr uint32_t kSparseSlotWords = 5;
 // Sparse group-by key: k0 = occ | group<<59 | sub<<53 | s_slot1<<32 | s_ip
 //                      k1 = s_port17<<47 | d_port17<<30 | d_slot1<<9
 //                      k2 = d_ip<<32 | dns_id
@@ -252,6 +253,14 @@ GA_HD uint64_t key_hash(uint64_t k0, uint64_t k1, uint64_t k2) {
 constexpr uint32_t kSparseMaxProbe = 1u << 16;
 // compact table segments: 2^13 (key, count) slots = 128 KiB, folded in LDS
 constexpr uint32_t kSparseSegLog2 = 13, kSparseMaxSegLists = 4096;
+// Wide-key table segments (192-bit keys): 2^12 slots of 40 bytes = the 160 KiB LDS of one
+// fold workgroup.  Probing wraps inside the segment, so a segment is folded alone
+// (sparse_fold_wide_kernel); tables of up to 2^24 slots (4096 segments) take the
+// per-segment lists, bigger ones probe the whole table with memory-side atomics.
+constexpr uint32_t kWideSegLog2 = 12, kWideMaxLog2 = kWideSegLog2 + 12;
+// A wide list entry: k0 k1 k2 and count << 40 | bytes (updates that do not fit go to the
+// table directly)
+constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40;
 constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------

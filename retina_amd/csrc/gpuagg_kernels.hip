@@ -269,9 +269,12 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
     sparse_add_compact(s, k0 | (k2 & 0xFFFFFFFFULL), c);
     return;
   }
-  uint32_t h = (uint32_t)key_hash(k0, k1, k2) & s.mask;
-  for (uint32_t probe = 0; probe < kSparseMaxProbe; ++probe) {
-    const size_t o = (size_t)h * kSparseSlotWords;  // slot h's line (k1 = k0 + 1, ...)
+  // probing wraps inside the key's segment (the unit sparse_fold_wide_kernel folds)
+  const uint32_t h0 = (uint32_t)key_hash(k0, k1, k2) & s.mask, smask = (1u << s.seg_log2) - 1u;
+  const uint32_t seg = h0 & ~smask, nprobe = smask < kSparseMaxProbe ? smask + 1u : kSparseMaxProbe;
+  for (uint32_t probe = 0; probe < nprobe; ++probe) {
+    const uint32_t h = seg | ((h0 + probe) & smask);
+    const size_t o = (size_t)h * kSparseSlotWords;  // slot h (k1 = k0 + 1, ...)
     const unsigned long long cur = atomicCAS(&s.k0[o], 0ULL, (unsigned long long)k0);
     if (cur == 0ULL) {
       atomicExch(&s.k1[o], (unsigned long long)k1);
@@ -292,9 +295,28 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
         }
       }
     }
-    h = (h + 1) & s.mask;
   }
-  atomicAdd(s.dropped, 1ULL);
+  atomicAdd(s.dropped, c);
+}
+
+// Wide keys (192 bits) through per-segment lists: the update is appended to this
+// workgroup's list for the key's table segment (LDS fill counter, one 32-byte store) and
+// sparse_fold_wide_kernel later adds every list into its segment in LDS -- instead of a
+// memory-side CAS + two reads + two adds per cold key.  A full list, or a count / byte
+// sum too wide for the entry, goes to the table directly (exact).
+__device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
+                                            uint64_t b) {
+  if (c < (1ULL << (64 - kWideCountShift)) && b < (1ULL << kWideCountShift)) {
+    const uint32_t w = ((uint32_t)key_hash(k0, k1, k2) & s.mask) >> s.seg_log2;
+    const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
+    if (pos < s.lcap) {
+      ulonglong2 *e = (ulonglong2 *)(s.lists + ((size_t)w * s.lcap + pos) * kWideEntryWords);
+      e[0] = make_ulonglong2(k0, k1);
+      e[1] = make_ulonglong2(k2, (c << kWideCountShift) | b);
+      return;
+    }
+  }
+  sparse_add(s, k0, k1, k2, c, b);
 }
 
 // Exact add of one (count 1, bytes nb) update into a packed u64 LDS word
@@ -446,7 +468,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
 // `valid` is false on lanes with nothing to insert.
 __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, uint64_t k0, uint64_t k1,
                                               uint64_t k2, uint64_t b) {
-  if (s.lists) {  // compact keys: append to the segment's list (LDS fill counter)
+  if (s.lists && s.compact) {  // compact keys: append to the segment's list (LDS fill counter)
     if (!valid) return;
     const uint64_t key = k0 | (k2 & 0xFFFFFFFFULL);
     const uint32_t w = compact_home(s, key) >> s.seg_log2;
@@ -486,7 +508,10 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
       }
     }
   }
-  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b))) sparse_add(s, k0, k1, k2, c, b);
+  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b))) {
+    if (s.lists) wide_append(s, k0, k1, k2, c, b);
+    else sparse_add(s, k0, k1, k2, c, b);
+  }
 }
 
 // One record through every metric group.  Converged: every lane of the wave runs it
@@ -742,8 +767,8 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
   const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and the tags too)
   DevSparse s = a.s;
-  if (a.sp_lists) {
-    s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap;
+  if (a.sp_lists) {  // this workgroup's lists: compact u64 keys or wide 4-word entries
+    s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * (s.compact ? 1u : kWideEntryWords);
     s.lctr = sctr;
     s.lcap = a.sp_cap;
   }
@@ -758,15 +783,20 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
                           if (kSketch && act) sketch_update(a.sk, sip, dip, ports, meta_proto(meta), ls);
                         });
   dense_flush(a, ds);  // (starts with a barrier)
-  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
-    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
-  if (a.hot_n) {  // the cached keys, once per workgroup (dense_flush's barrier precedes)
-    DevSparse g = a.s;
+  if (a.hot_n) {  // the cached keys, once per workgroup (dense_flush's barrier precedes):
+    // into the segment lists with their counts, or straight into the table
+    DevSparse g = s;
+    g.hot = nullptr;
     for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) {
       const HotKey e = hot[i];
-      if (e.tag == 2ULL) sparse_add(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
+      if (e.tag != 2ULL) continue;
+      if (g.lists) wide_append(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
+      else sparse_add(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
     }
+    __syncthreads();
   }
+  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
+    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
 }
 
 // Workgroup w folds table segment w: its 2^seg_log2 (key, count) slots are loaded into
@@ -816,6 +846,72 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) g[i] = ((const ulonglong2 *)seg)[i];
+}
+
+// Workgroup w folds wide-key table segment w (2^seg_log2 slots of k0 k1 k2 cnt byt): the
+// segment is loaded into LDS (field-major, so probes of consecutive slots hit consecutive
+// banks), every aggregation workgroup's list of entries for the segment is inserted with
+// LDS 64-bit CAS / adds -- the probe sequence and claim / publish protocol of sparse_add
+// (a lane that meets a key still being published moves on, so a key may take two slots;
+// the host sums them) -- and the segment is stored back.  Segments no list reaches are
+// not touched.
+__global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, const unsigned long long *lists,
+                                                                const uint32_t *counts, uint32_t n_lists,
+                                                                uint32_t nwin, uint32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long seg[];
+  const uint32_t w = blockIdx.x, N = 1u << s.seg_log2, smask = N - 1u;
+  // lanes per list: the workgroup's threads spread over the lists (a power of two <= 64)
+  uint32_t lpl = 1;
+  while (lpl < 64 && lpl * 2 * n_lists <= blockDim.x) lpl *= 2;
+  const uint32_t lists_per_round = blockDim.x / lpl, sub = threadIdx.x & (lpl - 1);
+  uint32_t any = 0;
+  for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) any |= counts[(size_t)l * nwin + w];
+  if (!__syncthreads_or(any != 0)) return;
+  unsigned long long *K0 = seg, *K1 = seg + N, *K2 = seg + 2 * N, *CN = seg + 3 * N, *BY = seg + 4 * N;
+  unsigned long long *g = s.k0 + (size_t)kSparseSlotWords * ((size_t)w << s.seg_log2);
+  for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {  // coalesced words
+    const uint32_t slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
+    seg[f * N + slot] = g[j];
+  }
+  __syncthreads();
+  auto insert = [&](uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {
+    const uint32_t h = (uint32_t)key_hash(x0, x1, x2) & smask;
+    for (uint32_t probe = 0; probe < N; ++probe) {
+      const uint32_t i = (h + probe) & smask;
+      const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
+      if (cur == 0ULL) {
+        K1[i] = x1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&K2[i], (unsigned long long)x2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // publish
+        atomicAdd(&CN[i], (unsigned long long)c);
+        if (b) atomicAdd(&BY[i], (unsigned long long)b);
+        return;
+      }
+      if (cur == x0 &&
+          __hip_atomic_load(&K2[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == x2 && K1[i] == x1) {
+        atomicAdd(&CN[i], (unsigned long long)c);
+        if (b) atomicAdd(&BY[i], (unsigned long long)b);
+        return;
+      }
+    }
+    atomicAdd(s.dropped, (unsigned long long)c);
+  };
+  // lpl lanes per list, each taking every lpl-th entry (two 16-byte loads per entry)
+  for (uint32_t l0 = 0; l0 < n_lists; l0 += lists_per_round) {
+    const uint32_t l = l0 + threadIdx.x / lpl;
+    if (l >= n_lists) continue;
+    const uint32_t cnt = counts[(size_t)l * nwin + w];
+    const ulonglong2 *e = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap * kWideEntryWords);
+    for (uint32_t k = sub; k < cnt; k += lpl) {
+      const ulonglong2 a0 = e[2 * k], a1 = e[2 * k + 1];
+      insert(a0.x, a0.y, a1.x, a1.y >> kWideCountShift, a1.y & ((1ULL << kWideCountShift) - 1));
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {
+    const uint32_t slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
+    g[j] = seg[f * N + slot];
+  }
 }
 
 // Dense local-context fast path: every group is endpoint-keyed (forward / drop /
@@ -2151,14 +2247,12 @@ __global__ __launch_bounds__(256) void stage_reduce_kernel(const uint32_t *stage
   else stage_reduce_b(stage_b, nwin, nparts, W, lo0, dense_len, d, blockIdx.x - na);
 }
 
-// Writes every slot whole (k0 k1 = 0, k2 = pending, cnt byt pad = 0): four 16-byte
-// stores per 64-byte line, no separate memset.
+// Writes every slot whole (k0 k1 = 0, k2 = pending, cnt byt = 0), no separate memset.
 __global__ void sparse_init_kernel(unsigned long long *k0, size_t n) {
-  static_assert(kSparseSlotWords == 8, "one 64-byte line per slot");
-  ulonglong2 *v = (ulonglong2 *)k0;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n * 4;
+  static_assert(kSparseSlotWords == 5, "k0 k1 k2 cnt byt");
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n * kSparseSlotWords;
        i += (size_t)gridDim.x * blockDim.x)
-    v[i] = (i & 3) == 1 ? make_ulonglong2(kKeyPending, 0ULL) : make_ulonglong2(0ULL, 0ULL);
+    k0[i] = i % kSparseSlotWords == 2 ? kKeyPending : 0ULL;
 }
 
 __global__ void sparse_export_kernel(DevSparse s, size_t cap_slots, unsigned long long *out,
@@ -2472,12 +2566,21 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
                        with_b ? a.win_blocks / a.nwin : 0u, W, a.spill_lo, a.dense_len, dd);
     return hipGetLastError();
   };
-  if (a.sp_lists) {
+  if (a.sp_lists && a.sparse.compact) {
     const size_t seg_lds = (size_t)16 << a.sparse.seg_log2;
     if ((e = hipFuncSetAttribute((const void *)sparse_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)seg_lds)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(sparse_fold_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, dev_sparse(a.sparse),
+                       (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else if (a.sp_lists) {
+    const size_t seg_lds = (size_t)8 * kSparseSlotWords << a.sparse.seg_log2;
+    if (seg_lds > kLdsBytes) return hipErrorInvalidValue;
+    if ((e = hipFuncSetAttribute((const void *)sparse_fold_wide_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)seg_lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(sparse_fold_wide_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, dev_sparse(a.sparse),
                        (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

@@ -212,7 +212,8 @@ struct gpuagg_ctx {
   uint64_t lat_carry_bound = 0;  // >= entries currently carried
   void *d_lat_tmp = nullptr;
   size_t lat_tmp_alloc = 0;
-  uint64_t *h_lat_n = nullptr;   // pinned: the batch's event count
+  uint64_t *h_lat_n = nullptr;   // pinned: state words [kLatPending, kLatEvents] of the batch
+  uint64_t lat_peak_pending = 0; // most requests carried into a batch since the reconcile
   int64_t time_offset = 0;       // ktime.MonotonicOffset added to decoded record times
   uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
   size_t ipl_all_alloc = 0;
@@ -521,7 +522,7 @@ int ensure_sparse(gpuagg_ctx *c) {
   if (lg < 4 || lg > 30) return fail(c, GPUAGG_EINVAL, "sparse_capacity_log2 %u out of [4,30]", lg);
   const size_t n = (size_t)1 << lg;
   int rc;
-  // one interleaved array: slot h = words [8h, 8h + 8) = k0 k1 k2 cnt byt pad (kSparseSlotWords)
+  // one interleaved array: slot h = words [5h, 5h + 5) = k0 k1 k2 cnt byt (kSparseSlotWords)
   if ((rc = dev_alloc(c, &c->sv.k0, n * kSparseSlotWords)) || (rc = dev_alloc(c, &c->sv.dropped, 1)) ||
       (rc = dev_alloc(c, &c->d_counter, 1)))
     return rc;
@@ -772,6 +773,7 @@ int lat_reset(gpuagg_ctx *c, bool full) {
   if (full) {
     HIPCHK(c, hipMemsetAsync(c->d_lat, 0, kLatStateWords * 8, c->stream));
     c->lat_carry_bound = 0;
+    c->lat_peak_pending = 0;
   } else {
     HIPCHK(c, hipMemsetAsync(c->d_lat + kLatHist, 0, (kLatStateWords - kLatHist) * 8, c->stream));
   }
@@ -834,13 +836,16 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.hash_out = c->d_lat_hash + c->lat_ev_alloc;
   a.idx_in = c->d_lat_idx;
   a.idx_out = c->d_lat_idx + c->lat_ev_alloc;
-  if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8, hipHostMallocDefault) != hipSuccess)
-    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(8)");
+  constexpr size_t kLatReadWords = kLatEvents - kLatPending + 1;
+  if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8 * kLatReadWords, hipHostMallocDefault) != hipSuccess)
+    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", 8 * kLatReadWords);
   a.carry_in = c->d_lat_carry[c->lat_carry_cur];  // copied into the events by the front
   HIPCHK(c, launch_latency_front(a, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_lat_n, c->d_lat + kLatEvents, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_lat_n, c->d_lat + kLatPending, 8 * kLatReadWords, hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint64_t ne = *c->h_lat_n;
+  const uint64_t ne = c->h_lat_n[kLatEvents - kLatPending];
+  c->lat_peak_pending = std::max<uint64_t>(c->lat_peak_pending, c->h_lat_n[0]);  // carried into this batch
   // carry-out buffer: at most one entry per event
   if (ne > c->lat_carry_alloc) {
     LatEvent *keep = c->d_lat_carry[c->lat_carry_cur];  // read by this batch already (copied)
@@ -869,6 +874,8 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 
 // Launches whose list folds may wait for one fold_pending (see Pending).
 constexpr uint64_t kDeferLaunches = 16;
+// Device memory for the wide-key segment lists of one ctx (32-byte entries).
+constexpr uint64_t kWideListBytes = 2ull << 30;
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
@@ -940,7 +947,11 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   // counters take LDS words from the dense window
   const bool generic = !a.dense_ng || a.dns_compact;  // kernels that take compact-key lists
   const uint64_t sp_nwin = c->sparse_slots ? c->sparse_slots >> c->sv.seg_log2 : 0;
-  const bool sp_lists = generic && c->sv.compact && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
+  // wide (192-bit) keys take per-segment lists too when the table has at most 4096
+  // segments of 2^12 slots (sparse_fold_wide_kernel folds one per workgroup)
+  const bool wide_lists = !c->sv.compact && c->sparse_slots && c->sparse_slots <= (1ull << kWideMaxLog2) &&
+                          !(c->cfg.flags & GPUAGG_FLAG_NO_WIDE_LISTS);
+  const bool sp_lists = generic && (c->sv.compact || wide_lists) && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
                         !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH);
   // plans with HBM-table keys (remote context, ip / port options): an LDS cache of the
   // hot keys per workgroup in front of the table (hot_add in gpuagg_kernels.hip)
@@ -1035,7 +1046,11 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       if (sp_lists) {
         const uint64_t mean = budget / sp_nwin;
         g.sp_nwin = (uint32_t)sp_nwin;
-        g.sp_cap = (uint32_t)((mean + mean / 4 + 64 + 1) & ~1ULL);  // even: 16-byte key pairs
+        uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
+        if (!c->sv.compact)  // 32-byte entries: at most kWideListBytes of lists per ctx
+          cap = std::max<uint64_t>(16, std::min<uint64_t>(cap, kWideListBytes / (8 * kWideEntryWords) /
+                                                                   ((uint64_t)a.blocks * sp_nwin)));
+        g.sp_cap = (uint32_t)cap;
       }
       return g;
     };
@@ -1064,6 +1079,10 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     uint64_t budget = defer ? std::max<uint64_t>(a.chunk, std::min<uint64_t>(kMaxRecordsPerBlock,
                                                                              kDeferLaunches * a.chunk))
                             : a.chunk;
+    if (defer && !c->sv.compact) {  // wide lists: only as many launches as the list memory holds
+      const uint64_t cap = kWideListBytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin);
+      budget = std::max<uint64_t>(a.chunk, std::min<uint64_t>(budget, cap * sp_nwin * 4 / 5));
+    }
     bool accum = false;
     if (c->pend.active) {
       const LaunchArgs &q = c->pend.a;
@@ -1094,7 +1113,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.sp_counts = nullptr;
     a.sp_nwin = 0;
     if (g.sp_nwin) {
-      if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc, (size_t)a.blocks * g.sp_nwin * g.sp_cap)))
+      if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc,
+                           (size_t)a.blocks * g.sp_nwin * g.sp_cap * (c->sv.compact ? 1u : kWideEntryWords))))
         return rc;
       if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * g.sp_nwin))) return rc;
       a.sp_lists = c->d_sp_lists;
@@ -1525,6 +1545,11 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
       compact &= (groups[g].family == FAM_DNS_REQ || groups[g].family == FAM_DNS_RESP) &&
                  !(groups[g].src_opts & (OPT_IP | OPT_PORT));
   c->sv.compact = compact ? 1u : 0u;
+  if (c->sparse_slots) {  // probe / fold segments: compact 2^13 slots; wide 2^12 (or the table)
+    const uint32_t lg = (uint32_t)__builtin_ctzll(c->sparse_slots);
+    c->sv.seg_log2 = compact ? std::min<uint32_t>(lg, kSparseSegLog2)
+                             : (lg <= kWideMaxLog2 ? std::min<uint32_t>(lg, kWideSegLog2) : lg);
+  }
   c->inst = inst;
   c->groups = groups;
   c->plan = p;
@@ -2493,6 +2518,10 @@ int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   o->hll_len = c->hll_len;
   o->sparse_entry_words = kSparseEntryWords;
   o->sparse_len = c->sparse_slots;
+  // the latency words a merge sums: both histograms (buckets, count, sum) and no_response
+  // (the gaps between them are zero); the clock and the carried requests stay per shard
+  o->latency = c->d_lat ? (uint64_t *)c->d_lat + kLatHist : nullptr;
+  o->latency_len = c->d_lat ? kLatStateWords - kLatHist : 0;
   return GPUAGG_OK;
 }
 
@@ -2764,6 +2793,7 @@ int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
   out->handshake_sum = (int64_t)w[kLatHandshake + 12];
   out->no_response = w[kLatNoResponse];
   out->pending = w[kLatPending];
+  out->peak_pending = std::max<uint64_t>(c->lat_peak_pending, w[kLatPending]);
   return GPUAGG_OK;
 }
 

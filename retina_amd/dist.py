@@ -10,6 +10,7 @@
     HLL registers   all_reduce MAX (u8)
     sparse table    all_gather of compacted (k0,k1,k2,count,bytes) entries, inserted-and-
                     added on the merging rank (gpuagg_sparse_import)
+    latency         all_reduce SUM of the histogram / count / sum / no_response words
   Counters and count-min are linear and HLL max is exact, so the merged state equals the
   1-GPU state bit for bit.
 """
@@ -154,6 +155,10 @@ def merge_engine(engine, group=None, dst: int = 0) -> None:
         reduce(st.cms, st.cms_len, "<i4", dist.ReduceOp.SUM)
     if st.hll_len:
         reduce(st.hll, st.hll_len, "|u1", dist.ReduceOp.MAX)
+    # node-apiserver latency histograms / counts / sums and no_response: summed like the
+    # counters (the pending requests stay on their shard: each shard runs its own clock)
+    if st.latency_len:
+        reduce(st.latency, st.latency_len, "<i8", dist.ReduceOp.SUM)
     # sparse table: every rank's compact entries gathered on dst and inserted-and-added
     cap = int(st.sparse_len)
     local = torch.empty((max(cap, 1), 5), dtype=torch.int64, device=device)

@@ -287,7 +287,8 @@ class GpuAgg:
         return {"enabled": st.enabled, "latency_buckets": list(st.latency_buckets),
                 "latency_count": st.latency_count, "latency_sum": st.latency_sum,
                 "handshake_buckets": list(st.handshake_buckets), "handshake_count": st.handshake_count,
-                "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending}
+                "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending,
+                "peak_pending": st.peak_pending}
 
     # -- enriched-flow emission, standard mode (enrich_kernel) --------------------------
     def enrich_device(self, cols: "_abi.Columns", n: int, src_slot, dst_slot) -> None:

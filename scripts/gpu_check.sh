@@ -47,8 +47,8 @@ for s in $STEPS; do
       i=0
       for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
                  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS" \
-                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_FLAT GRBM_GUI_ACTIVE" \
-                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_FLAT SQ_INSTS_LDS_ATOMIC GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_ATOMIC_sum"; do
         i=$((i+1))
         timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d "$OUT/${TAG}_pmc_${cfg}_$i" -o run \
           -- python3 "$R/bench.py" --config "$cfg" --steps 2 --warmup 1 --no-cpu-baseline --no-host-fed \

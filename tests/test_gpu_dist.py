@@ -115,3 +115,76 @@ def test_two_rank_engine_merge_equals_single(gpu_device):
     # the merged state is non-trivial: dense, sparse (DNS, remote) and sketches all present
     assert any(k[0].endswith("dns_request_count") for k in want[0][0])
     assert len(want[1][0]) > 1000 and want[0][1].sum() == 4 * N
+
+
+LAT_API = [W.ip_le(10, 255, 0, 1), W.ip_le(10, 255, 0, 2)]
+LAT_SPEC = [{"metric_name": "node_apiserver_latency"}, {"metric_name": "node_apiserver_handshake_latency"},
+            {"metric_name": "node_apiserver_no_response"},
+            {"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+
+
+def _lat_data():
+    pods = W.make_pods(200, seed=31)
+    return pods, W.gen_latency_records(400, pods, LAT_API, seed=32, background=3000)
+
+
+def _lat_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from retina_amd import GpuAgg
+    from retina_amd import dist as D
+    from .test_gpu_latency import _dev
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        pods, recs = _lat_data()
+        mine = D.shard_records(recs, world, rank)
+        g = make_engine(pods, LAT_SPEC, False, 0)
+        g.set_apiserver_ips(LAT_API)
+        g.submit_device(GpuAgg.device_columns(*_dev(mine, 0)), len(mine.src_ip))
+        D.merge_engine(g)
+        st = g.latency_state()
+        g.close()
+        q.put((rank, len(mine.src_ip), st))
+    except Exception as e:
+        q.put((rank, -1, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_latency_merge(gpu_device):
+    """merge_engine sums the node-apiserver latency histograms and no_response of every
+    rank into rank 0 before the other ranks reset (their observations used to be lost)."""
+    import torch.multiprocessing as mp
+    from .latency_helpers import as_state, oracle_latency
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_lat_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    deadline = time.monotonic() + 240
+    while len(res) < world:
+        try:
+            rank, n, r = q.get(timeout=5)
+            assert n >= 0, r
+            res[rank] = (n, r)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, "rank exited with %r" % dead
+            assert time.monotonic() < deadline, "ranks did not report within 240 s"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pods, recs = _lat_data()
+    want = as_state(oracle_latency(recs, LAT_API))
+    got, rest = res[0][1], res[1][1]
+    for k in ("latency_buckets", "latency_count", "latency_sum", "handshake_buckets", "handshake_count",
+              "handshake_sum"):
+        assert got[k] == want[k], k
+    assert got["no_response"] + got["pending"] + rest["pending"] == want["no_response"] + want["pending"]
+    assert rest["latency_count"] == 0 and rest["no_response"] == 0
+    assert want["latency_count"] > 0

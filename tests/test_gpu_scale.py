@@ -110,13 +110,16 @@ def test_packed_field_overflow_exact(gpu_device, flags):
 
 
 DEFER = [
-    ("c2", W.LOCAL_FWD_DROP, 10_000, {}),
-    ("c5", W.C5_SPEC, 100_000, {"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
+    ("c2", W.LOCAL_FWD_DROP, False, 10_000, {}),
+    ("c5", W.C5_SPEC, False, 100_000, {"drop_frac": 0.0, "retrans_frac": 0.05, "dns_frac": 0.35}),
+    # wide (192-bit) keys through the per-segment lists: local ip option and remote context
+    ("c1-local", W.C1_LOCAL, False, 10_000, {}),
+    ("c4-remote", W.C1_REMOTE, True, 10_000, dict(W.CONFIGS["c4"]["gen"])),
 ]
 
 
-@pytest.mark.parametrize("cid,sp,npods,gen", DEFER, ids=[d[0] for d in DEFER])
-def test_deferred_folds_exact(gpu_device, cid, sp, npods, gen):
+@pytest.mark.parametrize("cid,sp,remote,npods,gen", DEFER, ids=[d[0] for d in DEFER])
+def test_deferred_folds_exact(gpu_device, cid, sp, remote, npods, gen):
     """Spill / segment lists of consecutive launches are folded once (gpuagg_sync or any
     state read).  43 batches of unequal sizes: a growing chunk changes the list geometry,
     a snapshot folds early, then 36 equal batches exhaust the 16-launch budget twice --
@@ -131,7 +134,7 @@ def test_deferred_folds_exact(gpu_device, cid, sp, npods, gen):
     n_mid, n = int(bounds[4]), int(bounds[-1])
 
     def run(flags):
-        g = make_engine(pods, sp, False, gpu_device, recs, sparse_capacity_log2=23, flags=flags)
+        g = make_engine(pods, sp, remote, gpu_device, recs, sparse_capacity_log2=23, flags=flags)
         try:
             ts = to_device(recs, gpu_device)
             mid = None
@@ -146,7 +149,7 @@ def test_deferred_folds_exact(gpu_device, cid, sp, npods, gen):
     def port(m):
         part = W.Records(recs.src_ip[:m], recs.dst_ip[:m], recs.bytes[:m], recs.meta[:m], recs.ports[:m],
                          recs.dns_id[:m])
-        r = RefCPU(sp, pods.endpoints, False, recs.dns)
+        r = RefCPU(sp, pods.endpoints, remote, recs.dns)
         r.process(part)
         s = r.series()
         r.close()
@@ -174,8 +177,65 @@ def test_hot_key_cache_exact(gpu_device, gen):
     b = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
                                   sparse_capacity_log2=23, flags=_abi.FLAG_NO_HOT_KEYS))
     assert a == b, diff_series(a, b)
+    # neither the hot-key cache nor the per-segment lists: memory-side atomics only
+    c = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
+                                  sparse_capacity_log2=23,
+                                  flags=_abi.FLAG_NO_HOT_KEYS | _abi.FLAG_NO_WIDE_LISTS))
+    assert a == c, diff_series(a, c)
     r = RefCPU(W.C1_REMOTE, pods.endpoints, True, recs.dns)
     r.process(recs)
     want = r.series()
     r.close()
     assert a == want, diff_series(a, want)
+
+
+def _table_entries(g, device):
+    """The engine's group-by table as canonical (k0, k1, k2) -> (count, bytes) tensors:
+    exported on the device, keys that took two slots summed (torch.unique + index_add)."""
+    import torch
+    st = g.state()
+    cap = int(st.sparse_len)
+    out = torch.empty((cap, 5), dtype=torch.int64, device=device)
+    n = g.sparse_export(out.data_ptr(), cap)
+    e = out[:n]
+    keys, inv = torch.unique(e[:, :3], dim=0, return_inverse=True)
+    vals = torch.zeros((keys.shape[0], 2), dtype=torch.int64, device=device)
+    vals.index_add_(0, inv, e[:, 3:5])
+    return keys, vals
+
+
+def test_full_c4_remote_linearity(gpu_device):
+    """C4 through the remote context at the full bench size: 100M Zipf(1.2) flow records,
+    every update a 192-bit group-by key (~6.7M distinct).  The per-segment lists + LDS
+    segment folds equal the memory-side-atomics path exactly; a second pass of the same
+    records doubles every entry (determinism, linearity); no update is dropped."""
+    import torch
+    from retina_amd import GpuAgg, _abi
+    pods = W.make_pods(10_000, seed=4)
+    n, chunk = 100_000_000, 8_000_000
+    dev = torch.device("cuda", gpu_device)
+    cols = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(6)]
+    for k, a in enumerate(range(0, n, chunk)):
+        m = min(chunk, n - a)
+        r = W.gen_records(m, pods, seed=4000 + k, **W.CONFIGS["c4"]["gen"])
+        for t, x in zip(cols, (r.src_ip, r.dst_ip, r.bytes, r.meta, r.ports, r.dns_id)):
+            t[a:a + m].copy_(torch.from_numpy(x.view(np.int32)))
+    dc = GpuAgg.device_columns(*cols)
+    g = make_engine(pods, W.C1_REMOTE, True, gpu_device, sparse_capacity_log2=24)
+    g.submit_device(dc, n)
+    g.sync()
+    k1, v1 = _table_entries(g, dev)
+    g.submit_device(dc, n)
+    g.sync()
+    k2, v2 = _table_entries(g, dev)
+    assert g.stats()["sparse_dropped"] == 0
+    g.close()
+    assert torch.equal(k1, k2) and torch.equal(v2, 2 * v1)
+    assert int(v1[:, 0].sum()) == n  # every record is one forward or one drop update
+    b = make_engine(pods, W.C1_REMOTE, True, gpu_device, sparse_capacity_log2=24,
+                    flags=_abi.FLAG_NO_HOT_KEYS | _abi.FLAG_NO_WIDE_LISTS)
+    b.submit_device(dc, n)
+    b.sync()
+    kb, vb = _table_entries(b, dev)
+    b.close()
+    assert torch.equal(k1, kb) and torch.equal(v1, vb)
