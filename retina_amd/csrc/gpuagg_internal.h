@@ -201,6 +201,29 @@ GA_HD uint32_t ipl_image_bytes(uint32_t nb) {
   return ((nb * kIplWays * 4 + 15) & ~15u) + ((nb * kIplWays * 2 + 2 + 15) & ~15u);
 }
 GA_HD uint32_t ipl_vals_offset(uint32_t nb) { return (nb * kIplWays * 4 + 15) & ~15u; }
+// Radix LDS image (tier-1, when every pod IP falls in at most kIprMaxPfx /16 prefixes, as
+// cluster pod CIDRs do): a /16 prefix is matched by compares against kernel arguments,
+// the third octet indexes that prefix's row of u16 block ids, and the block's 256 u16
+// slots are indexed by the fourth octet -- two dependent u16 reads and ~8 VALU per IP
+// instead of two 8-byte bucket reads, a slot read and ~20 VALU.  Node pod CIDRs are /24s,
+// so the blocks are the populated /24s (C2's 10k pods + secondaries: 80 blocks, 42 KiB).
+// Layout: bidx u16[(npfx + 1) * 256] (row npfx: no prefix matched, all 0), then
+// blk u16[(nblk + 1) * 256] with block 0 the "no pod" block (all kIplNoSlot).
+constexpr uint32_t kIprMaxPfx = 4;
+constexpr uint32_t kIprNoPfx = 0xFFFFFFFFu;  // unused prefix value: never equals ip & 0xFFFF
+GA_HD uint32_t ipr_blk_offset(uint32_t npfx) { return (npfx + 1) * 256 * 2; }
+GA_HD uint32_t ipr_image_bytes(uint32_t npfx, uint32_t nblk) { return ipr_blk_offset(npfx) + (nblk + 1) * 256 * 2; }
+// row of bidx for ip: prefix index (npfx when none matches) << 8 | third octet
+GA_HD uint32_t ipr_row(uint32_t ip, uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t npfx) {
+  const uint32_t p = ip & 0xFFFFu;
+  uint32_t j = npfx;
+  j = p == p3 ? 3u : j;
+  j = p == p2 ? 2u : j;
+  j = p == p1 ? 1u : j;
+  j = p == p0 ? 0u : j;
+  return (j << 8) | ((ip >> 16) & 0xFFu);
+}
+
 // 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
 // correct the rare carry / wrap exactly with global atomics; count-only families
 // (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).

@@ -866,7 +866,15 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   const uint32_t lists_per_round = blockDim.x / lpl, sub = threadIdx.x & (lpl - 1);
   uint32_t any = 0;
   for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) any |= counts[(size_t)l * nwin + w];
-  if (!__syncthreads_or(any != 0)) return;
+  // (a flag word in the segment's LDS: __syncthreads_or would take static LDS beyond the
+  // 160 KiB the segment may fill)
+  if (threadIdx.x == 0) seg[0] = 0ULL;
+  __syncthreads();
+  if (any) seg[0] = 1ULL;
+  __syncthreads();
+  const bool work = seg[0] != 0ULL;
+  __syncthreads();
+  if (!work) return;
   unsigned long long *K0 = seg, *K1 = seg + N, *K2 = seg + 2 * N, *CN = seg + 3 * N, *BY = seg + 4 * N;
   unsigned long long *g = s.k0 + (size_t)kSparseSlotWords * ((size_t)w << s.seg_log2);
   for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {  // coalesced words

@@ -91,4 +91,55 @@ inline uint32_t ipl_probe(const uint8_t *img, uint32_t nb, uint32_t seed, uint32
   return vals[j];
 }
 
+// ---- radix LDS image (gpuagg_internal.h, "Radix LDS image") --------------------------
+struct IprImage {
+  uint32_t npfx = 0, nblk = 0;
+  uint32_t pfx[kIprMaxPfx] = {kIprNoPfx, kIprNoPfx, kIprNoPfx, kIprNoPfx};
+  std::vector<uint8_t> bytes;  // ipr_image_bytes(npfx, nblk)
+};
+
+// Returns false when the set needs more than kIprMaxPfx /16 prefixes, a slot >= 0xFFFF,
+// or more than max_bytes of image; the caller then uses the cuckoo image.
+inline bool ipr_build(const std::vector<std::pair<uint32_t, uint32_t>> &ents, IprImage *out,
+                      uint32_t max_bytes = kIplMaxBytes) {
+  IprImage im;
+  std::vector<uint32_t> rowblk;  // (prefix, third octet) -> block, 0 = none yet
+  for (const auto &e : ents) {
+    if (e.second >= kIplNoSlot) return false;
+    const uint32_t p = e.first & 0xFFFFu;
+    uint32_t j = 0;
+    while (j < im.npfx && im.pfx[j] != p) ++j;
+    if (j == im.npfx) {
+      if (im.npfx == kIprMaxPfx) return false;
+      im.pfx[im.npfx++] = p;
+    }
+  }
+  rowblk.assign((size_t)kIprMaxPfx * 256, 0);
+  std::vector<uint16_t> blk(256, (uint16_t)kIplNoSlot);  // block 0: no pod
+  for (const auto &e : ents) {
+    const uint32_t row = ipr_row(e.first, im.pfx[0], im.pfx[1], im.pfx[2], im.pfx[3], im.npfx);
+    if (!rowblk[row]) {
+      if (im.nblk + 1 >= 0xFFFFu) return false;
+      rowblk[row] = ++im.nblk;
+      blk.resize((size_t)(im.nblk + 1) * 256, (uint16_t)kIplNoSlot);
+    }
+    blk[(size_t)rowblk[row] * 256 + (e.first >> 24)] = (uint16_t)e.second;
+  }
+  if (ipr_image_bytes(im.npfx, im.nblk) > max_bytes) return false;
+  im.bytes.assign(ipr_image_bytes(im.npfx, im.nblk), 0);
+  uint16_t *bidx = (uint16_t *)im.bytes.data();
+  for (uint32_t r = 0; r < im.npfx * 256; ++r) bidx[r] = (uint16_t)rowblk[r];
+  memcpy(im.bytes.data() + ipr_blk_offset(im.npfx), blk.data(), blk.size() * 2);
+  *out = std::move(im);
+  return true;
+}
+
+// Host mirror of the kernel's radix probe: slot or kIplNoSlot.
+inline uint32_t ipr_probe(const IprImage &im, uint32_t ip) {
+  const uint16_t *bidx = (const uint16_t *)im.bytes.data();
+  const uint16_t *blk = (const uint16_t *)(im.bytes.data() + ipr_blk_offset(im.npfx));
+  const uint32_t row = ipr_row(ip, im.pfx[0], im.pfx[1], im.pfx[2], im.pfx[3], im.npfx);
+  return blk[((uint32_t)bidx[row] << 8) | (ip >> 24)];
+}
+
 }  // namespace gpuagg

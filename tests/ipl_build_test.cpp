@@ -34,8 +34,27 @@ int main() {
         absent_ok += ipl_probe(im.bytes.data(), im.nb, im.seed, ip) == kIplNoSlot;
       }
     }
-    printf("%d %u %u %zu %.1f %ld %ld\n", ok ? 1 : 0, im.nb, im.seed, im.bytes.size(),
-           ok ? 100.0 * n / (im.nb * kIplWays) : 0.0, found, absent_ok);
+    // the radix image of the same set (when its prefixes allow one): same answers
+    IprImage ir;
+    const bool rok = ipr_build(ents, &ir);
+    long rfound = 0, rabsent = 0;  // rabsent: absent IPs that did NOT miss
+    if (rok) {
+      for (const auto &e : ents) rfound += ipr_probe(ir, e.first) == e.second;
+      std::mt19937 rng(s + 1000);
+      std::vector<uint32_t> sorted;
+      for (const auto &e : ents) sorted.push_back(e.first);
+      std::sort(sorted.begin(), sorted.end());
+      for (int i = 0; i < 100000; ++i) {
+        // half random, half near the pod IPs (same /16 and /24 prefixes)
+        uint32_t ip = rng();
+        if (i & 1 && !sorted.empty()) ip = (sorted[rng() % sorted.size()] & 0x00FFFFFFu) | (rng() & 0xFF000000u);
+        if (std::binary_search(sorted.begin(), sorted.end(), ip)) continue;
+        rabsent += ipr_probe(ir, ip) != kIplNoSlot;  // wrong answers
+      }
+    }
+    printf("%d %u %u %zu %.1f %ld %ld %d %u %u %zu %ld %ld\n", ok ? 1 : 0, im.nb, im.seed, im.bytes.size(),
+           ok ? 100.0 * n / (im.nb * kIplWays) : 0.0, found, absent_ok, rok ? 1 : 0, ir.npfx, ir.nblk,
+           ir.bytes.size(), rfound, rabsent);
   }
   return 0;
 }

@@ -31,9 +31,10 @@ def run_sets(exe, sets):
     res = []
     for ln in out:
         if ln.strip():
-            built, nb, seed, nbytes, load, found, absent = ln.split()
+            built, nb, seed, nbytes, load, found, absent, rbuilt, npfx, nblk, rbytes, rfound, rabsent = ln.split()
             res.append(dict(built=int(built), nb=int(nb), bytes=int(nbytes), load=float(load),
-                            found=int(found), absent=int(absent)))
+                            found=int(found), absent=int(absent), rbuilt=int(rbuilt), npfx=int(npfx),
+                            nblk=int(nblk), rbytes=int(rbytes), rfound=int(rfound), rabsent=int(rabsent)))
     return res
 
 
@@ -64,3 +65,22 @@ def test_builder_refuses_unimageable(harness):
     bad_key = [(0xFFFFFFFF, 3)]                                      # empty-key marker
     r = run_sets(harness, [too_many, bad_slot, bad_key])
     assert [x["built"] for x in r] == [0, 0, 0]
+
+
+def test_radix_image_matches(harness):
+    """The radix image (pod IPs in <= 4 /16 prefixes): every key found with its slot,
+    absent IPs -- random and next to pod IPs -- miss; C2's 10k pods take ~80 /24 blocks."""
+    sets = pod_sets()
+    res = run_sets(harness, sets)
+    for ents, r in zip(sets, res):
+        if not r["rbuilt"]:
+            continue
+        assert r["rfound"] == len(ents)
+        assert r["rabsent"] == 0  # no absent IP resolves to a slot
+        assert r["rbytes"] <= 112 * 1024
+    c2 = res[4]  # make_pods(10_000): 10.0.x.x primaries + 10.128.x.x secondaries
+    assert c2["rbuilt"] == 1 and c2["npfx"] == 2 and 70 <= c2["nblk"] <= 80
+    assert res[5]["rbuilt"] == 0  # random IPs: far more than 4 prefixes
+    # more than 4 prefixes, or a reserved slot id, refuse
+    r = run_sets(harness, [[(0x0A00 + k | (i << 24), i) for k in range(5) for i in range(3)], [(1, 0xFFFF)]])
+    assert [x["rbuilt"] for x in r] == [0, 0]
