@@ -71,6 +71,8 @@ typedef struct gpuagg_config {
 #define GPUAGG_FLAG_NO_HOT_KEYS 16u    /* no LDS hot-key cache in front of the group-by table (diagnostics) */
 #define GPUAGG_FLAG_FOLD_PER_BATCH 8u  /* fold the spill / segment lists after every batch instead of
                                           once per gpuagg_sync or state read (diagnostics) */
+#define GPUAGG_FLAG_LDS_CUCKOO 64u     /* tier-1 LDS IP image as the cuckoo table even when the radix
+                                          image fits (diagnostics) */
 #define GPUAGG_FLAG_NO_WIDE_LISTS 32u  /* 192-bit group-by keys straight into the table with memory-side
                                           atomics, not through per-segment lists (diagnostics) */
 

@@ -31,6 +31,7 @@ class Config(C.Structure):
 FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table
+FLAG_LDS_CUCKOO = 64  # diagnostics: cuckoo LDS IP image even when the radix image fits
 FLAG_NO_WIDE_LISTS = 32  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
 
 

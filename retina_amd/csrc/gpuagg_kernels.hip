@@ -146,6 +146,7 @@ struct KArgs {
   // tier-1: LDS image of the IP table
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (dense_lds_kernel kRadix)
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
   // compact group-by keys bucketed per table segment (generic kernel), or null
@@ -1336,12 +1337,45 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
   }
 }
 
-template <int NG, bool kVec, uint32_t SIG>
+// One IP through the tier-1 LDS image: slot or kIplNoSlot (inactive lanes: kIplNoSlot).
+// kRadix: the radix image (two dependent u16 reads); else the cuckoo image.
+template <bool kRadix>
+struct IplView {
+  const uint8_t *smem;
+  uint32_t nb, seed, npfx, p0, p1, p2, p3;
+  __device__ __forceinline__ uint32_t lookup(uint32_t ip) const {
+    if (kRadix) {
+      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
+      return blk[((uint32_t)bidx[ipr_row(ip, p0, p1, p2, p3, npfx)] << 8) | (ip >> 24)];
+    }
+    return ipl_slot((const uint16_t *)(smem + ipl_vals_offset(nb)), ipl_probe_index((const uint32_t *)smem, nb, seed, ip));
+  }
+  // the 8 IPs of a step, every read of a level issued before the next level
+  __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
+    if (kRadix) {
+      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
+      uint32_t bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bi[k] = bidx[act ? ipr_row(ip[k], p0, p1, p2, p3, npfx) : npfx << 8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = blk[(bi[k] << 8) | (ip[k] >> 24)];
+      return;
+    }
+    const uint32_t *keys = (const uint32_t *)smem;
+    const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+    uint32_t j[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
+  }
+};
+
+template <int NG, bool kVec, uint32_t SIG, bool kRadix>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t nb = a.ipl_nb;
-  const uint32_t *keys = (const uint32_t *)smem;
-  const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+  const IplView<kRadix> iv{smem, a.ipl_nb, a.ipl_seed, a.ipl_npfx, a.ipl_pfx[0], a.ipl_pfx[1], a.ipl_pfx[2],
+                           a.ipl_pfx[3]};
   uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
   const uint32_t L4 = a.lds_bins;
   for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
@@ -1354,7 +1388,6 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const L4Ctx l4{bins, L4 + lane, a.d};
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
   const DenseGroups<NG, SIG> G(a.p, L4);
-  const uint32_t seed = a.ipl_seed;
   SpillQ q{};
   // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
   auto q_flush = [&](bool full) {
@@ -1388,12 +1421,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
       nbv = rec_ld(&b4[vl]);
       nm = rec_ld(&m4[vl]);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
-      uint32_t j[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
       uint32_t sl[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
+      iv.lookup8(ip, act, sl);
       const uint32_t ss[4] = {sl[0], sl[1], sl[2], sl[3]}, sd[4] = {sl[4], sl[5], sl[6], sl[7]};
       const uint32_t by[4] = {vb.x, vb.y, vb.z, vb.w}, me[4] = {vm.x, vm.y, vm.z, vm.w};
       if (!G.any_spilled) {
@@ -1428,8 +1457,8 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     tail = start + (vn << 2);
   }
   for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {
-    const uint32_t ss[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.src[i]))};
-    const uint32_t sd[1] = {ipl_slot(vals, ipl_probe_index(keys, nb, seed, a.c.dst[i]))};
+    const uint32_t ss[1] = {iv.lookup(a.c.src[i])};
+    const uint32_t sd[1] = {iv.lookup(a.c.dst[i])};
     const uint32_t by[1] = {a.c.bytes[i]}, me[1] = {a.c.meta[i]};
     l4_records<NG, SIG, 1>(G, l4, ds, by, me, ss, sd);
   }
@@ -2435,6 +2464,16 @@ static hipError_t launch_k(K kern, const KArgs &k, uint32_t blocks, uint32_t thr
   return hipGetLastError();
 }
 
+// dense_lds_kernel<NG, ., SIG, .> by the launch's vector loads and LDS image form
+template <int NG, uint32_t SIG>
+static hipError_t launch_lds(const LaunchArgs &a, const KArgs &k, uint32_t B, uint32_t T, size_t lds, hipStream_t st) {
+  if (a.vec)
+    return a.ipl_radix ? launch_k(dense_lds_kernel<NG, true, SIG, true>, k, B, T, lds, st)
+                       : launch_k(dense_lds_kernel<NG, true, SIG, false>, k, B, T, lds, st);
+  return a.ipl_radix ? launch_k(dense_lds_kernel<NG, false, SIG, true>, k, B, T, lds, st)
+                     : launch_k(dense_lds_kernel<NG, false, SIG, false>, k, B, T, lds, st);
+}
+
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between, const char **kernel) {
   if (a.n == 0) return hipSuccess;
   KArgs k{};
@@ -2457,6 +2496,8 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_nb = a.ipl_nb;
   k.ipl_seed = a.ipl_seed;
   k.ipl_bytes = a.ipl_bytes;
+  k.ipl_npfx = a.ipl_npfx;
+  for (uint32_t j = 0; j < kIprMaxPfx; ++j) k.ipl_pfx[j] = a.ipl_pfx[j];
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
   k.sp_lists = (unsigned long long *)a.sp_lists;
@@ -2492,8 +2533,9 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (kernel) {
     static thread_local char name[64];
     if (a.tier1)
-      snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu>", variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng,
-               a.vec ? "true" : "false", variant >= 200 ? a.sig : 0u);
+      snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu, %s>",
+               variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng, a.vec ? "true" : "false",
+               variant >= 200 ? a.sig : 0u, a.ipl_radix ? "true" : "false");
     else if (a.dense_ng)
       snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu%s>", a.dense_ng, a.vec ? "true" : "false",
                a.dns_compact ? "true" : "false", variant >= 305 ? a.sig : 0u, variant == 306 ? ", true" : "");
@@ -2502,21 +2544,14 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     *kernel = name;
   }
   switch (variant) {
-    case 101: e = a.vec ? launch_k(dense_lds_kernel<1, true, 0>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<1, false, 0>, k, B, T, lds, st); break;
-    case 102: e = a.vec ? launch_k(dense_lds_kernel<2, true, 0>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<2, false, 0>, k, B, T, lds, st); break;
-    case 104: e = a.vec ? launch_k(dense_lds_kernel<4, true, 0>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<4, false, 0>, k, B, T, lds, st); break;
-    case 108: e = a.vec ? launch_k(dense_lds_kernel<8, true, 0>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<8, false, 0>, k, B, T, lds, st); break;
+    case 101: e = launch_lds<1, 0>(a, k, B, T, lds, st); break;
+    case 102: e = launch_lds<2, 0>(a, k, B, T, lds, st); break;
+    case 104: e = launch_lds<4, 0>(a, k, B, T, lds, st); break;
+    case 108: e = launch_lds<8, 0>(a, k, B, T, lds, st); break;
     // compile-time specialised signatures (tier1_signature): the common C2 shapes
-    case 200: e = a.vec ? launch_k(dense_lds_kernel<2, true, kSigFwdLdsDropSpill>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<2, false, kSigFwdLdsDropSpill>, k, B, T, lds, st); break;
-    case 201: e = a.vec ? launch_k(dense_lds_kernel<2, true, kSigFwdLdsDropLds>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<2, false, kSigFwdLdsDropLds>, k, B, T, lds, st); break;
-    case 202: e = a.vec ? launch_k(dense_lds_kernel<1, true, kSigFwdLds>, k, B, T, lds, st)
-                        : launch_k(dense_lds_kernel<1, false, kSigFwdLds>, k, B, T, lds, st); break;
+    case 200: e = launch_lds<2, kSigFwdLdsDropSpill>(a, k, B, T, lds, st); break;
+    case 201: e = launch_lds<2, kSigFwdLdsDropLds>(a, k, B, T, lds, st); break;
+    case 202: e = launch_lds<1, kSigFwdLds>(a, k, B, T, lds, st); break;
     case 1: e = a.vec ? launch_k(dense_local_kernel<1, true, false>, k, B, T, lds, st)
                       : launch_k(dense_local_kernel<1, false, false>, k, B, T, lds, st); break;
     case 2: e = a.vec ? launch_k(dense_local_kernel<2, true, false>, k, B, T, lds, st)

@@ -58,6 +58,8 @@ struct LaunchArgs {
   uint32_t sig;         // tier-1 group signature (kSig*), 0 when the plan has none
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  bool ipl_radix;                   // radix image (ipr_build): prefixes below, no nb / seed
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];
   // staged flushes (null: flush with global atomics)
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;

@@ -219,6 +219,9 @@ struct gpuagg_ctx {
   size_t ipl_all_alloc = 0;
   uint32_t ipl_all_nb = 0, ipl_all_seed = 0, ipl_all_bytes = 0;
   uint32_t ipl_nb = 0, ipl_seed = 0, ipl_bytes = 0;
+  // the tier-1 image is the radix form (ipr_build) when the pod IPs allow it
+  bool ipl_radix = false;
+  uint32_t ipl_npfx = 0, ipl_pfx[kIprMaxPfx] = {};
   uint64_t ip_version = 0;
 
   // dense counters
@@ -989,6 +992,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.ipl_nb = c->ipl_nb;
       a.ipl_seed = c->ipl_seed;
       a.ipl_bytes = c->ipl_bytes;
+      a.ipl_radix = c->ipl_radix;
+      a.ipl_npfx = c->ipl_npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) a.ipl_pfx[j] = c->ipl_pfx[j];
     }
   }
   // one 1024-thread workgroup per CU whenever LDS holds bins or spill counters: with
@@ -1707,17 +1713,23 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       if (!((kv.second >> 53) & 1))
         ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
     IplImage im;
-    if (ipl_build(ents, &im)) {
-      const uint32_t bytes = (uint32_t)im.bytes.size();
+    IprImage ir;
+    const bool radix = !(c->cfg.flags & GPUAGG_FLAG_LDS_CUCKOO) && ipr_build(ents, &ir);
+    if (radix || ipl_build(ents, &im)) {
+      const std::vector<uint8_t> &img = radix ? ir.bytes : im.bytes;
+      const uint32_t bytes = (uint32_t)img.size();
       if (bytes > c->ipl_alloc) {
         dev_free(c->d_ipl);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
       }
-      HIPCHK(c, hipMemcpy(c->d_ipl, im.bytes.data(), bytes, hipMemcpyHostToDevice));
-      c->ipl_nb = im.nb;
-      c->ipl_seed = im.seed;
+      HIPCHK(c, hipMemcpy(c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_radix = radix;
+      c->ipl_nb = radix ? 0 : im.nb;
+      c->ipl_seed = radix ? 0 : im.seed;
+      c->ipl_npfx = radix ? ir.npfx : 0;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) c->ipl_pfx[j] = radix ? ir.pfx[j] : kIprNoPfx;
       c->ipl_bytes = bytes;
     }
   }

@@ -17,6 +17,7 @@ MID = [
     ("c1-local", W.C1_LOCAL, False, 10_000, {}),
     ("c1-remote", W.C1_REMOTE, True, 10_000, {}),
     ("c2-local", W.LOCAL_FWD_DROP, False, 10_000, {}),
+    ("c2-local-lds-cuckoo", W.LOCAL_FWD_DROP, False, 10_000, {"flags": 64}),  # FLAG_LDS_CUCKOO
     ("c4-zipf", W.LOCAL_FWD_DROP, False, 10_000, {"zipf": 1.2}),
     ("c4-flows", W.LOCAL_FWD_DROP, False, 10_000, dict(W.CONFIGS["c4"]["gen"])),
     ("c4-flows-remote", W.C1_REMOTE, True, 10_000, dict(W.CONFIGS["c4"]["gen"])),
@@ -26,6 +27,8 @@ MID = [
 
 @pytest.mark.parametrize("cid,sp,remote,npods,gen", MID, ids=[m[0] for m in MID])
 def test_midsize_vs_c_port(gpu_device, cid, sp, remote, npods, gen):
+    gen = dict(gen)
+    flags = gen.pop("flags", 0)
     pods = W.make_pods(npods, seed=2)
     recs = W.gen_records(1_000_000, pods, seed=77, **gen)
     r = RefCPU(sp, pods.endpoints, remote, recs.dns)
@@ -33,7 +36,7 @@ def test_midsize_vs_c_port(gpu_device, cid, sp, remote, npods, gen):
     want = r.series()
     r.close()
     got = values_only(engine_series(recs, pods, sp, remote, gpu_device, host_fed=False, chunks=3,
-                                    sparse_capacity_log2=23))
+                                    sparse_capacity_log2=23, flags=flags))
     assert got == want, diff_series(got, want)
 
 
@@ -74,7 +77,7 @@ def test_host_fed_equals_device_and_chunking(gpu_device):
     assert a == b, diff_series(a, b)
 
 
-@pytest.mark.parametrize("flags", [0, 1], ids=["tier1", "no-lds-ip-table"])
+@pytest.mark.parametrize("flags", [0, 64, 1], ids=["tier1-radix", "tier1-cuckoo", "no-lds-ip-table"])
 def test_packed_field_overflow_exact(gpu_device, flags):
     """Packed LDS counters (u32 count:12|bytes:20 in tier-1, u64 count:20|bytes:44 in the
     other kernels and the fold windows) must carry exactly.  One hot pod pair, 60M
