@@ -417,6 +417,8 @@ class Cache:
             self.ip_to_ep_key[ip] = ep.key()
 
     def update_retina_svc(self, svc: RetinaSvc) -> None:
+        if not svc.ip:  # svc.GetPrimaryIP() error (cache.go:244-251)
+            raise ValueError("no primary IP for service " + svc.key())
         self._delete_by_ip(svc.ip, svc.key())
         self.ip_to_svc_key[svc.ip] = svc.key()
         self.svc_map[svc.key()] = svc
@@ -434,11 +436,15 @@ class Cache:
         for ip in ep.ips():
             self.ip_to_ep_key.pop(ip, None)
 
-    def delete_retina_svc(self, key: str) -> None:
+    def delete_retina_svc(self, key: str) -> None:  # deleteSvc (cache.go:347-371)
+        if key not in self.svc_map:
+            raise KeyError("service not found in cache: " + key)
         svc = self.svc_map.pop(key)
         self.ip_to_svc_key.pop(svc.ip, None)
 
-    def delete_retina_node(self, name: str) -> None:
+    def delete_retina_node(self, name: str) -> None:  # deleteNode (cache.go:381-397)
+        if name not in self.node_map:
+            raise KeyError("node not found in cache: " + name)
         node = self.node_map.pop(name)
         self.ip_to_node_name.pop(node.ip, None)
 
@@ -924,12 +930,47 @@ class DNSMetrics(BaseMetric):
         self.vec.add(labels, 1)
 
 
+def _same_set(a: Optional[List[str]], b: Optional[List[str]]) -> bool:
+    """utils.CompareStringSlice (pkg/utils/common.go:58-84): equal lengths and equal sets."""
+    a, b = list(a or []), list(b or [])
+    return len(a) == len(b) and set(a) == set(b)
+
+
+def options_equal(old: List[MetricsContextOptions], new: List[MetricsContextOptions]) -> bool:
+    """validations.MetricsContextOptionsCompare (validate_metricconfiguration.go:118-162)."""
+    if len(old) != len(new):
+        return False
+    om = {o.metric_name: o for o in old}
+    nm = {o.metric_name: o for o in new}
+    if len(om) != len(nm):
+        return False
+    for k, o in om.items():
+        n = nm.get(k)
+        if n is None or not _same_set(o.source_labels, n.source_labels) \
+                or not _same_set(o.destination_labels, n.destination_labels):
+            return False
+    return True
+
+
 class Module:
     """metrics.Module registry + per-flow dispatch (metrics_module.go:205-305)."""
 
     def __init__(self, remote_context: bool = False):
         self.ctx = REMOTE_CONTEXT if remote_context else LOCAL_CONTEXT
         self.registry: Dict[str, BaseMetric] = {}
+        self.current_spec: Optional[List[MetricsContextOptions]] = None
+
+    def reconcile_spec(self, context_options: List[MetricsContextOptions]) -> bool:
+        """Module.Reconcile (metrics_module.go:142-170): nothing happens when the spec equals
+        currentSpec, or -- with a currentSpec -- when MetricsContextOptionsCompare finds the
+        options equal (validate_metricconfiguration.go:118-162: same metric names, label
+        lists equal as sets); otherwise updateMetricsContexts rebuilds the registry.
+        Returns whether the registry was rebuilt."""
+        rebuild = self.current_spec is None or not options_equal(self.current_spec, context_options)
+        if rebuild:
+            self.reconcile(context_options)
+        self.current_spec = list(context_options)
+        return rebuild
 
     def reconcile(self, context_options: List[MetricsContextOptions]) -> None:
         self.registry = {}

@@ -221,6 +221,103 @@ mo("tcpflags", "local ctx src and dest opts with flow with all flags", o("flag",
    fl(F, source=EMPTY_EP, destination=EMPTY_EP, l4=tcp(ALL_FLAGS)), ["flag"] + LOC_ALL, 14,
    adv=True, local=True, src=S)
 
+# ---- pkg/controllers/cache/cache_test.go: the IP cache's update / delete / lookup rules ----
+def upd_ep(ns, name, ips, error=False):
+    return {"op": "update_endpoint", "namespace": ns, "name": name, "ips": ips, "error": error}
+
+
+def upd_svc(ns, name, ip, error=False):
+    return {"op": "update_service", "namespace": ns, "name": name, "ip": ip, "error": error}
+
+
+def upd_node(name, ip, error=False):
+    return {"op": "update_node", "name": name, "ip": ip, "error": error}
+
+
+def get(ip, kind=None, ns="", name=""):
+    return {"op": "get", "ip": ip, "want": None if kind is None else {"kind": kind, "namespace": ns, "name": name}}
+
+
+kat["cache_sequences"] = [
+    {"name": "TestCacheEndpoints", "src": "cache_test.go:31-96", "ops": [
+        upd_ep("ns1", "pod1", [], error=True),              # no IPs: ep.IPs() error
+        upd_ep("ns1", "pod1", ["1.2.3.4", "1.2.3.5"]),      # IPv4 + OtherIPv4s
+        get("1.2.3.4", "pod", "ns1", "pod1"),
+        get("1.2.3.5", "pod", "ns1", "pod1"),               # by secondary IP
+        {"op": "delete_endpoint", "namespace": "ns1", "name": "pod1", "error": False}]},
+    {"name": "TestCacheServices", "src": "cache_test.go:98-140", "ops": [
+        upd_svc("ns1", "svc1", None, error=True),           # GetPrimaryIP error
+        upd_svc("ns1", "svc1", "1.2.3.4"),
+        get("1.2.3.4", "svc", "ns1", "svc1"),
+        {"op": "delete_service", "namespace": "ns1", "name": "svc1", "error": False}]},
+    {"name": "TestCacheNodes", "src": "cache_test.go:142-173", "ops": [
+        upd_node("node1", "1.2.3.4"),
+        get("1.2.3.4", "node", "", "node1"),
+        {"op": "delete_node", "name": "node1", "error": False}]},
+    {"name": "TestAddPodSvcNodeSameIP", "src": "cache_test.go:175-225", "ops": [
+        upd_ep("ns1", "pod1", ["1.2.3.4"]),
+        upd_svc("ns1", "svc1", "1.2.3.4"),
+        get("1.2.3.4", "svc", "ns1", "svc1"),               # the service took the IP
+        upd_node("node1", "1.2.3.4"),
+        get("1.2.3.4", "node", "", "node1")]},              # then the node
+    {"name": "TestAddPodSvcNodeSameIPDiffNS", "src": "cache_test.go:227-278", "ops": [
+        upd_ep("ns1", "pod1", ["1.2.3.4"]),
+        upd_svc("ns2", "svc1", "1.2.3.4"),
+        get("1.2.3.4", "svc", "ns2", "svc1"),
+        upd_node("node1", "1.2.3.4"),
+        get("1.2.3.4", "node", "", "node1")]},
+    {"name": "TestAddPodDiffNs", "src": "cache_test.go:280-322", "ops": [
+        upd_ep("ns1", "pod1", ["1.2.3.4"]),
+        upd_ep("ns2", "pod1", ["1.2.3.4"]),
+        get("1.2.3.4", "pod", "ns2", "pod1")]},             # last writer wins
+    {"name": "TestFailDelete", "src": "cache_test.go:324-349", "ops": [
+        {"op": "delete_endpoint", "namespace": "ns1", "name": "pod1", "error": False},  # ignored
+        {"op": "delete_service", "namespace": "ns1", "name": "svc1", "error": True},
+        {"op": "delete_node", "name": "node1", "error": True}]},
+]
+
+# ---- pkg/module/metrics/metrics_module_test.go:369-615 (TestModule_Reconcile) ----
+# `prior`: the options the module's registry was built from (the test's pre-Init'ed metric
+# objects, remote context: the test's Module has no daemonConfig); `current_spec`: the
+# module's currentSpec (nil except in the no-op case).  The reference's Reconcile returns
+# nil in every case (its updateMetricsContexts logs invalid names instead of failing, so
+# the test's expectErr is permissive: `err != nil && !expectErr`); expect_no_calls: the
+# spec equals currentSpec, so nothing is re-registered and the registry is left alone.
+# AdditionalLabels is not read on the metrics path and is omitted.
+def mco(name, src=None, dst=None):
+    d = {"metric_name": name}
+    if src is not None:
+        d["source_labels"] = src
+    if dst is not None:
+        d["destination_labels"] = dst
+    return d
+
+
+_DC = mco("drop_count", ["ip"], ["pod"])
+_FC = mco("forward_count", ["ip"], ["pod"])
+kat["reconcile"] = [
+    {"name": "Registry is empty and no error", "src": "metrics_module_test.go:427-446",
+     "prior": [], "current_spec": None, "spec": [mco("drop_count", ["ip", "pod"], ["pod"])],
+     "reference_error": False, "expect_no_calls": False},
+    {"name": "Registry is not empty and no error", "src": "metrics_module_test.go:447-475",
+     "prior": [_DC, _FC], "current_spec": None,
+     "spec": [mco("drop_count", ["ip", "pod"], ["pod"]), mco("forward_count", ["ip", "pod"], ["pod"])],
+     "reference_error": False, "expect_no_calls": False},
+    {"name": "Registry is not empty and no error for bytes", "src": "metrics_module_test.go:476-514",
+     "prior": [_DC, mco("drop_bytes", ["ip"]), _FC, mco("forward_bytes", ["ip"])], "current_spec": None,
+     "spec": [mco("drop_count", ["ip", "pod"], ["pod"]), mco("drop_bytes", ["ip"]),
+              mco("forward_count", ["ip", "pod"], ["pod"]), mco("forward_bytes", ["ip"])],
+     "reference_error": False, "expect_no_calls": False},
+    {"name": "Registry is not empty and error for invalid name", "src": "metrics_module_test.go:515-553",
+     "prior": [_DC, mco("drop_bytes", ["ip"]), _FC, mco("forward_bytes", ["ip"])], "current_spec": None,
+     "spec": [mco("drop_hello", ["ip", "pod"], ["pod"]), mco("drop_bytes", ["ip"]),
+              mco("forward_count", ["ip", "pod"], ["pod"]), mco("forward_hi", ["ip"])],
+     "reference_error": False, "expect_no_calls": False},
+    {"name": "Expect no change for spec the same", "src": "metrics_module_test.go:554-587",
+     "prior": [_DC], "current_spec": [_DC], "spec": [_DC],
+     "reference_error": False, "expect_no_calls": True},
+]
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kat.json")
     with open(out, "w") as f:

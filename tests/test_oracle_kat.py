@@ -156,3 +156,73 @@ def test_decode_packet_roundtrip():
 def test_enum_names_unknown_numbers():
     assert O.enum_string(O.DROP_REASON_NAMES, 7) == "7"
     assert O.traffic_direction_string(3) == "3"
+
+
+def _obj_kind(obj):
+    if obj is None:
+        return None
+    if isinstance(obj, O.RetinaEndpoint):
+        return {"kind": "pod", "namespace": obj.namespace, "name": obj.name}
+    if isinstance(obj, O.RetinaSvc):
+        return {"kind": "svc", "namespace": obj.namespace, "name": obj.name}
+    return {"kind": "node", "namespace": "", "name": obj.name}
+
+
+def run_cache_ops(c, ops):
+    """Applies a cache_sequences op list to the oracle Cache; yields (op, error, got)."""
+    for op in ops:
+        kind = op["op"]
+        err, got = False, None
+        try:
+            if kind == "update_endpoint":
+                ips = op["ips"]
+                c.update_retina_endpoint(O.RetinaEndpoint(name=op["name"], namespace=op["namespace"],
+                                                          ipv4=ips[0] if ips else None, other_ipv4s=ips[1:]))
+            elif kind == "update_service":
+                c.update_retina_svc(O.RetinaSvc(op["name"], op["namespace"], op["ip"]))
+            elif kind == "update_node":
+                c.update_retina_node(O.RetinaNode(op["name"], op["ip"]))
+            elif kind == "delete_endpoint":
+                c.delete_retina_endpoint(op["namespace"] + "/" + op["name"])
+            elif kind == "delete_service":
+                c.delete_retina_svc(op["namespace"] + "/" + op["name"])
+            elif kind == "delete_node":
+                c.delete_retina_node(op["name"])
+            elif kind == "get":
+                got = _obj_kind(c.get_obj_by_ip(op["ip"]))
+        except (ValueError, KeyError):
+            err = True
+        yield op, err, got
+
+
+@pytest.mark.parametrize("case", KAT["cache_sequences"], ids=lambda c: c["name"])
+def test_cache_sequences(case):
+    """pkg/controllers/cache/cache_test.go: last writer wins across pods, services and
+    nodes; deleting a missing pod is ignored, a missing service or node is an error."""
+    for op, err, got in run_cache_ops(O.Cache(), case["ops"]):
+        if op["op"] == "get":
+            assert got == op["want"], (case["src"], op)
+        else:
+            assert err == op["error"], (case["src"], op)
+
+
+@pytest.mark.parametrize("case", KAT["reconcile"], ids=lambda c: c["name"])
+def test_reconcile_transitions(case):
+    """metrics_module_test.go TestModule_Reconcile: the registry is rebuilt unless the spec
+    equals the current one; invalid metric names register no vector."""
+    from oracle import records as R
+    m = O.Module(remote_context=True)  # the test's Module has no daemonConfig: remote context
+    if case["prior"]:
+        m.reconcile(R.spec_from_json(case["prior"]))
+    if case["current_spec"] is not None:
+        m.current_spec = R.spec_from_json(case["current_spec"])
+    before = dict(m.registry)
+    rebuilt = m.reconcile_spec(R.spec_from_json(case["spec"]))
+    assert rebuilt == (not case["expect_no_calls"])
+    if case["expect_no_calls"]:
+        assert m.registry == before
+    else:
+        assert set(m.registry) == {o["metric_name"] for o in case["spec"]}
+        vecs = {n: m.registry[n].vec for n in m.registry}
+        for n, v in vecs.items():  # Init creates a vector only for the exact *_count / *_bytes names
+            assert (v is not None) == (n in ("drop_count", "drop_bytes", "forward_count", "forward_bytes")), n
