@@ -108,6 +108,8 @@ type gpuAgg struct {
 	mu       sync.Mutex
 	devs     []*device
 	rawBuf   map[int][]byte // per kind: back-to-back raw records awaiting submit
+	rawShard []uint32       // per raw record of a submit: its device (gpuagg_shard_raw)
+	rawPart  [][]byte       // per device: its raw records of a submit
 	spec     *api.MetricsSpec
 	vecs     map[string]*prometheus.GaugeVec
 	ctrs     map[string]*prometheus.CounterVec
@@ -126,6 +128,7 @@ type gpuAgg struct {
 	enrichDst []int32
 
 	records chan Record
+	batches chan []Record // WriteBatch: one channel operation per slice of records
 	raw     chan rawSample
 	done    chan struct{} // closed when Start returns
 
@@ -199,7 +202,8 @@ func init() {
 // New is the registry.PluginFunc (registry.go:37).
 func New(cfg *kcfg.Config) registry.Plugin {
 	g := &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, channelDepth),
-		raw: make(chan rawSample, channelDepth), rawBuf: map[int][]byte{}}
+		raw: make(chan rawSample, channelDepth), rawBuf: map[int][]byte{},
+		batches: make(chan []Record, channelDepth/64+1)}
 	instanceMu.Lock()
 	instance = g
 	instanceMu.Unlock()
@@ -482,6 +486,20 @@ func (g *gpuAgg) Write(r Record) {
 	}
 }
 
+// WriteBatch hands over a slice of decoded records with one channel operation (a
+// producer draining several perf records per wake-up); the slice is owned by the plugin
+// afterwards.  A full channel drops the whole slice and counts every record.
+func (g *gpuAgg) WriteBatch(rs []Record) {
+	if len(rs) == 0 {
+		return
+	}
+	select {
+	case g.batches <- rs:
+	default:
+		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Add(float64(len(rs)))
+	}
+}
+
 // WriteRaw takes one perf RawSample of the given kind; a sample of the wrong size is
 // refused like binary.Read's size mismatch (dropreason_linux.go:347-352).
 func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
@@ -496,9 +514,10 @@ func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
 	return nil
 }
 
-// shardOf is retina_amd/dist.py shard_of: fmix64 of the direction-free 5-tuple (the
+// shardOf is retina_amd/dist.py shard_of and the library's gpuagg_shard_columns (whose
+// agreement is tests/test_cpu_shard.py): fmix64 of the direction-free 5-tuple (the
 // (ip, port) ends in order, so a request and its reply meet on one device for the
-// latency join), mod the devices.
+// latency join), mod the devices.  Restated in Go so the per-record path needs no cgo call.
 func shardOf(r *Record, n int) int {
 	if n == 1 {
 		return 0
@@ -572,10 +591,44 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		if err := g.commitLocked(); err != nil {
 			return err
 		}
-		// raw records are not sharded by 5-tuple before decode: they go to device 0
-		err := check(devs[0].ctx, C.gpuagg_submit_raw(devs[0].ctx, C.int(kind), unsafe.Pointer(&buf[0]),
-			C.size_t(len(buf)/rawSize[kind])), "gpuagg_submit_raw")
-		g.rawBuf[kind] = buf[:0]
+		sz := rawSize[kind]
+		n := len(buf) / sz
+		defer func() { g.rawBuf[kind] = buf[:0] }()
+		if len(devs) == 1 {
+			return check(devs[0].ctx, C.gpuagg_submit_raw(devs[0].ctx, C.int(kind), unsafe.Pointer(&buf[0]),
+				C.size_t(n)), "gpuagg_submit_raw")
+		}
+		// shard by the 5-tuple read at the records' fixed offsets (conntrack.c:34-49,
+		// drop_reason.c:39-54) -- the same function as shardOf and dist.shard_of, so a
+		// flow's raw and decoded records meet on one device -- then one submit per device
+		if cap(g.rawShard) < n {
+			g.rawShard = make([]uint32, n)
+		}
+		shards := g.rawShard[:n]
+		if err := check(devs[0].ctx, C.gpuagg_shard_raw(C.int(kind), unsafe.Pointer(&buf[0]), C.size_t(n),
+			C.uint32_t(len(devs)), (*C.uint32_t)(unsafe.Pointer(&shards[0]))), "gpuagg_shard_raw"); err != nil {
+			return err
+		}
+		if len(g.rawPart) != len(devs) {
+			g.rawPart = make([][]byte, len(devs))
+		}
+		for i := range g.rawPart {
+			g.rawPart[i] = g.rawPart[i][:0]
+		}
+		for i, d := range shards {
+			g.rawPart[d] = append(g.rawPart[d], buf[i*sz:(i+1)*sz]...)
+		}
+		var err error
+		for i, d := range devs {
+			part := g.rawPart[i]
+			if len(part) == 0 {
+				continue
+			}
+			if e := check(d.ctx, C.gpuagg_submit_raw(d.ctx, C.int(kind), unsafe.Pointer(&part[0]),
+				C.size_t(len(part)/sz)), "gpuagg_submit_raw"); e != nil && err == nil {
+				err = e
+			}
+		}
 		return err
 	}
 	submitAll := func() error {
@@ -592,21 +645,29 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		}
 		return err
 	}
+	// put copies one decoded record into its device's pinned batch (device by shardOf)
+	put := func(r *Record) {
+		d := devs[shardOf(r, len(devs))]
+		i := d.n
+		d.cols[0][i], d.cols[1][i], d.cols[2][i], d.cols[3][i], d.cols[4][i], d.cols[5][i], d.cols[6][i] =
+			r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID, r.TcpID
+		d.times[i] = r.TimeNs
+		d.n++
+		if d.n == batchCapacity {
+			if err := submit(d); err != nil {
+				g.l.Error("submit failed", zap.Error(err))
+			}
+		}
+	}
 	for {
 		select {
 		case <-ctx.Done():
 			return submitAll()
 		case r := <-g.records:
-			d := devs[shardOf(&r, len(devs))]
-			i := d.n
-			d.cols[0][i], d.cols[1][i], d.cols[2][i], d.cols[3][i], d.cols[4][i], d.cols[5][i], d.cols[6][i] =
-				r.SrcIP, r.DstIP, r.Bytes, r.Meta, r.Ports, r.DNSID, r.TcpID
-			d.times[i] = r.TimeNs
-			d.n++
-			if d.n == batchCapacity {
-				if err := submit(d); err != nil {
-					g.l.Error("submit failed", zap.Error(err))
-				}
+			put(&r)
+		case rs := <-g.batches:
+			for i := range rs {
+				put(&rs[i])
 			}
 		case s := <-g.raw:
 			g.rawBuf[s.kind] = append(g.rawBuf[s.kind], s.b...)

@@ -252,6 +252,16 @@ int gpuagg_submit_raw_device(gpuagg_ctx *ctx, int kind, const void *dev_raw, siz
  * returns once host_raw may be reused (the packetparser/dropreason reader's batch). */
 int gpuagg_submit_raw(gpuagg_ctx *ctx, int kind, const void *host_raw, size_t n);
 
+/* Multi-GPU sharding on the host (retina_amd/dist.py shard_of): the device
+ * of each record, fmix64 of the direction-free 5-tuple (the two (ip, port) ends ordered,
+ * so a request and its reply meet on one device for the latency join) mod n_shards.
+ * gpuagg_shard_raw reads the fields at their fixed offsets of the raw perf records
+ * (GPUAGG_RAW_*: ports byte-swapped as the decode does), gpuagg_shard_columns decoded
+ * columns (ports may be NULL: port 0).  Host memory; no ctx or device needed. */
+int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uint32_t *shard_out);
+int gpuagg_shard_columns(const uint32_t *src_ip, const uint32_t *dst_ip, const uint32_t *ports,
+                         const uint32_t *meta, size_t n, uint32_t n_shards, uint32_t *shard_out);
+
 /* Wait for every submitted batch. */
 int gpuagg_sync(gpuagg_ctx *ctx);
 

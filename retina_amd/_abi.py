@@ -132,6 +132,8 @@ SIGNATURES = [
     ("gpuagg_sketch_kernel_name", C.c_char_p, [C.c_void_p]),
     ("gpuagg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("gpuagg_build_id", C.c_char_p, []),
+    ("gpuagg_shard_raw", C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_uint32, u32p]),
+    ("gpuagg_shard_columns", C.c_int, [u32p, u32p, u32p, u32p, C.c_size_t, C.c_uint32, u32p]),
     ("gpuagg_cache_update_endpoint", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
                                                u32p, C.c_size_t]),
     ("gpuagg_cache_delete_endpoint", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),

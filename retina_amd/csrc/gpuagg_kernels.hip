@@ -85,10 +85,7 @@ static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp"
 // memory-side atomics serialised on one table slot; the cache is added to the table
 // once per workgroup at the end (hot_flush).
 __device__ __forceinline__ bool hot_add(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
-                                        uint64_t b) {
-  // only keys that occur more than once in the wave (the de-dup count) claim an entry:
-  // under skew those are the hot ones; uniform keys (C1) then cost two tag reads
-  const bool may_claim = c > 1;
+                                        uint64_t b, bool may_claim) {
   const uint32_t h = (uint32_t)key_hash(k0, k1, k2);
 #pragma unroll
   for (uint32_t q = 0; q < 2; ++q) {
@@ -478,6 +475,15 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
     else sparse_add_compact(s, key, 1);  // full list: in place (exact)
     return;
   }
+  if (s.lists) {
+    // wide keys through the segment lists: no wave de-duplication (its leader loop costs
+    // one round per distinct key of a hash-bucket collision -- ~30 rounds per insert under
+    // C4's Zipf flows, the whole kernel's time).  Lanes with the same key meet in the LDS
+    // hot-key cache (any key may claim a free entry: the frequent ones arrive first) or
+    // append separately and are summed by the fold.
+    if (valid && !(s.hot && hot_add(s, k0, k1, k2, 1, b, true))) wide_append(s, k0, k1, k2, 1, b);
+    return;
+  }
   const uint64_t vm = __ballot(valid);
   if (!vm) return;
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -509,10 +515,9 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
       }
     }
   }
-  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b))) {
-    if (s.lists) wide_append(s, k0, k1, k2, c, b);
-    else sparse_add(s, k0, k1, k2, c, b);
-  }
+  // only keys that occur more than once in the wave (the de-dup count) claim a hot-key
+  // entry: under skew those are the hot ones; uniform keys (C1) then cost two tag reads
+  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b, c > 1))) sparse_add(s, k0, k1, k2, c, b);
 }
 
 // One record through every metric group.  Converged: every lane of the wave runs it

@@ -2829,6 +2829,42 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
 void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 const char *gpuagg_build_id(void) { return GPUAGG_BUILD_ID; }
+
+// dist.shard_of: h = fmix64(lo ^ fmix64(hi ^ proto << 48 ^ seed)) with lo <= hi the two
+// (ip << 16 | port) ends; shard = h mod n.
+static inline uint32_t shard_one(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto, uint32_t n) {
+  const uint64_t a = ((uint64_t)src << 16) | (ports & 0xFFFFu), b = ((uint64_t)dst << 16) | (ports >> 16);
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  const uint64_t h = fmix64(lo ^ fmix64(hi ^ ((uint64_t)(proto & 0xFFu) << 48) ^ 0x1F2E3D4C5B6A7988ULL));
+  return (uint32_t)(h % n);
+}
+
+int gpuagg_shard_columns(const uint32_t *src, const uint32_t *dst, const uint32_t *ports, const uint32_t *meta,
+                         size_t n, uint32_t n_shards, uint32_t *out) {
+  if (!n) return GPUAGG_OK;
+  if (!src || !dst || !meta || !out || !n_shards) return GPUAGG_EINVAL;
+  for (size_t i = 0; i < n; ++i) out[i] = shard_one(src[i], dst[i], ports ? ports[i] : 0u, meta[i], n_shards);
+  return GPUAGG_OK;
+}
+
+int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uint32_t *out) {
+  if (!n) return GPUAGG_OK;
+  if (!raw || !out || !n_shards || (kind != GPUAGG_RAW_PACKET && kind != GPUAGG_RAW_DROP)) return GPUAGG_EINVAL;
+  const uint8_t *p = (const uint8_t *)raw;
+  auto u32 = [](const uint8_t *q) { uint32_t v; memcpy(&v, q, 4); return v; };
+  auto bswap16 = [](uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); };
+  // field offsets: conntrack.c:34-49 (src 12, dst 16, ports 20, proto 42) and
+  // drop_reason.c:39-54 (src 0, dst 4, ports 8, proto 22); ports as HostToNetShort decodes them
+  const size_t sz = kind == GPUAGG_RAW_PACKET ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
+  const size_t o_ip = kind == GPUAGG_RAW_PACKET ? 12 : 0, o_port = o_ip + 8;
+  const size_t o_proto = kind == GPUAGG_RAW_PACKET ? 42 : 22;
+  for (size_t i = 0; i < n; ++i, p += sz) {
+    const uint32_t w = u32(p + o_port);
+    out[i] = shard_one(u32(p + o_ip), u32(p + o_ip + 4), bswap16(w & 0xFFFFu) | (bswap16(w >> 16) << 16), p[o_proto],
+                       n_shards);
+  }
+  return GPUAGG_OK;
+}
 const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }
 const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *c) { return c ? c->sketch_kernel_name.c_str() : ""; }
 

@@ -1,0 +1,68 @@
+"""The library's host sharding (gpuagg_shard_raw / gpuagg_shard_columns, used by the Go
+plugin to spread raw perf records and decoded records over the node's devices) equals
+retina_amd/dist.py shard_of on the decoded columns: one function on every side."""
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import decode as D
+from retina_amd import dist
+from retina_amd import workloads as W
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from retina_amd import _abi, build
+    build.build()
+    return _abi.load()
+
+
+def _u32p(a):
+    from retina_amd import _abi
+    return a.ctypes.data_as(_abi.u32p)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_raw_and_columns_match_dist(lib, world):
+    from retina_amd import _abi
+    pods = W.make_pods(500, seed=3)
+    for kind, raw, dec in ((_abi.RAW_PACKET, W.gen_raw_packets(20_000, pods, seed=4, odd_frac=0.05), D.decode_packets),
+                           (_abi.RAW_DROP, W.gen_raw_drops(20_000, pods, seed=5), D.decode_drops)):
+        b, _ = dec(raw)
+        n = len(b.src_ip)
+        want = dist.shard_of(b.src_ip, b.dst_ip, b.ports, b.meta, world)
+        got = np.zeros(n, np.uint32)
+        assert lib.gpuagg_shard_raw(kind, raw.ctypes.data_as(C.c_void_p), n, world, _u32p(got)) == 0
+        assert np.array_equal(got, want), kind
+        cols = [np.ascontiguousarray(x, np.uint32) for x in (b.src_ip, b.dst_ip, b.ports, b.meta)]
+        got2 = np.zeros(n, np.uint32)
+        assert lib.gpuagg_shard_columns(*[_u32p(x) for x in cols], n, world, _u32p(got2)) == 0
+        assert np.array_equal(got2, want)
+        assert len(set(got.tolist())) == world  # every shard gets records
+
+
+def test_mirrored_tuple_same_shard(lib):
+    """A request and its mirrored reply land on one shard (the latency join needs both)."""
+    rng = np.random.default_rng(9)
+    n = 5000
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(0, 65536, n, dtype=np.uint32)
+    dp = rng.integers(0, 65536, n, dtype=np.uint32)
+    meta = np.full(n, 6, np.uint32)
+    a, b = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    fwd = [src, dst, (sp | (dp << 16)).astype(np.uint32), meta]
+    rev = [dst, src, (dp | (sp << 16)).astype(np.uint32), meta]
+    assert lib.gpuagg_shard_columns(*[_u32p(x) for x in fwd], n, 8, _u32p(a)) == 0
+    assert lib.gpuagg_shard_columns(*[_u32p(x) for x in rev], n, 8, _u32p(b)) == 0
+    assert np.array_equal(a, b)
+
+
+def test_bad_arguments(lib):
+    from retina_amd import _abi
+    out = np.zeros(1, np.uint32)
+    raw = np.zeros(72, np.uint8)
+    assert lib.gpuagg_shard_raw(99, raw.ctypes.data_as(C.c_void_p), 1, 2, _u32p(out)) == _abi.EINVAL
+    assert lib.gpuagg_shard_raw(_abi.RAW_PACKET, raw.ctypes.data_as(C.c_void_p), 1, 0, _u32p(out)) == _abi.EINVAL
