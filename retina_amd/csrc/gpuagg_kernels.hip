@@ -133,9 +133,9 @@ struct KArgs {
   DevSparse s;
   DevSketch sk;
   uint32_t lds_bins;  // L: dense bins privatised in LDS (u64 words; tier-1: u32 words)
-  // spill lists: per workgroup, one list per fold window of 2^kFoldWindowShift bins
+  // spill lists: per workgroup, one list per fold window of 2^win_shift bins
   // starting at dense bin `spill_lo`; list (b, w) at spill + (b*nwin + w)*spill_cap;
-  // entries u32 = bin offset in the window | bytes << kFoldWindowShift (spill_entry)
+  // entries u32 = bin offset in the window | bytes << win_shift (DenseSink::entry)
   uint32_t spill_cap;
   uint32_t nwin, win_shift, spill_lo;
   uint32_t *spill;  // or null: bins >= lds_bins use global atomics
@@ -345,13 +345,14 @@ struct DenseSink {
   DevDense d;
   uint32_t wbits;           // bits of a window index (nwin <= 2^wbits)
 
-  __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> kFoldWindowShift; }
+  __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> win_shift; }
   // 4-byte entry: the bin's offset in its window and the bytes; bytes that do not fit
-  // the field are added to the global counter here (rare) and the entry carries 0
+  // the field (2^(32 - win_shift)) are added to the global counter here (rare) and the
+  // entry carries 0
   __device__ __forceinline__ uint32_t entry(uint32_t bin, uint32_t nbytes) const {
-    const bool fits = nbytes < kSpillByteLimit;
+    const bool fits = (nbytes >> (32u - win_shift)) == 0u;
     if (!fits) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
-    return ((bin - spill_lo) & (kFoldWindowBins - 1)) | ((fits ? nbytes : 0u) << kFoldWindowShift);
+    return ((bin - spill_lo) & ((1u << win_shift) - 1u)) | ((fits ? nbytes : 0u) << win_shift);
   }
   // store one reserved spill entry (pos from the window counter); full list -> global
   __device__ __forceinline__ void spill_put(uint32_t bin, uint32_t w, uint32_t pos, uint32_t nbytes) const {
@@ -2137,20 +2138,57 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   return hipSuccess;
 }
 
+// Sums the tier-1 workgroups' staged u32 bins: part `y` of `ny` takes 1/ny of the
+// copies, so each bin gets ny global atomics instead of one per workgroup.
+__device__ __forceinline__ void stage_reduce_a(const uint32_t *stage, uint32_t ncopies, uint32_t stride,
+                                               uint32_t L4, const Plan &p, const DevDense &d, uint32_t bx,
+                                               uint32_t y, uint32_t ny) {
+  const uint32_t bin = bx * blockDim.x + threadIdx.x;
+  if (bin >= L4) return;
+  bool packed = false;
+  for (int g = 0; g < p.ngroups; ++g)
+    if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
+      packed = p.g[g].family <= FAM_DROP;
+  const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * y) / ny);
+  const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (y + 1)) / ny);
+  unsigned long long cnt = 0, byt = 0;
+#pragma unroll 8  // 8 independent copy loads in flight per lane
+  for (uint32_t c = c0; c < c1; ++c) {
+    const uint32_t w = stage[(size_t)c * stride + bin];
+    cnt += packed ? (w >> kL4CountShift) : w;
+    byt += packed ? (w & kL4BytesMask) : 0u;
+  }
+  if (cnt) atomicAdd(&d.cnt[bin], cnt);
+  if (byt) atomicAdd(&d.byt[bin], byt);
+}
+
 // Folds the spill lists into dense counters, one LDS window of bins per workgroup.
 // List (A-workgroup l, window w) holds only window w's updates, so every entry is read
 // once.  Workgroup b folds window b % nwin over partition b / nwin of the lists; with
 // W = 8192 bins (64 KB of LDS) two workgroups fit a CU, and the runtime sizes the grid
 // to 2 x CUs so the fold runs in a single wave of the chip.
+//
+// One launch ends the step: blocks [nfold, gridDim.x) sum the tier-1 workgroups' LDS bin
+// copies (stage_a, disjoint bins), and a window's partition partials are summed in the
+// same launch by the window's last-arriving partition (agent-scope release -> ticket ->
+// acquire, cdna_hip_programming.md section 5 "in-launch split-K reduction"): the partials
+// are nparts x 2^win_shift words (24 KiB at C2), so the serial combine costs less than
+// the extra launch it replaces.
 __global__ __launch_bounds__(1024) void spill_window_kernel(
     const uint32_t *spill, const uint32_t *spill_count, uint32_t n_lists,
     uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d,
-    unsigned long long *stage) {
+    unsigned long long *stage, uint32_t *ticket, uint32_t nfold, const uint32_t *stage_a, uint32_t ncopies,
+    uint32_t stride, uint32_t L4, uint32_t na_x, uint32_t ny, Plan p) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
+  if (blockIdx.x >= nfold) {  // the tier-1 copies (independent of the fold)
+    const uint32_t ba = blockIdx.x - nfold;
+    stage_reduce_a(stage_a, ncopies, stride, L4, p, d, ba % na_x, ba / na_x, ny);
+    return;
+  }
   const uint32_t b = blockIdx.x;
   const uint32_t w = b % nwin;
   const uint32_t part = b / nwin;
-  const uint32_t nparts = gridDim.x / nwin;
+  const uint32_t nparts = nfold / nwin;
   const uint64_t lo = (uint64_t)lo0 + (uint64_t)w * W;
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
@@ -2161,9 +2199,9 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   uint64_t total = 0;
   for (uint32_t l = part; l < n_lists; l += nparts) total += spill_count[(size_t)l * nwin + w];
   const bool fast = total < (1ULL << 20);
-  const uint32_t off_mask = kFoldWindowBins - 1;
+  const uint32_t off_mask = W - 1, wshift = 31u - (uint32_t)__builtin_clz(W);
   auto add = [&](uint32_t x) {
-    const uint32_t off = x & off_mask, nb = x >> kFoldWindowShift;
+    const uint32_t off = x & off_mask, nb = x >> wshift;
     if (fast) atomicAdd(&win[off], kLdsCountOne | nb);
     else lds_add64_exact(&win[off], (uint32_t)lo + off, nb, d);
   };
@@ -2217,9 +2255,38 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
   }  // long lists
   __syncthreads();
-  if (stage) {  // staged: this window partial, whole, for stage_reduce_kernel
+  if (stage) {  // staged: this window partial, whole; the window's last partition sums them
     uint4 *dst = (uint4 *)(stage + ((size_t)b * W));
     for (uint32_t i = threadIdx.x; i < W / 2; i += blockDim.x) dst[i] = ((const uint4 *)win)[i];
+    if (!ticket) return;  // summed by stage_reduce_kernel
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(&ticket[w], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      win[0] = t == nparts - 1 ? 1ULL : 0ULL;  // "last" through the window's LDS
+    }
+    __syncthreads();
+    const bool last = win[0] != 0ULL;
+    if (!last) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ticket[w] = 0u;  // ready for the next launch (zeroed at allocation)
+    }
+    __syncthreads();
+    // this window's bins: only this workgroup writes them in this launch (plain RMW)
+    for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
+      unsigned long long cnt = 0, byt = 0;
+      for (uint32_t q = 0; q < nparts; ++q) {
+        const unsigned long long v = stage[(size_t)(q * nwin + w) * W + i];
+        cnt += v >> kLdsCountShift;
+        byt += v & kLdsBytesMask;
+      }
+      if (cnt) d.cnt[lo + i] += cnt;
+      if (byt) d.byt[lo + i] += byt;
+    }
     return;
   }
   for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
@@ -2230,30 +2297,6 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
       if (by) atomicAdd(&d.byt[lo + i], by);
     }
   }
-}
-
-// Sums the tier-1 workgroups' staged u32 bins: part `y` of `ny` takes 1/ny of the
-// copies, so each bin gets ny global atomics instead of one per workgroup.
-__device__ __forceinline__ void stage_reduce_a(const uint32_t *stage, uint32_t ncopies, uint32_t stride,
-                                               uint32_t L4, const Plan &p, const DevDense &d, uint32_t bx,
-                                               uint32_t y, uint32_t ny) {
-  const uint32_t bin = bx * 256u + threadIdx.x;
-  if (bin >= L4) return;
-  bool packed = false;
-  for (int g = 0; g < p.ngroups; ++g)
-    if (bin >= p.g[g].dense_base && bin < p.g[g].dense_base + p.g[g].nbins)
-      packed = p.g[g].family <= FAM_DROP;
-  const uint32_t c0 = (uint32_t)(((uint64_t)ncopies * y) / ny);
-  const uint32_t c1 = (uint32_t)(((uint64_t)ncopies * (y + 1)) / ny);
-  unsigned long long cnt = 0, byt = 0;
-#pragma unroll 8  // 8 independent copy loads in flight per lane
-  for (uint32_t c = c0; c < c1; ++c) {
-    const uint32_t w = stage[(size_t)c * stride + bin];
-    cnt += packed ? (w >> kL4CountShift) : w;
-    byt += packed ? (w & kL4BytesMask) : 0u;
-  }
-  if (cnt) atomicAdd(&d.cnt[bin], cnt);
-  if (byt) atomicAdd(&d.byt[bin], byt);
 }
 
 // Sums the fold partials of every partition of a window (layout of spill_window_kernel).
@@ -2636,10 +2679,17 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
+  // with tickets: one launch (fold + partial sums + the tier-1 copies in extra blocks)
+  const bool one = a.stage_b && a.fold_ticket;
+  const uint32_t fa_x = (a.lds_bins + 1023) / 1024, fa_y = 8;
+  const uint32_t na = one && a.stage_a ? fa_x * fa_y : 0u;
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks + na), dim3(1024), (size_t)8 * W, st,
                      (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b);
+                     a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b,
+                     one ? a.fold_ticket : nullptr, a.win_blocks, a.stage_a, a.blocks, a.stage_a_stride,
+                     a.lds_bins, fa_x, fa_y, a.plan);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (one) return hipSuccess;
   return reduce(a.stage_b != nullptr);
 }
 

@@ -64,6 +64,7 @@ struct LaunchArgs {
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;
   uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
+  uint32_t *fold_ticket;    // [kMaxSpillWindows] zeroed: partials summed in the fold launch
   // compact group-by keys bucketed per table segment (null: inserted in place)
   uint64_t *sp_lists;       // [blocks][sp_nwin][sp_cap] keys
   uint32_t *sp_counts;      // [blocks][sp_nwin]

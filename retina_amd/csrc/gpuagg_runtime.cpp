@@ -291,6 +291,7 @@ struct gpuagg_ctx {
   hipEvent_t enrich_done = nullptr;
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
+  uint32_t *d_fold_ticket = nullptr;  // spill_window_kernel's per-window tickets
   // raw perf-record decode (gpuagg_decode.hip)
   uint64_t *d_decode_oor = nullptr;  // out-of-range field counter
   std::vector<std::array<hipEvent_t, 2>> pending_decode;  // decode start, end
@@ -1031,20 +1032,26 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     // insert per record, hashed evenly: budget / nwin per list + 25 % + 64; a full list
     // inserts in place, exact).
     struct Geom {
-      uint32_t nwin = 0, spill_cap = 0, win_blocks = 0, sp_nwin = 0, sp_cap = 0;
+      uint32_t nwin = 0, spill_cap = 0, win_blocks = 0, sp_nwin = 0, sp_cap = 0, win_shift = 0;
       bool operator==(const Geom &o) const {
         return nwin == o.nwin && spill_cap == o.spill_cap && win_blocks == o.win_blocks && sp_nwin == o.sp_nwin &&
-               sp_cap == o.sp_cap;
+               sp_cap == o.sp_cap && win_shift == o.win_shift;
       }
     };
     auto geom = [&](uint64_t budget) {
       Geom g;
       if (c->dense_len > a.lds_bins) {
         const uint64_t rem = c->dense_len - a.lds_bins;
-        const uint32_t nwin = (uint32_t)((rem + kFoldWindowBins - 1) / kFoldWindowBins);
+        // smallest window (fewest fold partitions per window, so fewest partial copies)
+        // that keeps the windows within the kernels' LDS counters; staged C5 rings need the
+        // windows unchanged (kStage sizes them per window)
+        uint32_t shift = kFoldWindowShiftMin;
+        while (shift < kFoldWindowShift && ((rem + (1ull << shift) - 1) >> shift) > kMaxSpillWindows) ++shift;
+        const uint32_t nwin = (uint32_t)((rem + (1ull << shift) - 1) >> shift);
         const uint64_t cap = ((2 * budget / nwin + 4096) + 3) & ~3ULL;
         if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
           g.nwin = nwin;
+          g.win_shift = shift;
           g.spill_cap = (uint32_t)cap;
           g.win_blocks = nwin * std::max<uint32_t>(1u, 2u * c->n_cu / nwin);  // one wave of 2 per CU
         }
@@ -1066,6 +1073,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         g.nwin = x.nwin;
         g.spill_cap = x.spill_cap;
         g.win_blocks = x.win_blocks;
+        g.win_shift = x.win_shift;
       }
       if (x.sp_lists) {
         g.sp_nwin = x.sp_nwin;
@@ -1108,12 +1116,17 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.spill_count = c->d_spill_count;
       a.nwin = g.nwin;
       a.spill_lo = a.lds_bins;
-      a.win_shift = kFoldWindowShift;
+      a.win_shift = g.win_shift;
       a.win_blocks = g.win_blocks;
       // fold partials are stored (not atomically added) and summed by a reduce pass
       const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
       if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
       a.stage_b = c->d_stage_b;
+      if (!c->d_fold_ticket) {  // per-window tickets, reset by each window's last partition
+        if ((rc = dev_alloc(c, &c->d_fold_ticket, kMaxSpillWindows))) return rc;
+        HIPCHK(c, hipMemsetAsync(c->d_fold_ticket, 0, kMaxSpillWindows * 4, c->stream));
+      }
+      a.fold_ticket = c->d_fold_ticket;
     }
     a.sp_lists = nullptr;
     a.sp_counts = nullptr;
@@ -1297,6 +1310,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c->d_stage_b);
   dev_free(c->d_sk_lists);
   dev_free(c->d_sk_counts);
+  dev_free(c->d_fold_ticket);
   dev_free(c->d_sp_lists);
   dev_free(c->d_sp_counts);
   dev_free(c->d_hll_lists);
