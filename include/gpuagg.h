@@ -73,6 +73,9 @@ typedef struct gpuagg_config {
                                           once per gpuagg_sync or state read (diagnostics) */
 #define GPUAGG_FLAG_LDS_CUCKOO 64u     /* tier-1 LDS IP image as the cuckoo table even when the radix
                                           image fits (diagnostics) */
+#define GPUAGG_FLAG_CPU_BACKEND 128u  /* run on host threads and host memory, no device (nodes without
+                                          a gfx950 GPU): the same plan, ABI and results; "device"
+                                          pointers of this ctx's calls are host pointers          */
 #define GPUAGG_FLAG_NO_WIDE_LISTS 32u  /* 192-bit group-by keys straight into the table with memory-side
                                           atomics, not through per-segment lists (diagnostics) */
 
@@ -456,6 +459,7 @@ typedef struct gpuagg_stats {
 #define GPUAGG_KERNEL_GENERIC 1u       /* aggregate_kernel: any plan                  */
 #define GPUAGG_KERNEL_DENSE_HBM_IP 2u  /* dense_local_kernel: IP table in HBM         */
 #define GPUAGG_KERNEL_DENSE_LDS_IP 3u  /* dense_lds_kernel: IP table + u32 bins in LDS */
+#define GPUAGG_KERNEL_CPU 4u           /* the CPU backend's host threads               */
 
 int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
 /* Enables HIP-event timing of the aggregation kernel on the ctx's stream. */

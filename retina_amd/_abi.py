@@ -32,7 +32,8 @@ FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table
 FLAG_LDS_CUCKOO = 64  # diagnostics: cuckoo LDS IP image even when the radix image fits
-FLAG_NO_WIDE_LISTS = 32  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
+FLAG_NO_WIDE_LISTS = 32
+FLAG_CPU_BACKEND = 128  # host threads and host memory instead of a device (GPUAGG_FLAG_CPU_BACKEND)  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
 
 
 class MetricOptions(C.Structure):
@@ -87,7 +88,7 @@ RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
 RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32}
 
 
-KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel"}
+KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel", 4: "cpu"}
 
 
 # (name, restype, argtypes) for every entry point declared in include/gpuagg.h

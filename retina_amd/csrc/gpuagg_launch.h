@@ -2,7 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <string>
+#include <vector>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -212,5 +214,42 @@ hipError_t launch_merge_max_u8(uint8_t *dst, const uint8_t *src, size_t n, hipSt
 hipError_t launch_sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t out_cap,
                                 uint64_t *counter, hipStream_t st);
 hipError_t launch_sparse_import(const SparseView &v, const uint64_t *in, size_t n, hipStream_t st);
+
+// ---- CPU backend (gpuagg_cpu.cpp): the same launches on host memory and threads --------
+namespace cpu {
+class Engine {
+ public:
+  explicit Engine(unsigned threads);
+  ~Engine();
+  // aggregate_kernel's per-record work (dense and group-by updates; no lists, no LDS):
+  // into per-thread accumulators, added to the ctx's arrays / table by flush()
+  void aggregate(const LaunchArgs &a);
+  void flush();
+  void drop();  // discards what flush() would add (the state is being reset)
+  bool pending() const { return pending_; }
+  void sketch(const SketchArgs &s);             // count-min + HLL (relaxed atomics)
+  uint64_t decode(const DecodeArgs &a);         // returns the out-of-range rows
+  void enrich(const EnrichArgs &a);
+  void hubble(const HubbleArgs &a);
+  void latency(const LatArgs &a, uint32_t enabled);  // state words in a.state (host)
+  void latency_reset();
+  unsigned threads() const { return threads_; }
+
+ private:
+  struct Part;
+  unsigned threads_;
+  std::vector<std::unique_ptr<Part>> parts_;
+  bool pending_ = false;
+  uint64_t dense_len_ = 0;
+  uint64_t *dense_cnt_ = nullptr, *dense_byt_ = nullptr;
+  SparseView sparse_{};
+  std::vector<LatEvent> carry_;  // requests pending across batches
+};
+void sparse_init(const SparseView &v, size_t slots);
+size_t sparse_export(const SparseView &v, size_t slots, uint64_t *out, size_t cap);  // returns entries
+void sparse_import(const SparseView &v, const uint64_t *in, size_t n);
+void zero_slots(uint64_t *cnt, uint64_t *byt, uint8_t *hll, uint32_t hll_p, const uint32_t *dead, uint32_t ndead,
+                const Plan &p);
+}  // namespace cpu
 
 }  // namespace gpuagg

@@ -19,8 +19,11 @@
 #include <array>
 #include <cmath>
 #include <cstdarg>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <set>
 #include <memory>
@@ -146,6 +149,10 @@ struct gpuagg_result {
 struct gpuagg_ctx {
   gpuagg_config cfg{};
   int device = 0;
+  // CPU backend (GPUAGG_FLAG_CPU_BACKEND, gpuagg_cpu.cpp): every "device" buffer below is
+  // host memory and the launches run on host threads; no HIP call is made
+  std::unique_ptr<gpuagg::cpu::Engine> cpu;
+  bool host_timing = false;  // CPU backend: gpuagg_set_timing measures the host launches
   hipStream_t stream = nullptr;
   std::string err;
 
@@ -336,14 +343,52 @@ int fail(gpuagg_ctx *c, int code, const char *fmt, ...) {
   } while (0)
 
 int bind(gpuagg_ctx *c) {
+  if (c->cpu) return GPUAGG_OK;
   HIPCHK(c, hipSetDevice(c->device));
   return GPUAGG_OK;
+}
+
+// ---- execution layer: the ctx's gfx950 device, or (CPU backend) host memory ------------
+hipError_t x_sync(gpuagg_ctx *c, hipStream_t st) { return c->cpu ? hipSuccess : hipStreamSynchronize(st); }
+hipError_t x_copy(gpuagg_ctx *c, void *dst, const void *src, size_t n, hipMemcpyKind k) {
+  if (!c->cpu) return hipMemcpy(dst, src, n, k);
+  if (n) memmove(dst, src, n);
+  return hipSuccess;
+}
+hipError_t x_copy_async(gpuagg_ctx *c, void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t st) {
+  if (!c->cpu) return hipMemcpyAsync(dst, src, n, k, st);
+  if (n) memmove(dst, src, n);
+  return hipSuccess;
+}
+hipError_t x_set_async(gpuagg_ctx *c, void *p, int v, size_t n, hipStream_t st) {
+  if (!c->cpu) return hipMemsetAsync(p, v, n, st);
+  if (n) memset(p, v, n);
+  return hipSuccess;
+}
+// pinned host memory (device mode) / plain host memory (CPU backend)
+hipError_t x_host_alloc(gpuagg_ctx *c, void **p, size_t n) {
+  if (!c->cpu) return hipHostMalloc(p, n, hipHostMallocDefault);
+  *p = calloc(1, n ? n : 1);
+  return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+void x_host_free(gpuagg_ctx *c, void *p) {
+  if (!p) return;
+  if (c->cpu) free(p);
+  else hipHostFree(p);
 }
 
 template <class T>
 int dev_alloc(gpuagg_ctx *c, T **p, size_t count) {
   *p = nullptr;
   if (!count) return GPUAGG_OK;
+  if (c->cpu) {  // 64-byte aligned like device allocations (vector loads, 16-byte slots)
+    const size_t bytes = (count * sizeof(T) + 63) & ~(size_t)63;
+    void *q = aligned_alloc(64, bytes);
+    if (!q) return fail(c, GPUAGG_ENOMEM, "aligned_alloc(%zu bytes)", bytes);
+    memset(q, 0, bytes);
+    *p = (T *)q;
+    return GPUAGG_OK;
+  }
   hipError_t e = hipMalloc((void **)p, count * sizeof(T));
   if (e != hipSuccess)
     return fail(c, GPUAGG_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
@@ -351,8 +396,11 @@ int dev_alloc(gpuagg_ctx *c, T **p, size_t count) {
 }
 
 template <class T>
-void dev_free(T *&p) {
-  if (p) hipFree((void *)p);
+void dev_free(gpuagg_ctx *c, T *&p) {
+  if (p) {
+    if (c->cpu) free((void *)p);
+    else hipFree((void *)p);
+  }
   p = nullptr;
 }
 
@@ -360,8 +408,8 @@ void dev_free(T *&p) {
 template <class T>
 int ensure_buf(gpuagg_ctx *c, T **p, size_t *alloc, size_t count) {
   if (count <= *alloc) return GPUAGG_OK;
-  if (*p) hipStreamSynchronize(c->stream);  // in-flight launches may still use the old buffer
-  dev_free(*p);
+  if (*p) x_sync(c, c->stream);  // in-flight launches may still use the old buffer
+  dev_free(c, *p);
   *alloc = 0;
   if (int rc = dev_alloc(c, p, count)) return rc;
   *alloc = count;
@@ -415,28 +463,27 @@ void ctx_values(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, 
   if (opts & OPT_PORT) out.push_back((port17 & 0x10000u) ? std::to_string(port17 & 0xFFFFu) : "unknown");
 }
 
-void free_batch_cols(gpuagg_batch *b) {
+void free_batch_cols(gpuagg_ctx *c, gpuagg_batch *b) {
   for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
-                       &b->cols.ports, &b->cols.dns_id, &b->cols.tcp_id})
-    if (*p) {
-      hipHostFree(*p);
-      *p = nullptr;
-    }
-  if (b->cols.time_ns) hipHostFree(b->cols.time_ns);
+                       &b->cols.ports, &b->cols.dns_id, &b->cols.tcp_id}) {
+    x_host_free(c, *p);
+    *p = nullptr;
+  }
+  x_host_free(c, b->cols.time_ns);
   b->cols.time_ns = nullptr;
 }
 
 int ensure_staging(gpuagg_ctx *c, size_t cap) {
   if (cap <= c->staging_cap) return GPUAGG_OK;
   if (c->staging_cap) {  // in-flight copies / launches may use the old columns
-    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, x_sync(c, c->copy_stream));
+    HIPCHK(c, x_sync(c, c->stream));
   }
   c->staging_cap = 0;
   for (auto &s : c->stg) {
-    for (auto &p : s.cols) dev_free(p);
-    dev_free(s.tcp_id);
-    dev_free(s.time_ns);
+    for (auto &p : s.cols) dev_free(c, p);
+    dev_free(c, s.tcp_id);
+    dev_free(c, s.time_ns);
     for (auto &p : s.cols)
       if (int rc = dev_alloc(c, &p, cap)) return rc;
     if (int rc = dev_alloc(c, &s.tcp_id, cap)) return rc;
@@ -482,6 +529,10 @@ constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 // of the counters or the group-by table calls it first: gpuagg_sync (and through it the
 // snapshot), state export, merge, slot retirement and dense re-layout.
 int fold_pending(gpuagg_ctx *c) {
+  if (c->cpu) {  // the host threads' accumulators into the ctx's counters and table
+    c->cpu->flush();
+    return GPUAGG_OK;
+  }
   if (!c->pend.active) return GPUAGG_OK;
   c->pend.active = false;
   LaunchArgs f = c->pend.a;
@@ -501,21 +552,25 @@ int fold_pending(gpuagg_ctx *c) {
 }
 
 // The state is being cleared: the waiting lists are discarded with it.
-void drop_pending(gpuagg_ctx *c) { c->pend.active = false; }
+void drop_pending(gpuagg_ctx *c) {
+  c->pend.active = false;
+  if (c->cpu) c->cpu->drop();
+}
 
 int reset_state(gpuagg_ctx *c) {
   drop_pending(c);
   if (c->dense_len) {
-    HIPCHK(c, hipMemsetAsync(c->d_dense_cnt, 0, c->dense_len * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_dense_byt, 0, c->dense_len * 8, c->stream));
+    HIPCHK(c, x_set_async(c, c->d_dense_cnt, 0, c->dense_len * 8, c->stream));
+    HIPCHK(c, x_set_async(c, c->d_dense_byt, 0, c->dense_len * 8, c->stream));
   }
   if (c->sparse_slots) {
-    HIPCHK(c, hipMemsetAsync(c->sv.dropped, 0, 8, c->stream));
-    HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+    HIPCHK(c, x_set_async(c, c->sv.dropped, 0, 8, c->stream));
+    if (c->cpu) cpu::sparse_init(c->sv, c->sparse_slots);
+    else HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
   }
-  if (c->cms_len) HIPCHK(c, hipMemsetAsync(c->d_cms, 0, c->cms_len * 4, c->stream));
-  if (c->hll_len) HIPCHK(c, hipMemsetAsync(c->d_hll, 0, c->hll_len, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->cms_len) HIPCHK(c, x_set_async(c, c->d_cms, 0, c->cms_len * 4, c->stream));
+  if (c->hll_len) HIPCHK(c, x_set_async(c, c->d_hll, 0, c->hll_len, c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   return GPUAGG_OK;
 }
 
@@ -570,42 +625,42 @@ int layout_dense(gpuagg_ctx *c, uint32_t key_cap, bool keep) {
     total += nkeys * 2 * gr.nsub;
   }
   if (total >= (1ull << 32)) return fail(c, GPUAGG_ECAPACITY, "dense counter space >= 2^32 bins");
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   int rc;
   uint64_t *cnt = nullptr, *byt = nullptr;
   if ((rc = dev_alloc(c, &cnt, total)) || (rc = dev_alloc(c, &byt, total))) {
-    dev_free(cnt);
+    dev_free(c, cnt);
     return rc;
   }
   if (total) {
-    HIPCHK(c, hipMemsetAsync(cnt, 0, total * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(byt, 0, total * 8, c->stream));
+    HIPCHK(c, x_set_async(c, cnt, 0, total * 8, c->stream));
+    HIPCHK(c, x_set_async(c, byt, 0, total * 8, c->stream));
   }
   for (size_t g = 0; keep && c->dense_len && g < c->groups.size(); ++g) {
     if (c->groups[g].sparse || !old_nbins[g]) continue;
     const uint64_t nb = std::min<uint64_t>(old_nbins[g], total - base[g]);
-    HIPCHK(c, hipMemcpyAsync(cnt + base[g], c->d_dense_cnt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(byt + base[g], c->d_dense_byt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, x_copy_async(c, cnt + base[g], c->d_dense_cnt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, x_copy_async(c, byt + base[g], c->d_dense_byt + old_base[g], nb * 8, hipMemcpyDeviceToDevice, c->stream));
   }
   if (c->cfg.hll_precision) {
     const size_t len = (size_t)key_cap << c->cfg.hll_precision;
     uint8_t *hll = nullptr;
     if ((rc = dev_alloc(c, &hll, len))) {
-      dev_free(cnt);
-      dev_free(byt);
+      dev_free(c, cnt);
+      dev_free(c, byt);
       return rc;
     }
-    HIPCHK(c, hipMemsetAsync(hll, 0, len, c->stream));
+    HIPCHK(c, x_set_async(c, hll, 0, len, c->stream));
     if (keep && c->hll_len)
-      HIPCHK(c, hipMemcpyAsync(hll, c->d_hll, std::min(len, c->hll_len), hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dev_free(c->d_hll);
+      HIPCHK(c, x_copy_async(c, hll, c->d_hll, std::min(len, c->hll_len), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, x_sync(c, c->stream));
+    dev_free(c, c->d_hll);
     c->d_hll = hll;
     c->hll_len = len;
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  dev_free(c->d_dense_cnt);
-  dev_free(c->d_dense_byt);
+  HIPCHK(c, x_sync(c, c->stream));
+  dev_free(c, c->d_dense_cnt);
+  dev_free(c, c->d_dense_byt);
   c->d_dense_cnt = cnt;
   c->d_dense_byt = byt;
   c->dense_len = total;
@@ -684,6 +739,12 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   s.blocks = c->n_cu;
   s.win_shift = std::min<uint32_t>(kCmsWindowShift, s.cms_wlog2);
   s.hll_slots = s.hll_p ? (uint32_t)(c->hll_len >> s.hll_p) : 0;
+  if (c->cpu) {  // relaxed atomics on the shared rows / registers
+    s.cols = ColsView{cv.src_ip, cv.dst_ip, nullptr, cv.meta, cv.ports, nullptr};
+    s.n = n;
+    c->cpu->sketch(s);
+    return GPUAGG_OK;
+  }
   if (s.hll_p && c->ipl_all_bytes) {
     s.ipl = c->d_ipl_all;
     s.ipl_nb = c->ipl_all_nb;
@@ -775,11 +836,12 @@ int lat_reset(gpuagg_ctx *c, bool full) {
     full = true;
   }
   if (full) {
-    HIPCHK(c, hipMemsetAsync(c->d_lat, 0, kLatStateWords * 8, c->stream));
+    HIPCHK(c, x_set_async(c, c->d_lat, 0, kLatStateWords * 8, c->stream));
     c->lat_carry_bound = 0;
     c->lat_peak_pending = 0;
+    if (c->cpu) c->cpu->latency_reset();
   } else {
-    HIPCHK(c, hipMemsetAsync(c->d_lat + kLatHist, 0, (kLatStateWords - kLatHist) * 8, c->stream));
+    HIPCHK(c, x_set_async(c, c->d_lat + kLatHist, 0, (kLatStateWords - kLatHist) * 8, c->stream));
   }
   return GPUAGG_OK;
 }
@@ -790,6 +852,22 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   if (!cv.ports || !cv.tcp_id || !cv.time_ns)
     return fail(c, GPUAGG_EINVAL, "node-apiserver latency metrics read the ports, tcp_id and time_ns columns");
   if (!c->d_lat && (rc = lat_reset(c, true))) return rc;
+  if (c->cpu) {  // the TTL join in record order on the host
+    LatArgs a{};
+    a.src = cv.src_ip;
+    a.dst = cv.dst_ip;
+    a.meta = cv.meta;
+    a.ports = cv.ports;
+    a.tcp_id = cv.tcp_id;
+    a.time_ns = cv.time_ns;
+    a.n = n;
+    a.api = c->d_api;
+    a.n_api = (uint32_t)c->api_ips.size();
+    a.state = c->d_lat;
+    c->lat_peak_pending = std::max<uint64_t>(c->lat_peak_pending, c->d_lat[kLatPending]);
+    c->cpu->latency(a, c->lat_enabled);
+    return GPUAGG_OK;
+  }
   LatArgs a{};
   a.src = cv.src_ip;
   a.dst = cv.dst_ip;
@@ -813,7 +891,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         (rc = dev_alloc(c, &c->d_lat_blk_base, nb)))
       return rc;
     if (c->lat_blk_alloc < nb) {  // keep every per-block array the same size
-      dev_free(c->d_lat_blk_cnt);
+      dev_free(c, c->d_lat_blk_cnt);
       c->lat_blk_alloc = 0;
       if ((rc = ensure_buf(c, &c->d_lat_blk_cnt, &c->lat_blk_alloc, nb))) return rc;
     }
@@ -825,10 +903,10 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   // events: carried entries + at most one per record
   const size_t cap = c->lat_carry_bound + n;
   if (cap > c->lat_ev_alloc) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dev_free(c->d_lat_ev);
-    dev_free(c->d_lat_hash);
-    dev_free(c->d_lat_idx);
+    HIPCHK(c, x_sync(c, c->stream));
+    dev_free(c, c->d_lat_ev);
+    dev_free(c, c->d_lat_hash);
+    dev_free(c, c->d_lat_idx);
     c->lat_ev_alloc = 0;
     if ((rc = dev_alloc(c, &c->d_lat_ev, cap)) || (rc = dev_alloc(c, &c->d_lat_hash, 2 * cap)) ||
         (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)))
@@ -845,17 +923,17 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", 8 * kLatReadWords);
   a.carry_in = c->d_lat_carry[c->lat_carry_cur];  // copied into the events by the front
   HIPCHK(c, launch_latency_front(a, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_lat_n, c->d_lat + kLatPending, 8 * kLatReadWords, hipMemcpyDeviceToHost,
+  HIPCHK(c, x_copy_async(c, c->h_lat_n, c->d_lat + kLatPending, 8 * kLatReadWords, hipMemcpyDeviceToHost,
                            c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   const uint64_t ne = c->h_lat_n[kLatEvents - kLatPending];
   c->lat_peak_pending = std::max<uint64_t>(c->lat_peak_pending, c->h_lat_n[0]);  // carried into this batch
   // carry-out buffer: at most one entry per event
   if (ne > c->lat_carry_alloc) {
     LatEvent *keep = c->d_lat_carry[c->lat_carry_cur];  // read by this batch already (copied)
-    dev_free(c->d_lat_carry[c->lat_carry_cur ^ 1]);
+    dev_free(c, c->d_lat_carry[c->lat_carry_cur ^ 1]);
     c->d_lat_carry[c->lat_carry_cur] = nullptr;
-    dev_free(keep);
+    dev_free(c, keep);
     c->lat_carry_alloc = 0;
     if ((rc = dev_alloc(c, &c->d_lat_carry[0], ne)) || (rc = dev_alloc(c, &c->d_lat_carry[1], ne))) return rc;
     c->lat_carry_alloc = ne;
@@ -932,6 +1010,23 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
           a.dense_ng = ng;
           break;
         }
+  }
+  if (c->cpu) {  // host threads: every update direct (no LDS, lists or spill)
+    a.cols = cv;
+    a.n = n;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (c->plan.ngroups > 0) c->cpu->aggregate(a);
+    if (c->host_timing) {
+      c->stats.kernel_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      c->stats.kernel_launches += 1;
+    }
+    c->kernel_name = "cpu";
+    if ((c->cms_len || c->hll_len) && (rc = launch_sketches(c, cv, n))) return rc;
+    if (c->lat_enabled && (rc = launch_latency(c, cv, n))) return rc;
+    c->stats.records += n;
+    c->stats.batches += 1;
+    c->stats.last_kernel = GPUAGG_KERNEL_CPU;
+    return GPUAGG_OK;
   }
   // geometry: one 1024-thread workgroup per CU holding L dense bins in LDS
   // LDS window: the longest prefix of whole dense groups (hottest first) that fits
@@ -1124,7 +1219,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.stage_b = c->d_stage_b;
       if (!c->d_fold_ticket) {  // per-window tickets, reset by each window's last partition
         if ((rc = dev_alloc(c, &c->d_fold_ticket, kMaxSpillWindows))) return rc;
-        HIPCHK(c, hipMemsetAsync(c->d_fold_ticket, 0, kMaxSpillWindows * 4, c->stream));
+        HIPCHK(c, x_set_async(c, c->d_fold_ticket, 0, kMaxSpillWindows * 4, c->stream));
       }
       a.fold_ticket = c->d_fold_ticket;
     }
@@ -1177,11 +1272,18 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols &out) {
   if (kind != kRawPacket && kind != kRawDrop) return fail(c, GPUAGG_EINVAL, "unknown raw record kind %d", kind);
   if (n == 0) return GPUAGG_OK;
-  if (!dev_raw || ((uintptr_t)dev_raw & 15u)) return fail(c, GPUAGG_EINVAL, "raw records must be 16-byte aligned");
+  if (!dev_raw || (!c->cpu && ((uintptr_t)dev_raw & 15u)))
+    return fail(c, GPUAGG_EINVAL, "raw records must be 16-byte aligned");
   if (!out.src_ip || !out.dst_ip || !out.bytes || !out.meta) return fail(c, GPUAGG_EINVAL, "decode: null column");
   if (!c->d_decode_oor) {
     if (int rc = dev_alloc(c, &c->d_decode_oor, 1)) return rc;
-    HIPCHK(c, hipMemsetAsync(c->d_decode_oor, 0, 8, c->stream));
+    HIPCHK(c, x_set_async(c, c->d_decode_oor, 0, 8, c->stream));
+  }
+  if (c->cpu) {
+    *c->d_decode_oor += c->cpu->decode(DecodeArgs{kind, dev_raw, n, out, c->d_decode_oor, c->n_cu,
+                                                  (uint64_t)c->time_offset});
+    c->stats.decoded += n;
+    return GPUAGG_OK;
   }
   std::array<hipEvent_t, 2> ev{};
   if (c->timing) {
@@ -1227,6 +1329,23 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
   if (cfg->cms_depth && (cfg->cms_width_log2 < 4 || cfg->cms_width_log2 > 28 || cfg->cms_depth > 16))
     return GPUAGG_EINVAL;
   if (cfg->hll_precision && (cfg->hll_precision < 4 || cfg->hll_precision > 18)) return GPUAGG_EINVAL;
+  if (cfg->flags & GPUAGG_FLAG_CPU_BACKEND) {
+    // host threads instead of a device: the node's CPU share (GPUAGG_CPU_THREADS, else the
+    // hardware threads, at most 64)
+    unsigned t = std::thread::hardware_concurrency();
+    if (const char *e = getenv("GPUAGG_CPU_THREADS")) t = (unsigned)atoi(e);
+    t = std::max(1u, std::min(64u, t ? t : 1u));
+    c->cpu.reset(new cpu::Engine(t));
+    c->cfg.flags |= GPUAGG_FLAG_NO_LDS_IP_TABLE;  // no LDS images to build
+    c->n_cu = t;
+    c->defer_folds = false;
+    if (cfg->cms_depth) {
+      c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
+      if (dev_alloc(c.get(), &c->d_cms, c->cms_len)) return GPUAGG_ENOMEM;
+    }
+    *out = c.release();
+    return GPUAGG_OK;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c->device || c->device < 0)
     return GPUAGG_EDEVICE;
@@ -1268,59 +1387,61 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
 
 void gpuagg_destroy(gpuagg_ctx *c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  if (!c->cpu) {
+    hipSetDevice(c->device);
+    if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+    if (c->stream) hipStreamSynchronize(c->stream);
+  }
   drain_timing(c);
   for (auto *b : c->batches) {
-    free_batch_cols(b);
+    free_batch_cols(c, b);
     delete b;
   }
-  dev_free(c->d_ip);
-  dev_free(c->d_rpre);
-  dev_free(c->d_rblk);
-  dev_free(c->d_ipl);
-  dev_free(c->d_ipl_all);
-  dev_free(c->d_ipc);
-  dev_free(c->d_api);
-  dev_free(c->d_lat);
-  dev_free(c->d_lat_blk_cnt);
-  dev_free(c->d_lat_blk_max);
-  dev_free(c->d_lat_blk_clk);
-  dev_free(c->d_lat_blk_base);
-  dev_free(c->d_lat_ev);
-  dev_free(c->d_lat_hash);
-  dev_free(c->d_lat_idx);
-  dev_free(c->d_lat_carry[0]);
-  dev_free(c->d_lat_carry[1]);
+  dev_free(c, c->d_ip);
+  dev_free(c, c->d_rpre);
+  dev_free(c, c->d_rblk);
+  dev_free(c, c->d_ipl);
+  dev_free(c, c->d_ipl_all);
+  dev_free(c, c->d_ipc);
+  dev_free(c, c->d_api);
+  dev_free(c, c->d_lat);
+  dev_free(c, c->d_lat_blk_cnt);
+  dev_free(c, c->d_lat_blk_max);
+  dev_free(c, c->d_lat_blk_clk);
+  dev_free(c, c->d_lat_blk_base);
+  dev_free(c, c->d_lat_ev);
+  dev_free(c, c->d_lat_hash);
+  dev_free(c, c->d_lat_idx);
+  dev_free(c, c->d_lat_carry[0]);
+  dev_free(c, c->d_lat_carry[1]);
   if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
-  if (c->h_lat_n) hipHostFree(c->h_lat_n);
-  dev_free(c->d_dense_cnt);
-  dev_free(c->d_dense_byt);
-  dev_free(c->sv.k0);  // k1, k2, cnt, byt point into the same array
-  dev_free(c->sv.dropped);
-  dev_free(c->d_counter);
-  dev_free(c->d_export);
-  dev_free(c->d_cms);
-  dev_free(c->d_hll);
-  dev_free(c->d_spill);
-  dev_free(c->d_spill_count);
-  dev_free(c->d_stage_a);
-  dev_free(c->d_enrich);
-  dev_free(c->d_stage_b);
-  dev_free(c->d_sk_lists);
-  dev_free(c->d_sk_counts);
-  dev_free(c->d_fold_ticket);
-  dev_free(c->d_sp_lists);
-  dev_free(c->d_sp_counts);
-  dev_free(c->d_hll_lists);
-  dev_free(c->d_hll_lists2);
-  dev_free(c->d_hll_counts2);
-  dev_free(c->d_hll_counts);
-  dev_free(c->d_decode_oor);
+  x_host_free(c, c->h_lat_n);
+  dev_free(c, c->d_dense_cnt);
+  dev_free(c, c->d_dense_byt);
+  dev_free(c, c->sv.k0);  // k1, k2, cnt, byt point into the same array
+  dev_free(c, c->sv.dropped);
+  dev_free(c, c->d_counter);
+  dev_free(c, c->d_export);
+  dev_free(c, c->d_cms);
+  dev_free(c, c->d_hll);
+  dev_free(c, c->d_spill);
+  dev_free(c, c->d_spill_count);
+  dev_free(c, c->d_stage_a);
+  dev_free(c, c->d_enrich);
+  dev_free(c, c->d_stage_b);
+  dev_free(c, c->d_sk_lists);
+  dev_free(c, c->d_sk_counts);
+  dev_free(c, c->d_fold_ticket);
+  dev_free(c, c->d_sp_lists);
+  dev_free(c, c->d_sp_counts);
+  dev_free(c, c->d_hll_lists);
+  dev_free(c, c->d_hll_lists2);
+  dev_free(c, c->d_hll_counts2);
+  dev_free(c, c->d_hll_counts);
+  dev_free(c, c->d_decode_oor);
   for (auto &st : c->stg) {
-    for (auto &p : st.cols) dev_free(p);
-    dev_free(st.raw);
+    for (auto &p : st.cols) dev_free(c, p);
+    dev_free(c, st.raw);
     if (st.copied) hipEventDestroy(st.copied);
     if (st.released) hipEventDestroy(st.released);
   }
@@ -1371,7 +1492,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
   // Module.Reconcile leaves the metrics alone when the context options compare equal
   // (metrics_module.go:142-166): a resync or a namespace-only change keeps the counters
   if (c->have_opts && same_options(c->cur_opts, new_opts)) return GPUAGG_OK;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   const bool local = !c->remote;
   // NewLatencyMetrics (latency.go:73-115): the three names it switches on
   uint32_t lat = 0;
@@ -1679,16 +1800,16 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     if (ok) break;
     if (cap > ((size_t)1 << 30)) return fail(c, GPUAGG_ECAPACITY, "IP table cannot be built");
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches use the old table
+  HIPCHK(c, x_sync(c, c->stream));  // in-flight batches use the old table
   // dense counters / HLL rows cover every interned slot
   if (c->slots.size() > c->key_cap && (rc = layout_dense(c, key_cap_for(c, c->slots.size()), true)))
     return rc;
   if (cap != c->ip_cap) {
-    dev_free(c->d_ip);
+    dev_free(c, c->d_ip);
     c->ip_cap = 0;
     if ((rc = dev_alloc(c, &c->d_ip, cap))) return rc;
   }
-  HIPCHK(c, hipMemcpy(c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, x_copy(c, c->d_ip, tab.data(), cap * 8, hipMemcpyHostToDevice));
   c->ip_cap = cap;
   // radix image when the IPs fall in at most kRadixMaxBlocks /16 prefixes (cluster pod
   // CIDRs): L2-resident where a hash table of 100k+ IPs is not
@@ -1714,8 +1835,8 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       }
       if (!c->d_rpre && (rc = dev_alloc(c, &c->d_rpre, (size_t)1 << 16))) return rc;
       if ((rc = ensure_buf(c, &c->d_rblk, &c->rblk_alloc, blk.size()))) return rc;
-      HIPCHK(c, hipMemcpy(c->d_rpre, pre.data(), pre.size() * 2, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMemcpy(c->d_rblk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(c, x_copy(c, c->d_rpre, pre.data(), pre.size() * 2, hipMemcpyHostToDevice));
+      HIPCHK(c, x_copy(c, c->d_rblk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
     }
   }
   // LDS image: non-apiserver pods only (local context treats the apiserver pseudo pod
@@ -1733,12 +1854,12 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
       const std::vector<uint8_t> &img = radix ? ir.bytes : im.bytes;
       const uint32_t bytes = (uint32_t)img.size();
       if (bytes > c->ipl_alloc) {
-        dev_free(c->d_ipl);
+        dev_free(c, c->d_ipl);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
       }
-      HIPCHK(c, hipMemcpy(c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
+      HIPCHK(c, x_copy(c, c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
       c->ipl_radix = radix;
       c->ipl_nb = radix ? 0 : im.nb;
       c->ipl_seed = radix ? 0 : im.seed;
@@ -1757,12 +1878,12 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     if (ipl_build(ents, &im)) {
       const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_all_alloc) {
-        dev_free(c->d_ipl_all);
+        dev_free(c, c->d_ipl_all);
         c->ipl_all_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
         c->ipl_all_alloc = bytes;
       }
-      HIPCHK(c, hipMemcpy(c->d_ipl_all, im.bytes.data(), bytes, hipMemcpyHostToDevice));
+      HIPCHK(c, x_copy(c, c->d_ipl_all, im.bytes.data(), bytes, hipMemcpyHostToDevice));
       c->ipl_all_nb = im.nb;
       c->ipl_all_seed = im.seed;
       c->ipl_all_bytes = bytes;
@@ -1888,7 +2009,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
   int rc = bind(c);
   if (rc) return rc;
   if ((rc = fold_pending(c))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   std::vector<char> live(c->slots.size(), 0);
   for (const auto &e : c->installed) live[e.second] = 1;
   std::vector<uint32_t> dead;
@@ -1902,12 +2023,15 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
   if (!dead_dev.empty() && (c->dense_len || c->hll_len)) {
     uint32_t *d = nullptr;
     if ((rc = dev_alloc(c, &d, dead_dev.size()))) return rc;
-    hipError_t e = hipMemcpyAsync(d, dead_dev.data(), dead_dev.size() * 4, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess)
+    hipError_t e = x_copy_async(c, d, dead_dev.data(), dead_dev.size() * 4, hipMemcpyHostToDevice, c->stream);
+    if (c->cpu)
+      cpu::zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
+                      c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan);
+    else if (e == hipSuccess)
       e = launch_zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
                             c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    dev_free(d);
+    if (e == hipSuccess) e = x_sync(c, c->stream);
+    dev_free(c, d);
     if (e != hipSuccess) return fail(c, GPUAGG_EDEVICE, "retire: %s", hipGetErrorString(e));
   }
   // group-by entries keyed by a dead slot (as source or destination): the table is
@@ -1916,7 +2040,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
     std::vector<char> is_dead(c->slots.size() + 1, 0);  // indexed by slot + 1
     for (uint32_t s : dead) is_dead[s + 1] = 1;
     if (c->export_cap < c->sparse_slots) {
-      dev_free(c->d_export);
+      dev_free(c, c->d_export);
       c->export_cap = 0;
       if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
       c->export_cap = c->sparse_slots;
@@ -1924,7 +2048,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
     size_t nent = 0;
     if ((rc = gpuagg_sparse_export(c, c->d_export, c->export_cap, &nent))) return rc;
     std::vector<uint64_t> ent(nent * kSparseEntryWords);
-    if (nent) HIPCHK(c, hipMemcpy(ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
+    if (nent) HIPCHK(c, x_copy(c, ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
     size_t keep = 0;
     for (size_t i = 0; i < nent; ++i) {
       const uint64_t *w = &ent[i * kSparseEntryWords];
@@ -1935,15 +2059,20 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
     }
     if (keep != nent) {
       uint64_t dropped = 0;
-      HIPCHK(c, hipMemcpy(&dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
-      HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
-      if (keep) {
-        HIPCHK(c, hipMemcpyAsync(c->d_export, ent.data(), keep * kSparseEntryWords * 8, hipMemcpyHostToDevice,
-                                 c->stream));
-        HIPCHK(c, launch_sparse_import(c->sv, c->d_export, keep, c->stream));
+      HIPCHK(c, x_copy(c, &dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+      if (c->cpu) {
+        cpu::sparse_init(c->sv, c->sparse_slots);
+        cpu::sparse_import(c->sv, ent.data(), keep);
+      } else {
+        HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+        if (keep) {
+          HIPCHK(c, x_copy_async(c, c->d_export, ent.data(), keep * kSparseEntryWords * 8, hipMemcpyHostToDevice,
+                                   c->stream));
+          HIPCHK(c, launch_sparse_import(c->sv, c->d_export, keep, c->stream));
+        }
       }
-      HIPCHK(c, hipMemcpyAsync(c->sv.dropped, &dropped, 8, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, x_copy_async(c, c->sv.dropped, &dropped, 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, x_sync(c, c->stream));
     }
   }
   // the dictionary: ids become reusable
@@ -1985,20 +2114,20 @@ int gpuagg_alloc_batch(gpuagg_ctx *c, size_t cap, gpuagg_batch **out) {
   b->capacity = cap;
   for (uint32_t **p : {&b->cols.src_ip, &b->cols.dst_ip, &b->cols.bytes, &b->cols.meta,
                        &b->cols.ports, &b->cols.dns_id, &b->cols.tcp_id}) {
-    if (hipHostMalloc((void **)p, cap * 4, hipHostMallocDefault) != hipSuccess) {
-      free_batch_cols(b);
+    if (x_host_alloc(c, (void **)p, cap * 4) != hipSuccess) {
+      free_batch_cols(c, b);
       delete b;
       return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", cap * 4);
     }
     memset(*p, 0, cap * 4);
   }
-  if (hipHostMalloc((void **)&b->cols.time_ns, cap * 8, hipHostMallocDefault) != hipSuccess) {
-    free_batch_cols(b);
+  if (x_host_alloc(c, (void **)&b->cols.time_ns, cap * 8) != hipSuccess) {
+    free_batch_cols(c, b);
     delete b;
     return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", cap * 8);
   }
   memset(b->cols.time_ns, 0, cap * 8);
-  if ((rc = ensure_staging(c, cap))) return rc;
+  if (!c->cpu && (rc = ensure_staging(c, cap))) return rc;
   c->batches.push_back(b);
   *out = b;
   return GPUAGG_OK;
@@ -2006,9 +2135,11 @@ int gpuagg_alloc_batch(gpuagg_ctx *c, size_t cap, gpuagg_batch **out) {
 
 void gpuagg_free_batch(gpuagg_ctx *c, gpuagg_batch *b) {
   if (!c || !b) return;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
-  free_batch_cols(b);
+  if (!c->cpu) {
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+  }
+  free_batch_cols(c, b);
   c->batches.erase(std::remove(c->batches.begin(), c->batches.end(), b), c->batches.end());
   delete b;
 }
@@ -2024,11 +2155,11 @@ int stage_batch(gpuagg_ctx *c, const gpuagg_batch *b, size_t n, gpuagg_ctx::Stag
                         (bool)c->plan.need_dns};
   for (int i = 0; i < 6; ++i)
     if (need[i] || (i == 4 && c->lat_enabled))
-      HIPCHK(c, hipMemcpyAsync(s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
+      HIPCHK(c, x_copy_async(c, s->cols[i], src[i], n * 4, hipMemcpyHostToDevice, c->copy_stream));
   *cv = ColsView{s->cols[0], s->cols[1], s->cols[2], s->cols[3], s->cols[4], s->cols[5]};
   if (c->lat_enabled) {
-    HIPCHK(c, hipMemcpyAsync(s->tcp_id, b->cols.tcp_id, n * 4, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(c, hipMemcpyAsync(s->time_ns, b->cols.time_ns, n * 8, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(c, x_copy_async(c, s->tcp_id, b->cols.tcp_id, n * 4, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(c, x_copy_async(c, s->time_ns, b->cols.time_ns, n * 8, hipMemcpyHostToDevice, c->copy_stream));
     cv->tcp_id = s->tcp_id;
     cv->time_ns = s->time_ns;
   }
@@ -2048,7 +2179,8 @@ int enrich_launch(gpuagg_ctx *c, const uint32_t *src, const uint32_t *dst, size_
   a.n = n;
   a.o_src = os;
   a.o_dst = od;
-  HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
+  if (c->cpu) c->cpu->enrich(a);
+  else HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
   return GPUAGG_OK;
 }
 
@@ -2057,6 +2189,9 @@ int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
   int rc = bind(c);
   if (rc) return rc;
   if (n == 0) return GPUAGG_OK;
+  if (c->cpu)  // the batch's host columns are read in place
+    return launch(c, ColsView{b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports,
+                              b->cols.dns_id, b->cols.tcp_id, b->cols.time_ns}, n);
   gpuagg_ctx::Staging *s;
   ColsView cv{};
   if ((rc = stage_batch(c, b, n, &s, &cv))) return rc;
@@ -2069,6 +2204,11 @@ int gpuagg_submit_enrich(gpuagg_ctx *c, gpuagg_batch *b, size_t n, int32_t *src_
   if (rc) return rc;
   if (n == 0) return GPUAGG_OK;
   if (!c->ip_cap) return fail(c, GPUAGG_ESTATE, "gpuagg_set_endpoints was never called");
+  if (c->cpu) {
+    if ((rc = enrich_launch(c, b->cols.src_ip, b->cols.dst_ip, n, src_slot, dst_slot))) return rc;
+    return launch(c, ColsView{b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports,
+                              b->cols.dns_id, b->cols.tcp_id, b->cols.time_ns}, n);
+  }
   if ((rc = ensure_buf(c, &c->d_enrich, &c->enrich_alloc, 2 * b->capacity))) return rc;
   gpuagg_ctx::Staging *s;
   ColsView cv{};
@@ -2077,8 +2217,8 @@ int gpuagg_submit_enrich(gpuagg_ctx *c, gpuagg_batch *b, size_t n, int32_t *src_
     // the endpoints first, so the host copy does not wait for the aggregation
     int r = enrich_launch(c, cv.src_ip, cv.dst_ip, n, c->d_enrich, c->d_enrich + n);
     if (r) return r;
-    HIPCHK(c, hipMemcpyAsync(src_slot, c->d_enrich, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(dst_slot, c->d_enrich + n, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, x_copy_async(c, src_slot, c->d_enrich, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, x_copy_async(c, dst_slot, c->d_enrich + n, n * 4, hipMemcpyDeviceToHost, c->stream));
     if ((r = launch(c, cv, n))) return r;
     // the slots are the caller's on return (the aggregation may still run)
     HIPCHK(c, hipEventRecord(c->enrich_done, c->stream));
@@ -2102,12 +2242,12 @@ int gpuagg_sync(gpuagg_ctx *c) {
   int rc = bind(c);
   if (rc) return rc;
   if ((rc = fold_pending(c))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   drain_timing(c);
   if (c->d_decode_oor)
-    HIPCHK(c, hipMemcpy(&c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, x_copy(c, &c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
   if (c->sparse_slots)
-    HIPCHK(c, hipMemcpy(&c->stats.sparse_dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, x_copy(c, &c->stats.sparse_dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
 }
 
@@ -2128,6 +2268,7 @@ int gpuagg_submit_raw_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_
   gpuagg_ctx::Staging *s;
   if ((rc = acquire_staging(c, &s))) return rc;
   rc = decode_and_launch(c, *s, kind, dev_raw, n);
+  if (c->cpu) return rc;
   HIPCHK(c, hipEventRecord(s->released, c->stream));
   s->in_use = true;
   return rc;
@@ -2141,15 +2282,16 @@ int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
   if (n == 0) return GPUAGG_OK;
   const size_t rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
   if ((rc = ensure_staging(c, n))) return rc;
+  if (c->cpu) return decode_and_launch(c, c->stg[0], kind, host_raw, n);  // decoded from the caller's memory
   gpuagg_ctx::Staging *s;
   if ((rc = acquire_staging(c, &s))) return rc;
   if (n * rec > s->raw_alloc) {  // (acquire_staging waited for the kernels reading it)
-    dev_free(s->raw);
+    dev_free(c, s->raw);
     s->raw_alloc = 0;
     if ((rc = dev_alloc(c, &s->raw, n * rec))) return rc;
     s->raw_alloc = n * rec;
   }
-  HIPCHK(c, hipMemcpyAsync(s->raw, host_raw, n * rec, hipMemcpyHostToDevice, c->copy_stream));
+  HIPCHK(c, x_copy_async(c, s->raw, host_raw, n * rec, hipMemcpyHostToDevice, c->copy_stream));
   return run_staged(c, *s, [&] { return decode_and_launch(c, *s, kind, s->raw, n); });
 }
 
@@ -2157,7 +2299,7 @@ int gpuagg_reset(gpuagg_ctx *c) {
   if (!c) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   if ((rc = lat_reset(c, false))) return rc;
   return reset_state(c);
 }
@@ -2175,25 +2317,25 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
   // dense counters
   std::vector<uint64_t> dc(c->dense_len), db(c->dense_len);
   if (c->dense_len) {
-    HIPCHK(c, hipMemcpy(dc.data(), c->d_dense_cnt, c->dense_len * 8, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(db.data(), c->d_dense_byt, c->dense_len * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, x_copy(c, dc.data(), c->d_dense_cnt, c->dense_len * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, x_copy(c, db.data(), c->d_dense_byt, c->dense_len * 8, hipMemcpyDeviceToHost));
   }
   // sparse entries
   std::vector<uint64_t> ent;
   size_t nent = 0;
   if (c->sparse_slots) {
     uint64_t dropped = 0;
-    HIPCHK(c, hipMemcpy(&dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, x_copy(c, &dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
     c->stats.sparse_dropped = dropped;  // reported with the result (gpuagg_result_dropped)
     if (c->export_cap < c->sparse_slots) {
-      dev_free(c->d_export);
+      dev_free(c, c->d_export);
       if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
       c->export_cap = c->sparse_slots;
     }
     rc = gpuagg_sparse_export(c, c->d_export, c->export_cap, &nent);
     if (rc) return rc;
     ent.resize(nent * kSparseEntryWords);
-    if (nent) HIPCHK(c, hipMemcpy(ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
+    if (nent) HIPCHK(c, x_copy(c, ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
     c->stats.sparse_entries = nent;
   }
 
@@ -2467,11 +2609,11 @@ int gpuagg_sketch_refresh(gpuagg_ctx *c) {
   if (!c) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   c->h_cms.resize(c->cms_len);
   c->h_hll.resize(c->hll_len);
-  if (c->cms_len) HIPCHK(c, hipMemcpy(c->h_cms.data(), c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
-  if (c->hll_len) HIPCHK(c, hipMemcpy(c->h_hll.data(), c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
+  if (c->cms_len) HIPCHK(c, x_copy(c, c->h_cms.data(), c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
+  if (c->hll_len) HIPCHK(c, x_copy(c, c->h_hll.data(), c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
 }
 
@@ -2513,8 +2655,8 @@ int gpuagg_cms_copy(gpuagg_ctx *c, uint32_t *out, size_t n) {
   if (!c || !out || n < c->cms_len) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->cms_len) HIPCHK(c, hipMemcpy(out, c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, x_sync(c, c->stream));
+  if (c->cms_len) HIPCHK(c, x_copy(c, out, c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
 }
 
@@ -2522,8 +2664,8 @@ int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
   if (!c || !out || n < c->hll_len) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->hll_len) HIPCHK(c, hipMemcpy(out, c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
+  HIPCHK(c, x_sync(c, c->stream));
+  if (c->hll_len) HIPCHK(c, x_copy(c, out, c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
 }
 
@@ -2533,7 +2675,7 @@ int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   if (c->pend.active) {  // the arrays below are read by the caller: fold what is waiting
     int rc = bind(c);
     if (rc || (rc = fold_pending(c))) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, x_sync(c, c->stream));
   }
   o->dense_count = c->d_dense_cnt;
   o->dense_bytes = c->d_dense_byt;
@@ -2558,11 +2700,17 @@ int gpuagg_sparse_export(gpuagg_ctx *c, uint64_t *dev_out, size_t cap, size_t *n
   int rc = bind(c);
   if (rc) return rc;
   if ((rc = fold_pending(c))) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_counter, 0, 8, c->stream));
+  if (c->cpu) {
+    const size_t n = cpu::sparse_export(c->sv, c->sparse_slots, dev_out, cap);
+    *n_out = std::min(n, cap);
+    if (n > cap) return fail(c, GPUAGG_ECAPACITY, "export buffer holds %zu of %zu entries", cap, n);
+    return GPUAGG_OK;
+  }
+  HIPCHK(c, x_set_async(c, c->d_counter, 0, 8, c->stream));
   HIPCHK(c, launch_sparse_export(c->sv, c->sparse_slots, dev_out, cap, c->d_counter, c->stream));
   uint64_t n = 0;
-  HIPCHK(c, hipMemcpyAsync(&n, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_copy_async(c, &n, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   *n_out = (size_t)std::min<uint64_t>(n, cap);
   if (n > cap) return fail(c, GPUAGG_ECAPACITY, "export buffer holds %zu of %llu entries", cap, (unsigned long long)n);
   return GPUAGG_OK;
@@ -2574,8 +2722,13 @@ int gpuagg_sparse_import(gpuagg_ctx *c, const uint64_t *dev_in, size_t n) {
   if (rc) return rc;
   if (!n) return GPUAGG_OK;
   if ((rc = ensure_sparse(c))) return rc;
+  if ((rc = fold_pending(c))) return rc;  // (CPU backend: the table has one writer at a time)
+  if (c->cpu) {
+    cpu::sparse_import(c->sv, dev_in, n);
+    return GPUAGG_OK;
+  }
   HIPCHK(c, launch_sparse_import(c->sv, dev_in, n, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
   return GPUAGG_OK;
 }
 
@@ -2595,11 +2748,14 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
   if (!ctxs || !n || !ctxs[0]) return GPUAGG_EINVAL;
   gpuagg_ctx *c0 = ctxs[0];
   int rc;
+  const bool host = c0->cpu != nullptr;  // CPU backend: host copies and loops
   // compatibility: one metric plan and one slot / DNS dictionary on every ctx
   size_t cap = c0->key_cap;
   for (size_t i = 1; i < n; ++i) {
     const gpuagg_ctx *ci = ctxs[i];
     if (!ci || ci == c0) return fail(c0, GPUAGG_EINVAL, "merge: ctx %zu is null or the target", i);
+    if ((ci->cpu != nullptr) != host)
+      return fail(c0, GPUAGG_EINVAL, "merge: ctx %zu and the target are on different backends", i);
     bool same = ci->remote == c0->remote && ci->groups.size() == c0->groups.size() &&
                 ci->cms_len == c0->cms_len && ci->cfg.hll_precision == c0->cfg.hll_precision &&
                 (ci->sparse_slots != 0) == (c0->sparse_slots != 0) && ci->slots.size() == c0->slots.size() &&
@@ -2625,8 +2781,8 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
     if ((rc = bind(ci))) return rc;
     if ((rc = fold_pending(ci))) return rc;
     if (ci->key_cap < cap && (rc = layout_dense(ci, (uint32_t)cap, true))) return rc;
-    HIPCHK(ci, hipStreamSynchronize(ci->stream));
-    HIPCHK(ci, hipStreamSynchronize(ci->copy_stream));
+    HIPCHK(ci, x_sync(ci, ci->stream));
+    HIPCHK(ci, x_sync(ci, ci->copy_stream));
   }
   if ((rc = bind(c0))) return rc;
   const size_t tmp_bytes = std::max({c0->dense_len * 8, c0->cms_len * 4, c0->hll_len, (size_t)8});
@@ -2635,26 +2791,45 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
   uint64_t *ent = nullptr;
   size_t ent_cap = 0;
   auto cleanup = [&] {
-    dev_free(tmp);
-    dev_free(ent);
+    dev_free(c0, tmp);
+    dev_free(c0, ent);
   };
-  auto peer = [&](void *dst, const void *src, int src_dev, size_t bytes) {
+  auto peer = [&](void *dst, const void *src, int src_dev, size_t bytes) -> hipError_t {
+    if (host) {
+      memcpy(dst, src, bytes);
+      return hipSuccess;
+    }
     return hipMemcpyPeerAsync(dst, c0->device, src, src_dev, bytes, c0->stream);
+  };
+  auto add_u64 = [&](uint64_t *d, const uint64_t *x, size_t m) -> hipError_t {
+    if (!host) return launch_merge_add_u64(d, x, m, c0->stream);
+    for (size_t k = 0; k < m; ++k) d[k] += x[k];
+    return hipSuccess;
+  };
+  auto add_u32 = [&](uint32_t *d, const uint32_t *x, size_t m) -> hipError_t {
+    if (!host) return launch_merge_add_u32(d, x, m, c0->stream);
+    for (size_t k = 0; k < m; ++k) d[k] += x[k];
+    return hipSuccess;
+  };
+  auto max_u8 = [&](uint8_t *d, const uint8_t *x, size_t m) -> hipError_t {
+    if (!host) return launch_merge_max_u8(d, x, m, c0->stream);
+    for (size_t k = 0; k < m; ++k) d[k] = std::max(d[k], x[k]);
+    return hipSuccess;
   };
   for (size_t i = 1; i < n; ++i) {
     gpuagg_ctx *ci = ctxs[i];
     hipError_t e = hipSuccess;
     if (c0->dense_len) {
       if ((e = peer(tmp, ci->d_dense_cnt, ci->device, c0->dense_len * 8)) == hipSuccess)
-        e = launch_merge_add_u64(c0->d_dense_cnt, (const uint64_t *)tmp, c0->dense_len, c0->stream);
+        e = add_u64(c0->d_dense_cnt, (const uint64_t *)tmp, c0->dense_len);
       if (e == hipSuccess && (e = peer(tmp, ci->d_dense_byt, ci->device, c0->dense_len * 8)) == hipSuccess)
-        e = launch_merge_add_u64(c0->d_dense_byt, (const uint64_t *)tmp, c0->dense_len, c0->stream);
+        e = add_u64(c0->d_dense_byt, (const uint64_t *)tmp, c0->dense_len);
     }
     if (e == hipSuccess && c0->cms_len && (e = peer(tmp, ci->d_cms, ci->device, c0->cms_len * 4)) == hipSuccess)
-      e = launch_merge_add_u32(c0->d_cms, (const uint32_t *)tmp, c0->cms_len, c0->stream);
+      e = add_u32(c0->d_cms, (const uint32_t *)tmp, c0->cms_len);
     if (e == hipSuccess && c0->hll_len && (e = peer(tmp, ci->d_hll, ci->device, c0->hll_len)) == hipSuccess)
-      e = launch_merge_max_u8(c0->d_hll, tmp, c0->hll_len, c0->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
+      e = max_u8(c0->d_hll, tmp, c0->hll_len);
+    if (e == hipSuccess) e = x_sync(c0, c0->stream);
     if (e != hipSuccess) {
       cleanup();
       return fail(c0, GPUAGG_EDEVICE, "merge of ctx %zu: %s", i, hipGetErrorString(e));
@@ -2662,7 +2837,7 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
     if (ci->sparse_slots) {  // group-by entries: exported on ci, inserted-and-added on c0
       if ((rc = bind(ci))) break;
       if (ci->export_cap < ci->sparse_slots) {
-        dev_free(ci->d_export);
+        dev_free(ci, ci->d_export);
         ci->export_cap = 0;
         if ((rc = dev_alloc(ci, &ci->d_export, ci->sparse_slots * kSparseEntryWords))) break;
         ci->export_cap = ci->sparse_slots;
@@ -2671,14 +2846,14 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
       if ((rc = gpuagg_sparse_export(ci, ci->d_export, ci->export_cap, &m))) break;
       if ((rc = bind(c0))) break;
       if (m > ent_cap) {
-        dev_free(ent);
+        dev_free(c0, ent);
         ent_cap = 0;
         if ((rc = dev_alloc(c0, &ent, m * kSparseEntryWords))) break;
         ent_cap = m;
       }
       if (m) {
         if ((e = peer(ent, ci->d_export, ci->device, m * kSparseEntryWords * 8)) == hipSuccess)
-          e = hipStreamSynchronize(c0->stream);
+          e = x_sync(c0, c0->stream);
         if (e != hipSuccess) {
           rc = fail(c0, GPUAGG_EDEVICE, "merge: %s", hipGetErrorString(e));
           break;
@@ -2689,18 +2864,18 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
     if (c0->lat_enabled && ci->d_lat && c0->d_lat) {  // histograms / no_response: summed on the host
       unsigned long long a0[kLatStateWords], ai[kLatStateWords];
       if ((rc = bind(ci))) break;
-      HIPCHK(ci, hipMemcpy(ai, ci->d_lat, sizeof ai, hipMemcpyDeviceToHost));
+      HIPCHK(ci, x_copy(ci, ai, ci->d_lat, sizeof ai, hipMemcpyDeviceToHost));
       if ((rc = bind(c0))) break;
-      HIPCHK(c0, hipMemcpy(a0, c0->d_lat, sizeof a0, hipMemcpyDeviceToHost));
+      HIPCHK(c0, x_copy(c0, a0, c0->d_lat, sizeof a0, hipMemcpyDeviceToHost));
       for (uint32_t w = kLatHist; w < kLatStateWords; ++w) a0[w] += ai[w];
-      HIPCHK(c0, hipMemcpy(c0->d_lat, a0, sizeof a0, hipMemcpyHostToDevice));
+      HIPCHK(c0, x_copy(c0, c0->d_lat, a0, sizeof a0, hipMemcpyHostToDevice));
     }
     if ((rc = gpuagg_reset(ci))) break;
     if ((rc = bind(c0))) break;
   }
   cleanup();
   if (rc) return rc;
-  HIPCHK(c0, hipStreamSynchronize(c0->stream));
+  HIPCHK(c0, x_sync(c0, c0->stream));
   return GPUAGG_OK;
 }
 
@@ -2709,10 +2884,10 @@ int gpuagg_set_apiserver_ips(gpuagg_ctx *c, const uint32_t *ipv4, size_t n) {
   if (n > kLatMaxApi) return fail(c, GPUAGG_ECAPACITY, "%zu apiserver IPs exceed %u", n, kLatMaxApi);
   int rc = bind(c);
   if (rc) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight batches read the old set
+  HIPCHK(c, x_sync(c, c->stream));  // in-flight batches read the old set
   if (!c->d_api && (rc = dev_alloc(c, &c->d_api, kLatMaxApi))) return rc;
   c->api_ips.assign(ipv4, ipv4 + n);
-  if (n) HIPCHK(c, hipMemcpy(c->d_api, ipv4, n * 4, hipMemcpyHostToDevice));
+  if (n) HIPCHK(c, x_copy(c, c->d_api, ipv4, n * 4, hipMemcpyHostToDevice));
   return GPUAGG_OK;
 }
 
@@ -2737,14 +2912,14 @@ int gpuagg_ipcache_set(gpuagg_ctx *c, const uint32_t *ipv4, const uint32_t *iden
     tab[h] = uint4{ipv4[i], identity[i], meta_id[i], 0u};
     max_probe = std::max(max_probe, p);
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // in-flight decodes read the old image
+  HIPCHK(c, x_sync(c, c->stream));  // in-flight decodes read the old image
   if (cap != c->ipc_cap) {
-    dev_free(c->d_ipc);
+    dev_free(c, c->d_ipc);
     c->ipc_cap = 0;
     if ((rc = dev_alloc(c, &c->d_ipc, cap))) return rc;
     c->ipc_cap = cap;
   }
-  HIPCHK(c, hipMemcpy(c->d_ipc, tab.data(), cap * sizeof(uint4), hipMemcpyHostToDevice));
+  HIPCHK(c, x_copy(c, c->d_ipc, tab.data(), cap * sizeof(uint4), hipMemcpyHostToDevice));
   c->ipc_seed = seed;
   c->ipc_max_probe = max_probe;
   return GPUAGG_OK;
@@ -2777,7 +2952,8 @@ int gpuagg_hubble_decode_device(gpuagg_ctx *c, const gpuagg_columns *in, size_t 
   a.o_dmeta = out->dst_meta;
   a.o_kind = out->summary_kind;
   a.o_arg = out->summary_arg;
-  HIPCHK(c, launch_hubble(a, c->n_cu, c->stream));
+  if (c->cpu) c->cpu->hubble(a);
+  else HIPCHK(c, launch_hubble(a, c->n_cu, c->stream));
   return GPUAGG_OK;
 }
 
@@ -2807,8 +2983,8 @@ int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
   out->enabled = c->lat_enabled;
   if (!c->d_lat) return GPUAGG_OK;
   unsigned long long w[kLatStateWords];
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(w, c->d_lat, sizeof w, hipMemcpyDeviceToHost));
+  HIPCHK(c, x_sync(c, c->stream));
+  HIPCHK(c, x_copy(c, w, c->d_lat, sizeof w, hipMemcpyDeviceToHost));
   for (int i = 0; i < 11; ++i) {
     out->latency_buckets[i] = w[kLatHist + i];
     out->handshake_buckets[i] = w[kLatHandshake + i];
@@ -2831,7 +3007,8 @@ int gpuagg_get_stats(gpuagg_ctx *c, gpuagg_stats *out) {
 
 int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   if (!c) return GPUAGG_EINVAL;
-  c->timing = enabled != 0;
+  if (c->cpu) c->host_timing = enabled != 0;  // host wall time of the launches (no HIP events)
+  else c->timing = enabled != 0;
   if (!enabled) {
     c->stats.kernel_ms = 0;
     c->stats.fold_ms = 0;
@@ -2840,7 +3017,7 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   return GPUAGG_OK;
 }
 
-void *gpuagg_stream(gpuagg_ctx *c) { return c ? (void *)c->stream : nullptr; }
+void *gpuagg_stream(gpuagg_ctx *c) { return c && !c->cpu ? (void *)c->stream : nullptr; }
 
 const char *gpuagg_build_id(void) { return GPUAGG_BUILD_ID; }
 

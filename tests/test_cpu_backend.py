@@ -1,0 +1,147 @@
+"""The CPU backend (GPUAGG_FLAG_CPU_BACKEND, retina_amd/csrc/gpuagg_cpu.cpp): the same
+C ABI on host threads for nodes without a gfx950 device.  Runs here (no GPU) against the
+oracle with the GPU parity cases, and covers the other entry points the Go plugin uses:
+raw perf-record decode, sketches, node-apiserver latency, enriched flows, Hubble decode,
+the multi-context merge and slot retirement."""
+
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import decode as DEC
+from oracle import records as R
+from oracle import sketch as S
+from retina_amd import workloads as W
+
+from .helpers import diff_series, engine_series, make_engine, oracle_series
+from .test_gpu_parity import CASES, MIX, spec
+
+CPU = 128  # GPUAGG_FLAG_CPU_BACKEND
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib():
+    from retina_amd import _abi, build
+    build.build()
+    return _abi.load()
+
+
+@pytest.mark.parametrize("cid,sp,remote,gen", CASES, ids=[c[0] for c in CASES])
+def test_parity_vs_oracle(cid, sp, remote, gen):
+    pods = W.make_pods(400, seed=11)
+    recs = W.gen_records(30_000, pods, seed=zlib.crc32(cid.encode()) & 0xFFFF, **gen)
+    want = oracle_series(recs, pods, sp, remote)
+    got = engine_series(recs, pods, sp, remote, host_fed=True, chunks=3, flags=CPU)
+    assert got == want, diff_series(got, want)
+
+
+def test_empty_and_stats():
+    from retina_amd import GpuAgg
+    pods = W.make_pods(50, seed=1)
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, flags=CPU)
+    try:
+        assert g.snapshot() == {}
+        st = g.stats()
+        assert st["records"] == 0
+        assert GpuAgg  # the same class drives both backends
+    finally:
+        g.close()
+
+
+def test_raw_decode_path():
+    """Raw packetparser / dropreason records decoded on the host equal the oracle decode."""
+    pods = W.make_pods(300, seed=5)
+    sp = spec(["forward_count", "forward_bytes", "drop_count", "drop_bytes", "tcp_flag_gauges"],
+              ["namespace", "podname", "port"])
+    pk = W.gen_raw_packets(20_000, pods, seed=6, odd_frac=0.05)
+    dr = W.gen_raw_drops(10_000, pods, seed=7)
+    bp, _ = DEC.decode_packets(pk)
+    bd, _ = DEC.decode_drops(dr)
+    recs = W.Records(*[np.concatenate([getattr(bp, k), getattr(bd, k)]) for k in
+                       ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id")])
+    want = oracle_series(recs, pods, sp, False)
+    from retina_amd import _abi
+    g = make_engine(pods, sp, False, flags=CPU)
+    try:
+        g.submit_raw(_abi.RAW_PACKET, pk)
+        g.submit_raw(_abi.RAW_DROP, dr)
+        got = g.snapshot()
+    finally:
+        g.close()
+    assert got == want, diff_series(got, want)
+
+
+def test_sketches_bit_exact():
+    pods = W.make_pods(500, seed=8)
+    recs = W.gen_records(60_000, pods, seed=9, flows=20_000, n_dst=5_000)
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, flags=CPU, cms_depth=4, cms_width_log2=12, hll_precision=10)
+    try:
+        g.submit_numpy(recs)
+        g.sync()
+        cms, hll = g.cms_array(), g.hll_array()
+    finally:
+        g.close()
+    from .test_gpu_sketch import _src_slots
+    want = np.zeros((4, 1 << 12), np.uint32)
+    S.cms_update(want, recs.src_ip, recs.dst_ip, recs.ports, recs.meta & np.uint32(0xFF))
+    assert np.array_equal(cms, want)
+    regs = np.zeros_like(hll)
+    slot = _src_slots(pods, recs.src_ip)
+    ok = (slot >= 0) & (slot < regs.shape[0])
+    S.hll_update(regs, slot[ok], recs.dst_ip[ok], 10)
+    assert np.array_equal(hll, regs) and hll.any()
+
+
+def test_latency_matches_oracle():
+    from .latency_helpers import as_state, oracle_latency
+    api = [W.ip_le(10, 255, 0, 1), W.ip_le(10, 255, 0, 2)]
+    sp = [{"metric_name": "node_apiserver_latency"}, {"metric_name": "node_apiserver_handshake_latency"},
+          {"metric_name": "node_apiserver_no_response"}]
+    pods = W.make_pods(100, seed=11)
+    recs = W.gen_latency_records(400, pods, api, seed=12, background=3000)
+    want = as_state(oracle_latency(recs, api))
+    g = make_engine(pods, sp, False, flags=CPU)
+    try:
+        g.set_apiserver_ips(api)
+        n = len(recs.src_ip)
+        hb = g.alloc_batch(n)
+        for a, b in ((0, n // 3), (n // 3, n)):  # two batches: requests carried across
+            hb.fill(recs, a, b - a)
+            g.submit(hb, b - a)
+        st = g.latency_state()
+    finally:
+        g.close()
+    assert {k: st[k] for k in want} == want
+    assert want["latency_count"] > 0 and want["no_response"] > 0
+
+
+def test_merge_and_enrich():
+    """Two CPU contexts fed the direction-free shards and merged equal one context;
+    enriched-flow slots equal the IP cache's pods."""
+    from retina_amd import dist as D
+    pods = W.make_pods(400, seed=13)
+    recs = W.gen_records(40_000, pods, seed=14, **MIX)
+    sp = spec(["forward_count", "forward_bytes", "drop_count", "drop_bytes", "dns_request_count"],
+              ["ip", "namespace", "podname"], ["podname", "port"])
+    want = oracle_series(recs, pods, sp, True)
+    parts = [make_engine(pods, sp, True, recs=recs, flags=CPU) for _ in range(2)]
+    try:
+        for r, g in enumerate(parts):
+            g.submit_numpy(D.shard_records(recs, 2, r))
+        parts[0].merge_from(parts[1:])
+        got = parts[0].snapshot()
+        rest = parts[1].snapshot()
+        hb = parts[0].alloc_batch(1000)
+        hb.fill(recs, 0, 1000)
+        s, d = parts[0].submit_enrich(hb, 1000)
+    finally:
+        for g in parts:
+            g.close()
+    assert got == want, diff_series(got, want)
+    assert rest == {}
+    cache = R.build_cache([R.EndpointSpec(e.namespace, e.name, list(e.ips), e.owner_refs) for e in pods.endpoints])
+    from oracle import oracle as O
+    for i in range(1000):
+        obj = cache.get_obj_by_ip(O.int2ip(int(recs.src_ip[i])))
+        assert (s[i] >= 0) == isinstance(obj, O.RetinaEndpoint)
