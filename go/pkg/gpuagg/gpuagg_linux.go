@@ -319,13 +319,18 @@ func (g *gpuAgg) each(what string, fn func(ctx *C.gpuagg_ctx) C.int) error {
 }
 
 // Init creates one engine context per gfx950 device (PluginManager calls Stop before
-// Init on every reconcile, pluginmanager.go:91-112).
+// Init on every reconcile, pluginmanager.go:91-112).  A node without one gets a single
+// context on the library's CPU backend (GPUAGG_FLAG_CPU_BACKEND: the same plan and
+// results on host threads), so advanced metrics exist on every node as the reference's
+// CPU loop provides them (metrics_module.go:276-317).
 func (g *gpuAgg) Init() error {
 	g.mu.Lock()
 	defer g.mu.Unlock()
 	var ndev C.int
+	flags := C.uint32_t(0)
 	if rc := C.gpuagg_device_count(&ndev); rc != C.GPUAGG_OK || ndev == 0 {
-		return errors.New("gpuagg: no MI355X (gfx950) device")
+		g.l.Warn("gpuagg: no MI355X (gfx950) device: aggregating on the CPU backend")
+		ndev, flags = 1, C.GPUAGG_FLAG_CPU_BACKEND
 	}
 	remote := C.int32_t(0)
 	if g.cfg.RemoteContext {
@@ -334,7 +339,7 @@ func (g *gpuAgg) Init() error {
 	for dev := 0; dev < int(ndev); dev++ {
 		cfg := C.gpuagg_config{
 			abi_version: C.GPUAGG_ABI_VERSION, device: C.int32_t(dev), remote_context: remote,
-			max_slots: maxSlots, max_ips: 2 * maxSlots, sparse_capacity_log2: sparseLog2,
+			max_slots: maxSlots, max_ips: 2 * maxSlots, sparse_capacity_log2: sparseLog2, flags: flags,
 		}
 		d := &device{}
 		if rc := C.gpuagg_create(&cfg, &d.ctx); rc != C.GPUAGG_OK {

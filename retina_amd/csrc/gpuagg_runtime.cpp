@@ -14,6 +14,7 @@
 #include "../../include/gpuagg.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -153,6 +154,10 @@ struct gpuagg_ctx {
   // host memory and the launches run on host threads; no HIP call is made
   std::unique_ptr<gpuagg::cpu::Engine> cpu;
   bool host_timing = false;  // CPU backend: gpuagg_set_timing measures the host launches
+  // in-process RCCL communicators of the last gpuagg_merge this ctx was the target of
+  // (one per device of the merge, created once per device list)
+  std::vector<int> rccl_devs;
+  std::vector<ncclComm_t> rccl_comms;
   hipStream_t stream = nullptr;
   std::string err;
 
@@ -1448,6 +1453,8 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   if (c->enrich_done) {
     hipEventDestroy(c->enrich_done);
   }
+  for (ncclComm_t cm : c->rccl_comms) ncclCommDestroy(cm);
+  c->rccl_comms.clear();
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -2744,6 +2751,100 @@ int gpuagg_device_count(int *n) {
   return GPUAGG_OK;
 }
 
+// gpuagg_merge over RCCL (one process driving every GPU of the node): in one group, a
+// reduce to ctxs[0] per state array -- dense counters, count-min and the latency words
+// summed, HLL registers max-ed, in place on ctxs[0] -- and each context's exported
+// group-by entries sent to ctxs[0], which inserts-and-adds them; then ctxs[1..n) reset.
+// sum for counters and count-min, max for HLL; the collectives run over
+// xGMI between the devices.  Bit-exact with the peer-copy merge (linear sums, exact max).
+namespace {
+const char *nccl_err(ncclResult_t r) { return ncclGetErrorString(r); }
+
+int merge_rccl(gpuagg_ctx *const *ctxs, size_t n, const std::vector<int> &devs) {
+  gpuagg_ctx *c0 = ctxs[0];
+  int rc;
+  if (c0->rccl_devs != devs) {  // communicators for this device list (created once)
+    for (ncclComm_t cm : c0->rccl_comms) ncclCommDestroy(cm);
+    c0->rccl_comms.assign(n, nullptr);
+    c0->rccl_devs.clear();
+    ncclResult_t r = ncclCommInitAll(c0->rccl_comms.data(), (int)n, devs.data());
+    if (r != ncclSuccess) {
+      c0->rccl_comms.clear();
+      return fail(c0, GPUAGG_EDEVICE, "ncclCommInitAll(%zu devices): %s", n, nccl_err(r));
+    }
+    c0->rccl_devs = devs;
+  }
+  const std::vector<ncclComm_t> &comm = c0->rccl_comms;
+  // group-by entries: exported on every context first (the counts size the transfers)
+  std::vector<size_t> m(n, 0);
+  size_t total = 0;
+  for (size_t i = 1; i < n && c0->sparse_slots; ++i) {
+    gpuagg_ctx *ci = ctxs[i];
+    if ((rc = bind(ci))) return rc;
+    if (ci->export_cap < ci->sparse_slots) {
+      dev_free(ci, ci->d_export);
+      ci->export_cap = 0;
+      if ((rc = dev_alloc(ci, &ci->d_export, ci->sparse_slots * kSparseEntryWords))) return rc;
+      ci->export_cap = ci->sparse_slots;
+    }
+    if ((rc = gpuagg_sparse_export(ci, ci->d_export, ci->export_cap, &m[i]))) return rc;
+    total += m[i];
+  }
+  if ((rc = bind(c0))) return rc;
+  uint64_t *ent = nullptr;
+  if (total && (rc = dev_alloc(c0, &ent, total * kSparseEntryWords))) return rc;
+  const bool lat = c0->lat_enabled != 0;
+  for (size_t i = 0; i < n; ++i)
+    if (lat && !ctxs[i]->d_lat) {
+      dev_free(c0, ent);
+      return fail(c0, GPUAGG_ESTATE, "merge: ctx %zu has no latency state", i);
+    }
+  ncclResult_t r = ncclGroupStart();
+  size_t off = 0;
+  for (size_t i = 0; i < n && r == ncclSuccess; ++i) {
+    gpuagg_ctx *ci = ctxs[i];
+    hipSetDevice(ci->device);
+    auto reduce = [&](void *buf, size_t count, ncclDataType_t t, ncclRedOp_t op) {
+      if (r == ncclSuccess && count) r = ncclReduce(buf, buf, count, t, op, 0, comm[i], ci->stream);
+    };
+    reduce(ci->d_dense_cnt, c0->dense_len, ncclUint64, ncclSum);
+    reduce(ci->d_dense_byt, c0->dense_len, ncclUint64, ncclSum);
+    reduce(ci->d_cms, c0->cms_len, ncclUint32, ncclSum);
+    reduce(ci->d_hll, c0->hll_len, ncclUint8, ncclMax);
+    if (lat) reduce(ci->d_lat + kLatHist, kLatStateWords - kLatHist, ncclUint64, ncclSum);
+    if (i > 0 && m[i] && r == ncclSuccess)
+      r = ncclSend(ci->d_export, m[i] * kSparseEntryWords, ncclUint64, 0, comm[i], ci->stream);
+  }
+  for (size_t i = 1; i < n && r == ncclSuccess; ++i) {
+    if (!m[i]) continue;
+    hipSetDevice(c0->device);
+    r = ncclRecv(ent + off * kSparseEntryWords, m[i] * kSparseEntryWords, ncclUint64, (int)i, comm[0], c0->stream);
+    off += m[i];
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r == ncclSuccess) r = r2;
+  for (size_t i = 0; i < n; ++i) {  // every stream idle
+    hipSetDevice(ctxs[i]->device);
+    hipError_t e = hipStreamSynchronize(ctxs[i]->stream);
+    if (e != hipSuccess && r == ncclSuccess) {
+      dev_free(c0, ent);
+      return fail(c0, GPUAGG_EDEVICE, "merge: %s", hipGetErrorString(e));
+    }
+  }
+  if (r != ncclSuccess) {
+    dev_free(c0, ent);
+    return fail(c0, GPUAGG_EDEVICE, "merge over RCCL: %s", nccl_err(r));
+  }
+  if ((rc = bind(c0))) return rc;
+  rc = total ? gpuagg_sparse_import(c0, ent, total) : GPUAGG_OK;
+  dev_free(c0, ent);
+  if (rc) return rc;
+  for (size_t i = 1; i < n; ++i)
+    if ((rc = gpuagg_reset(ctxs[i]))) return rc;
+  return bind(c0);
+}
+}  // namespace
+
 int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
   if (!ctxs || !n || !ctxs[0]) return GPUAGG_EINVAL;
   gpuagg_ctx *c0 = ctxs[0];
@@ -2785,6 +2886,17 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
     HIPCHK(ci, x_sync(ci, ci->copy_stream));
   }
   if ((rc = bind(c0))) return rc;
+  // distinct devices: the RCCL collectives over xGMI (merge_rccl); contexts sharing a
+  // device (several engines on one GPU) take the peer-copy path below
+  if (!host) {
+    std::vector<int> devs;
+    for (size_t i = 0; i < n; ++i) devs.push_back(ctxs[i]->device);
+    std::vector<int> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    const char *mode = getenv("GPUAGG_MERGE");
+    if (std::unique(sorted.begin(), sorted.end()) == sorted.end() && !(mode && !strcmp(mode, "peer")))
+      return merge_rccl(ctxs, n, devs);
+  }
   const size_t tmp_bytes = std::max({c0->dense_len * 8, c0->cms_len * 4, c0->hll_len, (size_t)8});
   uint8_t *tmp = nullptr;
   if ((rc = dev_alloc(c0, &tmp, tmp_bytes))) return rc;

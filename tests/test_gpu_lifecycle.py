@@ -214,6 +214,32 @@ def test_merge_contexts_equals_single(gpu_device):
     assert min(out) > 100
 
 
+def test_merge_rccl_one_device(gpu_device):
+    """gpuagg_merge over in-process RCCL (contexts on distinct devices): on a one-GPU lease
+    the communicator has one rank -- ncclCommInitAll, the in-place reduces of every state
+    array and the entry transfer run, and the state is unchanged (a second merge reuses the
+    communicator).  Multi-device RCCL merges are unmeasured here; the peer-copy path (same
+    device) is test_merge_contexts_equals_single."""
+    pods = W.make_pods(500, seed=83)
+    recs = W.gen_records(200_000, pods, seed=84, drop_frac=0.1, retrans_frac=0.05, dns_frac=0.1,
+                         udp_frac=0.1, n_queries=300)
+    sketch = dict(cms_depth=4, cms_width_log2=14, hll_precision=9)
+    for remote, spec, kw in ((False, FWD_DROP + W.C5_SPEC, sketch), (True, W.C1_REMOTE, {})):
+        g = make_engine(pods, spec, remote, gpu_device, recs, **kw)
+        try:
+            _submit(g, recs, gpu_device)
+            want = g.snapshot()
+            wc = g.cms_array() if kw else None
+            g.merge_from([])  # one context: a one-rank communicator
+            g.merge_from([])
+            got = g.snapshot()
+            if kw:
+                assert np.array_equal(g.cms_array(), wc)
+        finally:
+            g.close()
+        assert got == want and len(got) > 100, diff_series(got, want)
+
+
 @pytest.mark.parametrize("remote,spec", [(False, FWD_DROP + W.C5_SPEC), (True, W.C1_REMOTE)],
                          ids=["local", "remote"])
 def test_exposition_text_matches_oracle(gpu_device, remote, spec):
