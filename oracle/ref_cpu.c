@@ -119,6 +119,10 @@ typedef struct {
   size_t ndns, dns_cap;
   metric_t m[32];
   int nm;
+  /* tuned mode: hash-partitioned integer tables waiting to be rendered (ref_finish) */
+  void *tparts;
+  int ntparts;
+  int tleader[32];
   /* flattened output */
   char **out_metric, **out_labels;
   uint64_t *out_value;
@@ -607,9 +611,15 @@ typedef struct {
   const uint8_t *lead; /* [metric]: first metric of its group (same key -> count and bytes) */
   const uint32_t *src, *dst, *bytes, *meta, *ports, *dns_id;
   size_t a, b;
-  imap_t map;
+  imap_t *maps; /* one table per hash partition (nparts), so the merge is partitioned */
+  int nparts;
   int bad;
 } tjob_t;
+
+static int part_of(const ikey_t *k, int np) { return (int)((ikey_hash(k) >> 48) % (uint64_t)np); }
+static void tjob_add(tjob_t *j, const ikey_t *k, uint64_t c, uint64_t b) {
+  imap_add(&j->maps[j->nparts > 1 ? part_of(k, j->nparts) : 0], k, c, b);
+}
 
 static void tuned_flow(tjob_t *j, size_t i) {
   const ref_t *r = j->r;
@@ -657,7 +667,7 @@ static void tuned_flow(tjob_t *j, size_t i) {
         key.w[0] = (uint32_t)k | ((uint32_t)dest << 18);
         side_key(&key.w[1], opts, dest ? dip : sip, dest ? dep : sep, dest ? dport : sport, proto);
         key.w[7] = dns + 1;
-        imap_add(&j->map, &key, 1, 0);
+        tjob_add(j, &key, 1, 0);
         continue;
       }
       for (int side = 0; side < 2; ++side) {
@@ -667,12 +677,12 @@ static void tuned_flow(tjob_t *j, size_t i) {
         if (m->family == F_TCPFLAGS) {
           for (int f = 0; f < nflags; ++f) {
             key.w[0] = (uint32_t)k | ((uint32_t)fi[f] << 8) | ((uint32_t)dest << 18);
-            imap_add(&j->map, &key, 1, 0);
+            tjob_add(j, &key, 1, 0);
           }
           continue;
         }
         key.w[0] = (uint32_t)k | ((m->family == F_DROP ? reason : 0u) << 8) | ((uint32_t)dest << 18);
-        imap_add(&j->map, &key, 1, add);
+        tjob_add(j, &key, 1, add);
       }
       continue;
     }
@@ -682,20 +692,33 @@ static void tuned_flow(tjob_t *j, size_t i) {
     if (m->family == F_TCPFLAGS) {
       for (int f = 0; f < nflags; ++f) {
         key.w[0] = (uint32_t)k | ((uint32_t)fi[f] << 8);
-        imap_add(&j->map, &key, 1, 0);
+        tjob_add(j, &key, 1, 0);
       }
       continue;
     }
     key.w[0] = (uint32_t)k | ((m->family == F_DROP ? reason : 0u) << 8) |
                ((m->family == F_DNS ? 0u : tdir) << 16);
     if (m->family == F_DNS) key.w[7] = dns + 1;
-    imap_add(&j->map, &key, 1, add);
+    tjob_add(j, &key, 1, add);
   }
 }
 
 #include <pthread.h>
 static void *tuned_worker(void *p) {
   tjob_t *j = p;
+  /* presized tables (about two updates per record, spread over the partitions): no
+   * rehashing while the range streams through */
+  size_t want = 4096;
+  const size_t est = 4 * (j->b - j->a) / (size_t)(j->nparts > 0 ? j->nparts : 1);
+  while (want < est && want < ((size_t)1 << 22)) want <<= 1;
+  for (int q = 0; q < j->nparts; ++q) {
+    imap_t *m = &j->maps[q];
+    m->cap = want;
+    m->n = 0;
+    m->k = malloc(want * sizeof(ikey_t));
+    m->v = malloc(want * 2 * sizeof(uint64_t));
+    m->used = calloc(want, 1);
+  }
   for (size_t i = j->a; i < j->b; ++i) tuned_flow(j, i);
   return NULL;
 }
@@ -766,11 +789,57 @@ static void tuned_render(ref_t *r, int k, const ikey_t *key, uint64_t v) {
   update(m, lab, v);
 }
 
-/* Tuned CPU path over nthreads threads; accumulates into the same series as ref_process. */
+/* Renders the pending partitioned tables into the series (ref_finish, or before the
+ * next tuned call). */
+static void tuned_flush(ref_t *r) {
+  imap_t *parts = r->tparts;
+  if (!parts) return;
+  for (int p = 0; p < r->ntparts; ++p) {
+    for (size_t i = 0; i < parts[p].cap; ++i)
+      if (parts[p].used[i]) {
+        const int lk = (int)(parts[p].k[i].w[0] & 0xFF);
+        for (int k = 0; k < r->nm; ++k)
+          if (r->m[k].active && r->tleader[k] == lk)
+            tuned_render(r, k, &parts[p].k[i], parts[p].v[2 * i + (r->m[k].is_bytes ? 1 : 0)]);
+      }
+    imap_free(&parts[p]);
+  }
+  free(parts);
+  r->tparts = NULL;
+  r->ntparts = 0;
+}
+
+/* Phase 2 of the tuned path: partition p merges every thread's entries whose key hash
+ * falls in p, so the merge runs on all threads (the per-thread tables were split by hash
+ * at the end of phase 1). */
+typedef struct {
+  tjob_t *jobs;
+  int nthreads, p;
+  imap_t out;
+} mjob_t;
+static void *merge_worker(void *arg) {
+  mjob_t *mj = arg;
+  mj->out = mj->jobs[0].maps[mj->p];  /* thread 0's table of the partition is the base */
+  memset(&mj->jobs[0].maps[mj->p], 0, sizeof(imap_t));
+  for (int t = 1; t < mj->nthreads; ++t) {
+    imap_t *m = &mj->jobs[t].maps[mj->p];
+    for (size_t i = 0; i < m->cap; ++i)
+      if (m->used[i]) imap_add(&mj->out, &m->k[i], m->v[2 * i], m->v[2 * i + 1]);
+    imap_free(m);
+  }
+  return NULL;
+}
+
+/* Tuned CPU path over nthreads threads; accumulates into the same series as ref_process.
+ * Phase 1: each thread aggregates its record range into its own integer-keyed table;
+ * phase 2: the tables are merged by hash partition, one partition per thread.  The
+ * integer keys are rendered to label strings by ref_finish (as the engine renders at
+ * gpuagg_snapshot, outside the aggregation it is compared with). */
 int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const uint32_t *bytes,
                       const uint32_t *meta, const uint32_t *ports, const uint32_t *dns_id, size_t n,
                       int nthreads) {
   ref_t *r = h;
+  tuned_flush(r);
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   uint8_t *api = calloc(r->neps + 1, 1);
@@ -778,7 +847,7 @@ int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const u
   /* metrics whose label tuples coincide (forward_count / forward_bytes with the same
    * options, ...) share one key: the leader's table entry carries count and bytes */
   uint8_t lead[32];
-  int leader[32];
+  int *leader = r->tleader;
   for (int k = 0; k < r->nm; ++k) {
     const metric_t *m = &r->m[k];
     leader[k] = k;
@@ -808,6 +877,8 @@ int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const u
     j->dns_id = dns_id;
     j->a = n * (size_t)t / (size_t)nthreads;
     j->b = n * (size_t)(t + 1) / (size_t)nthreads;
+    j->nparts = nthreads;
+    j->maps = calloc((size_t)nthreads, sizeof(imap_t));
     if (t && pthread_create(&th[t], NULL, tuned_worker, j)) {
       tuned_worker(j); /* no thread: run it here */
       th[t] = 0;
@@ -818,21 +889,36 @@ int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const u
   for (int t = 1; t < nthreads; ++t) {
     if (th[t]) pthread_join(th[t], NULL);
     bad |= jobs[t].bad;
-    /* per-thread tables merged into thread 0's */
-    for (size_t i = 0; i < jobs[t].map.cap; ++i)
-      if (jobs[t].map.used[i])
-        imap_add(&jobs[0].map, &jobs[t].map.k[i], jobs[t].map.v[2 * i], jobs[t].map.v[2 * i + 1]);
-    imap_free(&jobs[t].map);
   }
-  if (!bad)
-    for (size_t i = 0; i < jobs[0].map.cap; ++i)
-      if (jobs[0].map.used[i]) {
-        const int lk = (int)(jobs[0].map.k[i].w[0] & 0xFF);
-        for (int k = 0; k < r->nm; ++k)
-          if (r->m[k].active && leader[k] == lk)
-            tuned_render(r, k, &jobs[0].map.k[i], jobs[0].map.v[2 * i + (r->m[k].is_bytes ? 1 : 0)]);
-      }
-  imap_free(&jobs[0].map);
+  mjob_t *mj = calloc((size_t)nthreads, sizeof(mjob_t));
+  for (int p = 0; p < nthreads; ++p) {
+    mj[p].jobs = jobs;
+    mj[p].nthreads = nthreads;
+    mj[p].p = p;
+    th[p] = 0;
+    if (p && !bad && pthread_create(&th[p], NULL, merge_worker, &mj[p])) {
+      merge_worker(&mj[p]);
+      th[p] = 0;
+    }
+  }
+  if (!bad) merge_worker(&mj[0]);
+  imap_t *parts = calloc((size_t)nthreads, sizeof(imap_t));
+  for (int p = 0; p < nthreads; ++p) {
+    if (p && th[p]) pthread_join(th[p], NULL);
+    parts[p] = mj[p].out;
+  }
+  for (int t = 0; t < nthreads; ++t) {
+    for (int p = 0; p < nthreads; ++p) imap_free(&jobs[t].maps[p]);
+    free(jobs[t].maps);
+  }
+  if (!bad) {
+    r->tparts = parts;
+    r->ntparts = nthreads;
+  } else {
+    for (int p = 0; p < nthreads; ++p) imap_free(&parts[p]);
+    free(parts);
+  }
+  free(mj);
   free(jobs);
   free(th);
   free(api);
@@ -842,6 +928,7 @@ int ref_process_tuned(void *h, const uint32_t *src, const uint32_t *dst, const u
 /* Flattens the series: labels are "\x1f"-separated values (label names are fixed per metric). */
 size_t ref_finish(void *h) {
   ref_t *r = h;
+  tuned_flush(r);
   size_t n = 0;
   for (int k = 0; k < r->nm; ++k) n += r->m[k].series.n;
   r->out_metric = calloc(n + 1, sizeof(char *));
@@ -874,6 +961,11 @@ int ref_series(void *h, size_t i, const char **metric, const char **labels, uint
 void ref_destroy(void *h) {
   ref_t *r = h;
   if (!r) return;
+  if (r->tparts) {
+    imap_t *parts = r->tparts;
+    for (int p = 0; p < r->ntparts; ++p) imap_free(&parts[p]);
+    free(parts);
+  }
   for (int k = 0; k < r->nm; ++k) smap_free(&r->m[k].series, 0);
   smap_free(&r->ip_to_ep, 0);
   for (size_t i = 0; i < r->neps; ++i) free(r->eps[i]);
