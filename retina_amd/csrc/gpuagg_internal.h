@@ -164,7 +164,11 @@ constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^2
 // the runtime takes the smallest that keeps the windows <= kMaxSpillWindows, so the fold
 // partitions per window -- and the partial copies summed after the fold -- are fewest.
 constexpr uint32_t kFoldWindowShift = 13, kFoldWindowBins = 1u << kFoldWindowShift;
+#ifdef EXP_FOLD_SHIFT_MIN
+constexpr uint32_t kFoldWindowShiftMin = EXP_FOLD_SHIFT_MIN;
+#else
 constexpr uint32_t kFoldWindowShiftMin = 10;
+#endif
 
 // ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------
 // Bucketized cuckoo: 2 candidate buckets of 2 keys (8 B, one ds_read_b64 each),

@@ -2680,7 +2680,11 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
   // with tickets: one launch (fold + partial sums + the tier-1 copies in extra blocks)
+#ifdef EXP_NO_FOLD_TICKET
+  const bool one = false;
+#else
   const bool one = a.stage_b && a.fold_ticket;
+#endif
   const uint32_t fa_x = (a.lds_bins + 1023) / 1024, fa_y = 8;
   const uint32_t na = one && a.stage_a ? fa_x * fa_y : 0u;
   hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks + na), dim3(1024), (size_t)8 * W, st,

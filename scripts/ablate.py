@@ -88,6 +88,13 @@ def main():
         run("c4-zipf", W.LOCAL_FWD_DROP, pods, cols_z, n)
         del cols_z
     run("remote", W.C1_REMOTE, pods, cols, n // 10, remote=True)
+    if not ONLY or any(v.startswith("c4r") for v in ONLY):  # C4 remote: Zipf 5-tuples, wide keys
+        c4 = W.CONFIGS["c4-remote"]
+        cols_z, _ = gen_device_records(n, pods, c4["seed"], dev, dict(c4["gen"]))
+        run("c4r", W.C1_REMOTE, pods, cols_z, n, remote=True)
+        run("c4r-nohot", W.C1_REMOTE, pods, cols_z, n, remote=True, flags=16)
+        run("c4r-nolists", W.C1_REMOTE, pods, cols_z, n, remote=True, flags=32)
+        del cols_z
     if not ONLY or "c2-lat" in ONLY:  # C2 + the latency join's filter pass (no apiserver rows)
         tcp_id = torch.zeros(n, dtype=torch.int32, device=dev)
         t_ns = torch.arange(n, dtype=torch.int64, device=dev) * 1000
