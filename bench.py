@@ -164,9 +164,15 @@ def pmc_traffic(cfg_name: str, kernel: str, build_id: str):
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 
 
-def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = 1 << 22):
-    """Host-fed throughput: two pinned batches (pre-filled from the workload) submitted
-    alternately, gpuagg_submit's H2D copy of one overlapping the other's aggregation."""
+# The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go: batchCapacity = 1 << 20
+# records per pinned batch, submitted when full or every flushInterval = 100 ms).
+GO_BATCH = 1 << 20
+
+
+def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
+    """Host-fed throughput at the Go plugin's batch size: two pinned batches (pre-filled
+    from the workload) submitted alternately through gpuagg_submit, the H2D copy of one
+    overlapping the other's aggregation."""
     import torch
     n = min(batch, n_total)
     hbs = [g.alloc_batch(n), g.alloc_batch(n)]
@@ -187,6 +193,39 @@ def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = 1 << 22):
             "note": "pinned host batches through gpuagg_submit (PCIe H2D included; not `value`)"}
 
 
+def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, launches: int = 100,
+                        batch: int = GO_BATCH):
+    """Device-resident launches of the Go plugin's batch size (GO_BATCH records each): the
+    per-launch fixed cost next to the headline's one big launch.  fixed_ms = the kernel's
+    time per launch minus the time the same records take at the full-size launch's rate
+    (LDS image fill, bin zeroing and flush, staged copies, spill folds do not shrink with
+    the batch)."""
+    from retina_amd import GpuAgg
+    n = min(batch, n_total)
+    sub = GpuAgg.device_columns(*[t[:n] for t in cols])
+    g.submit_device(sub, n)
+    g.sync()
+    g.set_timing(False)
+    g.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        g.submit_device(sub, n)
+    g.sync()
+    wall = (time.perf_counter() - t0) / launches
+    st = g.stats()
+    g.set_timing(False)
+    k = st["kernel_launches"] or 1
+    kms = st["kernel_ms"] / k
+    other = st["fold_ms"] / k + (st["sketch_ms"] / st["sketch_launches"] if st["sketch_launches"] else 0.0)
+    at_full_rate = full_kernel_ms * n / n_total
+    return {"batch_records": n, "launches": launches, "records_per_s": n / wall, "ms_per_launch": wall * 1e3,
+            "kernel_ms": kms, "other_kernels_ms": other,
+            "kernel_frac": bpr * n / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "fixed_ms": kms - at_full_rate,
+            "note": "device-resident %d-record launches (Go batchCapacity); fixed_ms = kernel ms per launch "
+                    "- the same records at the full-size launch's rate" % n}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,6 +237,8 @@ def main():
                     help="records in the tuned CPU baseline sample (go-shaped: 1/8 of it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
+    ap.add_argument("--no-production", action="store_true",
+                    help="skip the Go-batch-size (1M-record) device-resident launches")
     args = ap.parse_args()
 
     import torch
@@ -321,6 +362,8 @@ def main():
         },
         "build_id": build_id,
     }
+    if rank == 0 and world == 1 and not args.no_production and n > GO_BATCH:
+        result["production"] = production_geometry(g, cols, n, bpr, stats["kernel_ms"] / max(1, stats["kernel_launches"]))
     if rank == 0 and world == 1 and not args.no_host_fed:
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -160,15 +160,7 @@ constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^2
 // bin's window is a shift.  Spill entries are u32: the bin's offset in its window
 // (13 bits) | bytes << 13; a packet of >= 2^19 bytes adds its bytes with a global
 // atomic and spills 0.
-// Fold windows of 2^win_shift bins, win_shift in [kFoldWindowShiftMin, kFoldWindowShift]:
-// the runtime takes the smallest that keeps the windows <= kMaxSpillWindows, so the fold
-// partitions per window -- and the partial copies summed after the fold -- are fewest.
 constexpr uint32_t kFoldWindowShift = 13, kFoldWindowBins = 1u << kFoldWindowShift;
-#ifdef EXP_FOLD_SHIFT_MIN
-constexpr uint32_t kFoldWindowShiftMin = EXP_FOLD_SHIFT_MIN;
-#else
-constexpr uint32_t kFoldWindowShiftMin = 10;
-#endif
 
 // ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------
 // Bucketized cuckoo: 2 candidate buckets of 2 keys (8 B, one ds_read_b64 each),

@@ -21,6 +21,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gpuagg_internal.h"
 #include "gpuagg_launch.h"
@@ -66,9 +67,14 @@ struct DevSparse {
   unsigned long long *lists;
   uint32_t *lctr;
   uint32_t lcap;
-  // per-workgroup LDS cache of hot group-by keys (aggregate_kernel; null: none)
+  // per-workgroup LDS cache of hot group-by keys (aggregate_kernel)
   struct HotKey *hot;
-  uint32_t hot_n;  // entries, a power of two
+  uint32_t hot_n;  // entries, a power of two (0: no cache)
+  // doorkeeper bitmap (LDS, 2^door_log2 bits): a wide key may claim a cache entry only
+  // when its bit was already set, i.e. (up to collisions) on its second sighting in the
+  // workgroup, so the keys seen once -- the long tail -- do not take the entries
+  uint32_t *door;
+  uint32_t door_log2;  // 0: no doorkeeper
 };
 
 // One cached key: tag 0 free, 1 being claimed, 2 published (key words final).
@@ -77,16 +83,15 @@ struct HotKey {
 };
 static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp");
 
-// Adds (c, b) to key (k0, k1, k2) in this workgroup's LDS hot-key cache if the key is
-// there or a free entry can be claimed (two candidate entries; only a key seen more
-// than once in the wave claims); false: the caller adds
-// to the HBM table.  No lane ever waits: an entry being claimed by another lane is
-// skipped.  Under skew (C4's Zipf flows) the hot keys then cost LDS atomics instead of
-// memory-side atomics serialised on one table slot; the cache is added to the table
-// once per workgroup at the end (hot_flush).
-__device__ __forceinline__ bool hot_add(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
-                                        uint64_t b, bool may_claim) {
-  const uint32_t h = (uint32_t)key_hash(k0, k1, k2);
+// Adds (c, b) to key (k0, k1, k2) (hash h) in this workgroup's LDS hot-key cache if the
+// key is there or a free entry can be claimed (two candidate entries); false: the caller
+// adds to the lists / HBM table.  No lane ever waits: an entry being claimed by another
+// lane is skipped.  Under skew (C4's Zipf flows) the hot keys then cost LDS atomics
+// instead of memory-side atomics serialised on one table slot; the cache is added to the
+// table once per workgroup at the end.  Who may claim is the caller's policy (a key seen
+// more than once in the wave, or a key the doorkeeper bitmap has seen before).
+__device__ __forceinline__ bool hot_add(const DevSparse &s, uint32_t h, uint64_t k0, uint64_t k1, uint64_t k2,
+                                        uint64_t c, uint64_t b, bool may_claim) {
 #pragma unroll
   for (uint32_t q = 0; q < 2; ++q) {
     HotKey *e = &s.hot[(h + q * 0x9E37u) & (s.hot_n - 1u)];
@@ -154,6 +159,7 @@ struct KArgs {
   // LDS fill counters start from spill_count / sp_counts instead of 0
   uint32_t accum;
   uint32_t hot_n;  // LDS hot-key cache entries of aggregate_kernel (0: none)
+  uint32_t door_log2;  // doorkeeper bits of the hot-key cache (0: every key may claim)
   Plan p;
 };
 
@@ -301,11 +307,11 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
 // workgroup's list for the key's table segment (LDS fill counter, one 32-byte store) and
 // sparse_fold_wide_kernel later adds every list into its segment in LDS -- instead of a
 // memory-side CAS + two reads + two adds per cold key.  A full list, or a count / byte
-// sum too wide for the entry, goes to the table directly (exact).
-__device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t c,
-                                            uint64_t b) {
+// sum too wide for the entry, goes to the table directly (exact).  kh = key_hash(k0, k1, k2).
+__device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t kh, uint64_t k0, uint64_t k1, uint64_t k2,
+                                            uint64_t c, uint64_t b) {
   if (c < (1ULL << (64 - kWideCountShift)) && b < (1ULL << kWideCountShift)) {
-    const uint32_t w = ((uint32_t)key_hash(k0, k1, k2) & s.mask) >> s.seg_log2;
+    const uint32_t w = ((uint32_t)kh & s.mask) >> s.seg_log2;
     const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
     if (pos < s.lcap) {
       ulonglong2 *e = (ulonglong2 *)(s.lists + ((size_t)w * s.lcap + pos) * kWideEntryWords);
@@ -482,7 +488,17 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
     // C4's Zipf flows, the whole kernel's time).  Lanes with the same key meet in the LDS
     // hot-key cache (any key may claim a free entry: the frequent ones arrive first) or
     // append separately and are summed by the fold.
-    if (valid && !(s.hot && hot_add(s, k0, k1, k2, 1, b, true))) wide_append(s, k0, k1, k2, 1, b);
+    if (!valid) return;
+#ifdef EXP_SKIP_INSERT
+    if (k0 != 12345) return;
+#endif
+    const uint64_t kh = key_hash(k0, k1, k2);
+    bool claim = true;
+    if (s.door_log2) {  // doorkeeper: claim on the second sighting
+      const uint32_t bit = (uint32_t)(kh >> 40) & ((1u << s.door_log2) - 1u);
+      claim = (atomicOr(&s.door[bit >> 5], 1u << (bit & 31u)) >> (bit & 31u)) & 1u;
+    }
+    if (!(s.hot_n && hot_add(s, (uint32_t)kh, k0, k1, k2, 1, b, claim))) wide_append(s, kh, k0, k1, k2, 1, b);
     return;
   }
   const uint64_t vm = __ballot(valid);
@@ -518,7 +534,8 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
   }
   // only keys that occur more than once in the wave (the de-dup count) claim a hot-key
   // entry: under skew those are the hot ones; uniform keys (C1) then cost two tag reads
-  if (keep && !(s.hot && hot_add(s, k0, k1, k2, c, b, c > 1))) sparse_add(s, k0, k1, k2, c, b);
+  if (keep && !(s.hot_n && hot_add(s, (uint32_t)key_hash(k0, k1, k2), k0, k1, k2, c, b, c > 1)))
+    sparse_add(s, k0, k1, k2, c, b);
 }
 
 // One record through every metric group.  Converged: every lane of the wave runs it
@@ -769,19 +786,24 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
     const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
     sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
   }
-  // hot-key cache after the segment counters (8-byte aligned)
+  // hot-key cache after the segment counters (8-byte aligned), then the doorkeeper bitmap
   HotKey *hot = (HotKey *)&lds[a.lds_bins + kLdsExtraWords + (a.sp_nwin + 1) / 2];
   for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
-  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and the tags too)
+  uint32_t *door = (uint32_t *)(hot + a.hot_n);
+  const uint32_t door_words = a.door_log2 ? 1u << (a.door_log2 - 5) : 0u;
+  for (uint32_t i = threadIdx.x; i < door_words; i += blockDim.x) door[i] = 0u;
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr, tags, bitmap)
   DevSparse s = a.s;
+  // LDS pointers set unconditionally (hot_n / door_log2 = 0 disable them), so every access
+  // through them compiles to ds_* instructions, not flat ones
+  s.lctr = sctr;
+  s.hot = hot;
+  s.hot_n = a.hot_n;
+  s.door = door;
+  s.door_log2 = a.door_log2;
   if (a.sp_lists) {  // this workgroup's lists: compact u64 keys or wide 4-word entries
     s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * (s.compact ? 1u : kWideEntryWords);
-    s.lctr = sctr;
     s.lcap = a.sp_cap;
-  }
-  if (a.hot_n) {
-    s.hot = hot;
-    s.hot_n = a.hot_n;
   }
   for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
                         [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports,
@@ -793,11 +815,11 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   if (a.hot_n) {  // the cached keys, once per workgroup (dense_flush's barrier precedes):
     // into the segment lists with their counts, or straight into the table
     DevSparse g = s;
-    g.hot = nullptr;
+    g.hot_n = 0;
     for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) {
       const HotKey e = hot[i];
       if (e.tag != 2ULL) continue;
-      if (g.lists) wide_append(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
+      if (g.lists) wide_append(g, key_hash(e.k0, e.k1, e.k2), e.k0, e.k1, e.k2, e.cnt, e.byt);
       else sparse_add(g, e.k0, e.k1, e.k2, e.cnt, e.byt);
     }
     __syncthreads();
@@ -1418,14 +1440,31 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t vlast = vend - 1;  // vn >= 1
     uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
     uint4 ns = rec_ld(&s4[vl]), nd = rec_ld(&d4[vl]), nbv = rec_ld(&b4[vl]), nm = rec_ld(&m4[vl]);
+#ifdef EXP_PREFETCH2
+    // two steps of record loads in flight (128 B per lane)
+    vl = vwave + blockDim.x + lane < vend ? vwave + blockDim.x + lane : vlast;
+    uint4 ns2 = rec_ld(&s4[vl]), nd2 = rec_ld(&d4[vl]), nb2 = rec_ld(&b4[vl]), nm2 = rec_ld(&m4[vl]);
+#endif
     for (uint64_t vw = vwave; vw < vend; vw += blockDim.x) {
       const bool act = vw + lane < vend;
       const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
+#ifdef EXP_PREFETCH2
+      ns = ns2;
+      nd = nd2;
+      nbv = nb2;
+      nm = nm2;
+      vl = vw + 2 * blockDim.x + lane < vend ? vw + 2 * blockDim.x + lane : vlast;
+      ns2 = rec_ld(&s4[vl]);
+      nd2 = rec_ld(&d4[vl]);
+      nb2 = rec_ld(&b4[vl]);
+      nm2 = rec_ld(&m4[vl]);
+#else
       vl = vw + blockDim.x + lane < vend ? vw + blockDim.x + lane : vlast;  // clamped: no branch
       ns = rec_ld(&s4[vl]);
       nd = rec_ld(&d4[vl]);
       nbv = rec_ld(&b4[vl]);
       nm = rec_ld(&m4[vl]);
+#endif
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t sl[8];
       iv.lookup8(ip, act, sl);
@@ -1531,6 +1570,7 @@ struct SketchK {
   uint32_t hll_slots; // slots covered by the registers
   const uint8_t *ipl; // LDS image of every pod IP (source lookups), or null: HBM table
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (sketch_stage_kernel<2, .>)
   // LDS staging of list appends (sketch_stage_kernel): per count-min window sbc u16 and
   // per HLL super-window sbh u32 entries (powers of two), flushed every `round` records
   // per lane (2 or 4) as contiguous runs
@@ -1684,94 +1724,184 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
 // Staged scatter (the default when LDS allows): appends land in per-window LDS staging
 // rings and are written out as contiguous runs once per round, so every list write is a
 // coalesced wave store instead of one L2 request per 2- or 4-byte entry (PMC on the
-// unstaged kernel: 45 B written per record for 12 B of list entries).  Positions are
-// reserved exactly as in the unstaged kernel, so the lists are identical; an entry whose
-// position is past the staging ring is stored directly, a full list falls back to the
-// global atomic.
-struct StagedLists {
-  const SketchK &k;
-  uint32_t *wcnt, *hcnt, *wfl, *hfl;  // fill counters and flushed positions (LDS)
-  uint16_t *cst;                      // [nwin][sbc] staging (LDS)
-  uint32_t *hst;                      // [hnsup][sbh] staging (LDS)
-  uint16_t *mine;
-  uint32_t *hmine;
-  uint32_t wmask, hi_bits, omask;
-  __device__ __forceinline__ void record(uint32_t s, uint32_t d, uint32_t ports, uint32_t meta,
-                                         const Lk &ls, bool stage) const {
-    if (k.depth) {
-      const uint64_t base = cms_base(s, d, ports, meta_proto(meta));
-#pragma unroll 4
-      for (uint32_t r = 0; r < k.depth; ++r) {
-        const uint32_t col = cms_col(base, r, wmask);
-        const uint32_t w = (r << hi_bits) | (col >> k.wshift);
-        const uint32_t pos = atomicAdd(&wcnt[w], 1u);
-        const uint16_t e = (uint16_t)(col & omask);
-        if (pos >= k.cap) atomicAdd(&k.cms[((size_t)r << k.wlog2) + col], 1u);
-        else if (stage && pos - wfl[w] < k.sbc) cst[w * k.sbc + (pos & (k.sbc - 1u))] = e;
-        else mine[(size_t)w * k.cap + pos] = e;
-      }
-    }
-    if (k.p && ls.slot >= 0 && (uint32_t)ls.slot < k.hll_slots) {
-      const uint64_t h = hll_hash(d);
-      const uint32_t idx = (uint32_t)(h >> (64 - k.p));
-      const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
-      const uint32_t w = (uint32_t)ls.slot >> k.hsshift;
-      const uint32_t pos = atomicAdd(&hcnt[w], 1u);
-      const uint32_t e = (((uint32_t)ls.slot & ((1u << k.hsshift) - 1u)) << (k.p + 6)) | (idx << 6) | rho;
-      if (pos >= k.hcap) hll_update(k.hll, k.p, ls.slot, d);
-      else if (stage && pos - hfl[w] < k.sbh) hst[w * k.sbh + (pos & (k.sbh - 1u))] = e;
-      else hmine[(size_t)w * k.hcap + pos] = e;
-    }
-  }
-  // all threads, between barriers: write each window's staged run [flushed, filled)
-  __device__ __forceinline__ void flush() const {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-    for (uint32_t w = wave; w < k.nwin; w += nwaves) {
-      const uint32_t f = wfl[w], c = min(wcnt[w], k.cap), e = min(c, f + k.sbc);
-      for (uint32_t p = f + lane; p < e; p += 64) mine[(size_t)w * k.cap + p] = cst[w * k.sbc + (p & (k.sbc - 1u))];
-      if (lane == 0) wfl[w] = c;
-    }
-    for (uint32_t w = wave; w < k.hnsup; w += nwaves) {
-      const uint32_t f = hfl[w], c = min(hcnt[w], k.hcap), e = min(c, f + k.sbh);
-      for (uint32_t p = f + lane; p < e; p += 64) hmine[(size_t)w * k.hcap + p] = hst[w * k.sbh + (p & (k.sbh - 1u))];
-      if (lane == 0) hfl[w] = c;
-    }
-  }
-};
-
-// LDS words of the staged kernel before the IP image (counters, flushed positions, rings)
+// unstaged kernel: 45 B written per record for 12 B of list entries).
+//
+// Per-round counters: rc[w] counts window w's appends of this round (reset by the flush)
+// and rb[w] is the list length at the round's start, so an append's ring slot is the
+// value its LDS atomic returns -- one LDS round trip per update, no read of rb.  Every
+// update of a record (kD count-min rows and the HLL entry) is computed first and the
+// atomics of two records are issued back to back, so 2 x (kD + 1) LDS round trips are in
+// flight per lane instead of one after another.  A position past the ring (rare: rings
+// hold 1.5 x a round's mean + 64) is stored straight into the list at rb + pos; a list
+// position past the capacity falls back to the global atomic (exact).
+// kIp: source lookup 0 HBM table, 1 LDS cuckoo image, 2 LDS radix image.
+// kD: count-min depth fixed at compile time (4), or 0 = k.depth.
 __host__ __device__ inline uint32_t stage_words(uint32_t nwin, uint32_t hnsup, uint32_t sbc, uint32_t sbh) {
-  return ((2u * (nwin + hnsup) + 3u) & ~3u) + ((nwin * sbc / 2u + 3u) & ~3u) + hnsup * sbh;
+  // rc, rb per window + hc, hb per super-window; u16 rings (+ one dummy u32); u32 rings
+  // (+ 64 dummies)
+  return ((2u * (nwin + hnsup) + 3u) & ~3u) + ((nwin * sbc / 2u + 1u + 3u) & ~3u) + hnsup * sbh + 64u;
 }
 
-template <bool kLdsIp>
+template <int kIp, int kD>
 __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-  uint32_t *wcnt = sm, *hcnt = sm + k.nwin, *wfl = hcnt + k.hnsup, *hfl = wfl + k.nwin;
-  uint16_t *cst = (uint16_t *)(sm + ((2u * (k.nwin + k.hnsup) + 3u) & ~3u));
-  uint32_t *hst = (uint32_t *)cst + ((k.nwin * k.sbc / 2u + 3u) & ~3u);
-  const uint32_t img_off = stage_words(k.nwin, k.hnsup, k.sbc, k.sbh);
-  const uint32_t *keys = sm + img_off;
-  const uint16_t *vals = (const uint16_t *)((const uint8_t *)keys + ipl_vals_offset(k.ipl_nb));
-  for (uint32_t i = threadIdx.x; i < 2u * (k.nwin + k.hnsup); i += blockDim.x) sm[i] = 0u;
-  if (kLdsIp)
+  const uint32_t nw = k.nwin, nh = k.hnsup, sbc = k.sbc, sbh = k.sbh;
+  uint32_t *rc = sm, *rb = sm + nw, *hc = rb + nw, *hb = hc + nh;
+  uint16_t *cst = (uint16_t *)(sm + ((2u * (nw + nh) + 3u) & ~3u));
+  const uint32_t cdummy = nw * sbc;  // u16 index of the rings' dummy entry
+  uint32_t *hst = (uint32_t *)cst + ((nw * sbc / 2u + 1u + 3u) & ~3u);
+  const uint32_t hdummy = nh * sbh;  // 64 u32 dummies follow the HLL rings
+  const uint32_t img_off = stage_words(nw, nh, sbc, sbh);
+  const uint8_t *img = (const uint8_t *)(sm + img_off);
+  for (uint32_t i = threadIdx.x; i < 2u * (nw + nh); i += blockDim.x) sm[i] = 0u;
+  if (kIp)
     for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
       ((uint4 *)(sm + img_off))[i] = ((const uint4 *)k.ipl)[i];
   __syncthreads();
-  auto lookup = [&](uint32_t ip) {
-    if (kLdsIp) {
-      const uint32_t v = vals[ipl_probe_index(keys, k.ipl_nb, k.ipl_seed, ip)];
-      return Lk{v == kIplNoSlot ? -1 : (int32_t)v, 0u};
+  const uint32_t D = kD ? (uint32_t)kD : k.depth;
+  const uint32_t wmask = (1u << k.wlog2) - 1u, hi_bits = k.wlog2 - k.wshift, omask = (1u << k.wshift) - 1u;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint16_t *mine = k.lists + (size_t)blockIdx.x * nw * k.cap;
+  uint32_t *hmine = k.hlists + (size_t)blockIdx.x * nh * k.hcap;
+  const IplView<kIp == 2> iv{img, k.ipl_nb, k.ipl_seed, k.ipl_npfx, k.ipl_pfx[0], k.ipl_pfx[1], k.ipl_pfx[2],
+                             k.ipl_pfx[3]};
+  auto src_slot = [&](uint32_t ip) -> uint32_t {  // slot or >= hll_slots
+    if (kIp) return iv.lookup(ip);
+    const Lk l = k.p ? ip_lookup(k.t, ip) : Lk{-1, 0};
+    return l.slot < 0 ? 0xFFFFFFFFu : (uint32_t)l.slot;
+  };
+  // count-min entry that cannot be staged or listed: the global atomic
+  auto cms_direct = [&](uint32_t w, uint32_t e) {
+    const uint32_t r = w >> hi_bits, col = ((w & ((1u << hi_bits) - 1u)) << k.wshift) | e;
+    atomicAdd(&k.cms[((size_t)r << k.wlog2) + col], 1u);
+  };
+  auto hll_direct = [&](uint32_t wh, uint32_t e) {
+    const uint32_t slot = (wh << k.hsshift) | (e >> (k.p + 6));
+    const size_t byte = ((size_t)slot << k.p) + ((e >> 6) & ((1u << k.p) - 1u));
+    const uint32_t rho = e & 63u, sh = (uint32_t)(byte & 3) * 8u;
+    uint32_t *word = k.hll + (byte >> 2);
+    uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((old >> sh) & 0xFFu) < rho) {
+      const uint32_t prev = atomicCAS(word, old, (old & ~(0xFFu << sh)) | (rho << sh));
+      if (prev == old) break;
+      old = prev;
     }
-    return k.p ? ip_lookup(k.t, ip) : Lk{-1, 0};
+  };
+  // R records of this lane (act: real records) through every update: all positions
+  // reserved first, then the ring stores (dummy entries absorb the rest), then the rare
+  // overflow path for the whole wave at once
+  constexpr int kMaxD = kD ? kD : 8;
+  auto records = [&](auto R, const uint32_t *s, const uint32_t *d, const uint32_t *pt, const uint32_t *mt,
+                     const bool *act) {
+    constexpr int NR = decltype(R)::value;
+    uint32_t we[NR][kMaxD], pos[NR][kMaxD], he[NR], hw[NR], hp[NR];
+    bool hv[NR];
+    uint32_t sl[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) sl[j] = k.p ? src_slot(s[j]) : 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      if (D) {
+        const uint64_t base = cms_base(s[j], d[j], pt[j], meta_proto(mt[j]));
+#pragma unroll
+        for (int r = 0; r < kMaxD; ++r) {
+          if (!kD && (uint32_t)r >= D) break;
+          const uint32_t col = cms_col(base, (uint32_t)r, wmask);
+          we[j][r] = ((((uint32_t)r << hi_bits) | (col >> k.wshift)) << 16) | (col & omask);
+        }
+      }
+      hv[j] = act[j] && k.p && sl[j] < k.hll_slots;
+      hw[j] = 0u;
+      he[j] = 0u;
+      if (k.p) {
+        const uint64_t h = hll_hash(d[j]);
+        const uint32_t idx = (uint32_t)(h >> (64 - k.p));
+        const uint32_t rho = (uint32_t)__builtin_clzll((h << k.p) | (1ULL << (k.p - 1))) + 1u;
+        hw[j] = hv[j] ? sl[j] >> k.hsshift : 0u;
+        he[j] = ((sl[j] & ((1u << k.hsshift) - 1u)) << (k.p + 6)) | (idx << 6) | rho;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      if (D) {
+#pragma unroll
+        for (int r = 0; r < kMaxD; ++r) {
+          if (!kD && (uint32_t)r >= D) break;
+          pos[j][r] = act[j] ? atomicAdd(&rc[we[j][r] >> 16], 1u) : 0xFFFFFFFFu;
+        }
+      }
+      hp[j] = hv[j] ? atomicAdd(&hc[hw[j]], 1u) : 0xFFFFFFFFu;
+    }
+    bool slow = false;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      if (D) {
+#pragma unroll
+        for (int r = 0; r < kMaxD; ++r) {
+          if (!kD && (uint32_t)r >= D) break;
+          const uint32_t w = we[j][r] >> 16, p = pos[j][r];
+          const bool ring = p < sbc;
+          cst[ring ? w * sbc + p : cdummy] = (uint16_t)we[j][r];
+          slow |= act[j] & !ring;
+        }
+      }
+      const bool hring = hp[j] < sbh;
+      hst[hring ? hw[j] * sbh + hp[j] : hdummy + lane] = he[j];
+      slow |= hv[j] & !hring;
+    }
+    if (__builtin_expect(__ballot(slow) != 0, 0)) {  // past a ring: list at rb + pos, or global
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        if (D) {
+#pragma unroll
+          for (int r = 0; r < kMaxD; ++r) {
+            if (!kD && (uint32_t)r >= D) break;
+            const uint32_t w = we[j][r] >> 16, p = pos[j][r];
+            if (!act[j] || p < sbc) continue;
+            const uint32_t lp = rb[w] + p;
+            if (lp < k.cap) mine[(size_t)w * k.cap + lp] = (uint16_t)we[j][r];
+            else cms_direct(w, we[j][r] & 0xFFFFu);
+          }
+        }
+        if (!hv[j] || hp[j] < sbh) continue;
+        const uint32_t lp = hb[hw[j]] + hp[j];
+        if (lp < k.hcap) hmine[(size_t)hw[j] * k.hcap + lp] = he[j];
+        else hll_direct(hw[j], he[j]);
+      }
+    }
+  };
+  // all threads, between barriers: each window's staged run to its list (positions past
+  // the capacity: the global atomic), then the round counters reset
+  auto flush = [&]() {
+    const uint32_t wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    for (uint32_t w = wave; w < nw; w += nwaves) {
+      const uint32_t n = rc[w], b = rb[w], m = min(n, sbc);
+      for (uint32_t p = lane; p < m; p += 64) {
+        const uint16_t e = cst[w * sbc + p];
+        if (b + p < k.cap) mine[(size_t)w * k.cap + b + p] = e;
+        else cms_direct(w, e);
+      }
+      if (lane == 0) {
+        rb[w] = b + n;
+        rc[w] = 0u;
+      }
+    }
+    for (uint32_t w = wave; w < nh; w += nwaves) {
+      const uint32_t n = hc[w], b = hb[w], m = min(n, sbh);
+      for (uint32_t p = lane; p < m; p += 64) {
+        const uint32_t e = hst[w * sbh + p];
+        if (b + p < k.hcap) hmine[(size_t)w * k.hcap + b + p] = e;
+        else hll_direct(w, e);
+      }
+      if (lane == 0) {
+        hb[w] = b + n;
+        hc[w] = 0u;
+      }
+    }
   };
   const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
   const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
-  const StagedLists L{k, wcnt, hcnt, wfl, hfl, cst, hst,
-                      k.lists + (size_t)blockIdx.x * k.nwin * k.cap,
-                      k.hlists + (size_t)blockIdx.x * k.hnsup * k.hcap, (1u << k.wlog2) - 1u,
-                      k.wlog2 - k.wshift, (1u << k.wshift) - 1u};
-  const bool need_ports = k.depth != 0 && k.ports;
+  const bool need_ports = D != 0 && k.ports;
   uint64_t tail = start;
   if (start + 4 <= end) {
     const uint64_t v0 = start >> 2, vend = v0 + ((end - start) >> 2);
@@ -1789,7 +1919,7 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
     // block-uniform trip count: every thread reaches the flush barriers
     for (uint64_t vb = v0; vb < vend; vb += blockDim.x) {
       const uint64_t v = vb + threadIdx.x;
-      const bool act = v < vend;
+      const bool a = v < vend;
       const uint4 vs = ns, vd = nd, vm = nm, vp = np;
       const uint64_t vn = v + blockDim.x;
       if (vn < vend) {
@@ -1798,36 +1928,42 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
         nm = rec_ld(&m4[vn]);
         np = need_ports ? rec_ld(&p4[vn]) : z4;
       }
-      if (act) {
-        const Lk l0 = lookup(vs.x), l1 = lookup(vs.y);
-        L.record(vs.x, vd.x, vp.x, vm.x, l0, true);
-        L.record(vs.y, vd.y, vp.y, vm.y, l1, true);
+      const bool act[2] = {a, a};
+      {
+        const uint32_t s[2] = {vs.x, vs.y}, d[2] = {vd.x, vd.y}, pt[2] = {vp.x, vp.y}, mt[2] = {vm.x, vm.y};
+        records(std::integral_constant<int, 2>{}, s, d, pt, mt, act);
       }
       if (k.round == 2) {
         __syncthreads();
-        L.flush();
+        flush();
         __syncthreads();
       }
-      if (act) {
-        const Lk l2 = lookup(vs.z), l3 = lookup(vs.w);
-        L.record(vs.z, vd.z, vp.z, vm.z, l2, true);
-        L.record(vs.w, vd.w, vp.w, vm.w, l3, true);
+      {
+        const uint32_t s[2] = {vs.z, vs.w}, d[2] = {vd.z, vd.w}, pt[2] = {vp.z, vp.w}, mt[2] = {vm.z, vm.w};
+        records(std::integral_constant<int, 2>{}, s, d, pt, mt, act);
       }
       __syncthreads();
-      L.flush();
+      flush();
       __syncthreads();
     }
     tail = start + ((end - start) & ~3ULL);
   }
-  for (uint64_t i = tail + threadIdx.x; i < end; i += blockDim.x) {  // < 4 records: unstaged
-    const uint32_t s = k.src[i];
-    L.record(s, k.dst[i], need_ports ? k.ports[i] : 0u, k.meta[i], lookup(s), false);
+  // < 4 records left (the last workgroup's chunk): one more staged round
+  if (tail < end) {  // block-uniform
+    const uint64_t i = tail + threadIdx.x;
+    const bool a = i < end;
+    const uint32_t s[1] = {a ? k.src[i] : 0u}, d[1] = {a ? k.dst[i] : 0u},
+                   pt[1] = {a && need_ports ? k.ports[i] : 0u}, mt[1] = {a ? k.meta[i] : 0u};
+    const bool act[1] = {a};
+    records(std::integral_constant<int, 1>{}, s, d, pt, mt, act);
+    __syncthreads();
+    flush();
+    __syncthreads();
   }
-  __syncthreads();
-  for (uint32_t w = threadIdx.x; w < k.nwin; w += blockDim.x)
-    k.counts[(size_t)blockIdx.x * k.nwin + w] = wcnt[w] < k.cap ? wcnt[w] : k.cap;
-  for (uint32_t w = threadIdx.x; w < k.hnsup; w += blockDim.x)
-    k.hcounts[(size_t)blockIdx.x * k.hnsup + w] = hcnt[w] < k.hcap ? hcnt[w] : k.hcap;
+  for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
+    k.counts[(size_t)blockIdx.x * nw + w] = rb[w] < k.cap ? rb[w] : k.cap;
+  for (uint32_t w = threadIdx.x; w < nh; w += blockDim.x)
+    k.hcounts[(size_t)blockIdx.x * nh + w] = hb[w] < k.hcap ? hb[w] : k.hcap;
 }
 
 // HLL level 2: workgroup (super-window s, part b) reads scatter lists b, b + hb2, ... of
@@ -2042,7 +2178,8 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   hipError_t e;
   size_t scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   // source lookups in an LDS image of the IP table when it fits next to the counters
-  const bool lds_ip = a.ipl && a.hll_p && scatter_lds + a.ipl_bytes <= kLdsBytes;
+  const bool lds_ip_any = a.ipl && a.hll_p && scatter_lds + a.ipl_bytes <= kLdsBytes;
+  const bool lds_ip = lds_ip_any;  // (staged kernel: either image form)
   if (lds_ip) {
     k.ipl = a.ipl;
     k.ipl_nb = a.ipl_nb;
@@ -2053,16 +2190,22 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   // 16-byte loads need aligned columns and workgroup chunks of whole vectors
   const bool vec = a.chunk % 4 == 0 && ((uintptr_t)k.src | (uintptr_t)k.dst | (uintptr_t)k.meta |
                                         (uintptr_t)(k.ports ? k.ports : k.src)) % 16 == 0;
-  // staged scatter: rings sized for one round's expected appends x 2 (+ 64), flushed every
-  // 4 records per lane, or every 2 when the 4-record rings do not fit
+  // staged scatter: rings sized for a round's mean appends x 1.5 + 64 (the overflow goes
+  // straight to the list), flushed every 4 records per lane, or every 2 when the 4-record
+  // rings do not fit; sources looked up in the radix image when the pod IPs allow one
   bool staged = false;
   if (vec && (!a.cms_depth || a.nwin) && (!a.hll_p || a.hll_nsup) && (a.nwin || a.hll_nsup)) {
+    const int ip_kind = lds_ip ? (a.ipl_radix ? 2 : 1) : 0;
+    if (lds_ip) {
+      k.ipl_npfx = a.ipl_npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) k.ipl_pfx[j] = a.ipl_pfx[j];
+    }
     const uint32_t img = lds_ip ? a.ipl_bytes : 0u;
     for (uint32_t round : {4u, 2u}) {
       const uint64_t per_round = 1024ull * round;
       auto ring = [](uint64_t mean) {
         uint32_t r = 64;
-        while (r < 2 * mean + 64) r <<= 1;
+        while (r < mean + mean / 2 + 64) r <<= 1;
         return r;
       };
       const uint32_t sbc = a.nwin ? ring(per_round * a.cms_depth / a.nwin) : 0u;
@@ -2072,17 +2215,27 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
       k.sbc = sbc;
       k.sbh = sbh;
       k.round = round;
-      const void *fn = lds_ip ? (const void *)sketch_stage_kernel<true> : (const void *)sketch_stage_kernel<false>;
+      const bool d4 = a.cms_depth == 4;
+      const void *fn = ip_kind == 2 ? (d4 ? (const void *)sketch_stage_kernel<2, 4> : (const void *)sketch_stage_kernel<2, 0>)
+                     : ip_kind == 1 ? (d4 ? (const void *)sketch_stage_kernel<1, 4> : (const void *)sketch_stage_kernel<1, 0>)
+                                    : (d4 ? (const void *)sketch_stage_kernel<0, 4> : (const void *)sketch_stage_kernel<0, 0>);
       if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
-      if (lds_ip) hipLaunchKernelGGL((sketch_stage_kernel<true>), dim3(a.blocks), dim3(1024), lds, st, k);
-      else hipLaunchKernelGGL((sketch_stage_kernel<false>), dim3(a.blocks), dim3(1024), lds, st, k);
+      if (ip_kind == 2 && d4) hipLaunchKernelGGL((sketch_stage_kernel<2, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (ip_kind == 2) hipLaunchKernelGGL((sketch_stage_kernel<2, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (ip_kind == 1 && d4) hipLaunchKernelGGL((sketch_stage_kernel<1, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (ip_kind == 1) hipLaunchKernelGGL((sketch_stage_kernel<1, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (d4) hipLaunchKernelGGL((sketch_stage_kernel<0, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else hipLaunchKernelGGL((sketch_stage_kernel<0, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
       if ((e = hipGetLastError()) != hipSuccess) return e;
-      names = lds_ip ? "sketch_stage_kernel<true>" : "sketch_stage_kernel<false>";
+      names = std::string("sketch_stage_kernel<") + std::to_string(ip_kind) + ", " + (d4 ? "4" : "0") + ">";
       staged = true;
       break;
     }
   }
   if (!staged) {
+  // the unstaged kernel probes the cuckoo image only: a radix image is looked up in HBM
+  const bool lds_ip = lds_ip_any && !a.ipl_radix;
+  if (!lds_ip) scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   const void *fn = vec ? (lds_ip ? (const void *)sketch_scatter_kernel<true, true>
                                  : (const void *)sketch_scatter_kernel<true, false>)
                        : (lds_ip ? (const void *)sketch_scatter_kernel<false, true>
@@ -2166,29 +2319,21 @@ __device__ __forceinline__ void stage_reduce_a(const uint32_t *stage, uint32_t n
 // List (A-workgroup l, window w) holds only window w's updates, so every entry is read
 // once.  Workgroup b folds window b % nwin over partition b / nwin of the lists; with
 // W = 8192 bins (64 KB of LDS) two workgroups fit a CU, and the runtime sizes the grid
-// to 2 x CUs so the fold runs in a single wave of the chip.
-//
-// One launch ends the step: blocks [nfold, gridDim.x) sum the tier-1 workgroups' LDS bin
-// copies (stage_a, disjoint bins), and a window's partition partials are summed in the
-// same launch by the window's last-arriving partition (agent-scope release -> ticket ->
-// acquire, cdna_hip_programming.md section 5 "in-launch split-K reduction"): the partials
-// are nparts x 2^win_shift words (24 KiB at C2), so the serial combine costs less than
-// the extra launch it replaces.
+// to 2 x CUs so the fold runs in a single wave of the chip.  With `stage` the window
+// partial is stored whole and stage_reduce_kernel sums the partitions (with the tier-1
+// copies, one launch).  Round 3 measured two alternatives slower on one box
+// (profiles/round3/e3a_c2_tail.jsonl): the partials summed in this launch by each window's
+// last-arriving partition (agent-scope ticket; fold 0.036 -> 0.106 ms at W = 8192), and
+// smaller windows with fewer partitions each (W = 2048: main kernel 0.41 -> 0.45 ms).
 __global__ __launch_bounds__(1024) void spill_window_kernel(
     const uint32_t *spill, const uint32_t *spill_count, uint32_t n_lists,
     uint32_t spill_cap, uint32_t lo0, uint64_t dense_len, uint32_t W, uint32_t nwin, DevDense d,
-    unsigned long long *stage, uint32_t *ticket, uint32_t nfold, const uint32_t *stage_a, uint32_t ncopies,
-    uint32_t stride, uint32_t L4, uint32_t na_x, uint32_t ny, Plan p) {
+    unsigned long long *stage) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
-  if (blockIdx.x >= nfold) {  // the tier-1 copies (independent of the fold)
-    const uint32_t ba = blockIdx.x - nfold;
-    stage_reduce_a(stage_a, ncopies, stride, L4, p, d, ba % na_x, ba / na_x, ny);
-    return;
-  }
   const uint32_t b = blockIdx.x;
   const uint32_t w = b % nwin;
   const uint32_t part = b / nwin;
-  const uint32_t nparts = nfold / nwin;
+  const uint32_t nparts = gridDim.x / nwin;
   const uint64_t lo = (uint64_t)lo0 + (uint64_t)w * W;
   const uint64_t hi = lo + W < dense_len ? lo + W : dense_len;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) win[i] = 0ULL;
@@ -2255,38 +2400,9 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   }
   }  // long lists
   __syncthreads();
-  if (stage) {  // staged: this window partial, whole; the window's last partition sums them
+  if (stage) {  // staged: this window partial, whole, for stage_reduce_kernel
     uint4 *dst = (uint4 *)(stage + ((size_t)b * W));
     for (uint32_t i = threadIdx.x; i < W / 2; i += blockDim.x) dst[i] = ((const uint4 *)win)[i];
-    if (!ticket) return;  // summed by stage_reduce_kernel
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t t = __hip_atomic_fetch_add(&ticket[w], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      win[0] = t == nparts - 1 ? 1ULL : 0ULL;  // "last" through the window's LDS
-    }
-    __syncthreads();
-    const bool last = win[0] != 0ULL;
-    if (!last) return;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ticket[w] = 0u;  // ready for the next launch (zeroed at allocation)
-    }
-    __syncthreads();
-    // this window's bins: only this workgroup writes them in this launch (plain RMW)
-    for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
-      unsigned long long cnt = 0, byt = 0;
-      for (uint32_t q = 0; q < nparts; ++q) {
-        const unsigned long long v = stage[(size_t)(q * nwin + w) * W + i];
-        cnt += v >> kLdsCountShift;
-        byt += v & kLdsBytesMask;
-      }
-      if (cnt) d.cnt[lo + i] += cnt;
-      if (byt) d.byt[lo + i] += byt;
-    }
     return;
   }
   for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) {
@@ -2556,9 +2672,19 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.hot_n = a.hot_n;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
-  const size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
-                             : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4 +
-                                   (a.hot_n ? 4 + (size_t)a.hot_n * kHotKeyBytes : 0);
+  size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
+                       : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4 +
+                             (a.hot_n ? 4 + (size_t)a.hot_n * kHotKeyBytes : 0);
+  // the hot-key cache's doorkeeper bitmap takes what LDS is left (2^13 .. 2^18 bits) on the
+  // wide-key list path, where any key may otherwise claim an entry
+  k.door_log2 = 0;
+  if (!a.tier1 && a.hot_n && k.sp_nwin && !a.sparse.compact)
+    for (uint32_t l = 18; l >= 13; --l)
+      if (lds + ((size_t)1 << (l - 3)) <= kLdsBytes) {
+        k.door_log2 = l;
+        lds += (size_t)1 << (l - 3);
+        break;
+      }
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (a.dns_compact && a.dense_ng ? 300 : 0) + (int)a.dense_ng;
@@ -2679,21 +2805,10 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  // with tickets: one launch (fold + partial sums + the tier-1 copies in extra blocks)
-#ifdef EXP_NO_FOLD_TICKET
-  const bool one = false;
-#else
-  const bool one = a.stage_b && a.fold_ticket;
-#endif
-  const uint32_t fa_x = (a.lds_bins + 1023) / 1024, fa_y = 8;
-  const uint32_t na = one && a.stage_a ? fa_x * fa_y : 0u;
-  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks + na), dim3(1024), (size_t)8 * W, st,
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
                      (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
-                     a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b,
-                     one ? a.fold_ticket : nullptr, a.win_blocks, a.stage_a, a.blocks, a.stage_a_stride,
-                     a.lds_bins, fa_x, fa_y, a.plan);
+                     a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (one) return hipSuccess;
   return reduce(a.stage_b != nullptr);
 }
 

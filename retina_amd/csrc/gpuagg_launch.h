@@ -66,7 +66,6 @@ struct LaunchArgs {
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;
   uint64_t *stage_b;        // fold: [win_blocks][2^win_shift] window partials
-  uint32_t *fold_ticket;    // [kMaxSpillWindows] zeroed: partials summed in the fold launch
   // compact group-by keys bucketed per table segment (null: inserted in place)
   uint64_t *sp_lists;       // [blocks][sp_nwin][sp_cap] keys
   uint32_t *sp_counts;      // [blocks][sp_nwin]
@@ -193,6 +192,8 @@ struct SketchArgs {
   uint32_t *hll_lists2, *hll_counts2;
   const uint8_t *ipl;               // LDS image of every pod IP for the source lookup, or null
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
+  bool ipl_radix;                   // the image is the radix form (ipl_npfx / ipl_pfx)
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];
 };
 // *kernels: the pass's kernels in rocprofv3 spelling joined by "+"
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels);

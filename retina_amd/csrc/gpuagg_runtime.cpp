@@ -230,6 +230,8 @@ struct gpuagg_ctx {
   uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
   size_t ipl_all_alloc = 0;
   uint32_t ipl_all_nb = 0, ipl_all_seed = 0, ipl_all_bytes = 0;
+  bool ipl_all_radix = false;  // radix form (<= kIprMaxPfx /16 prefixes), else cuckoo
+  uint32_t ipl_all_npfx = 0, ipl_all_pfx[kIprMaxPfx] = {};
   uint32_t ipl_nb = 0, ipl_seed = 0, ipl_bytes = 0;
   // the tier-1 image is the radix form (ipr_build) when the pod IPs allow it
   bool ipl_radix = false;
@@ -303,7 +305,6 @@ struct gpuagg_ctx {
   hipEvent_t enrich_done = nullptr;
   uint64_t *d_stage_b = nullptr;
   size_t stage_b_alloc = 0;
-  uint32_t *d_fold_ticket = nullptr;  // spill_window_kernel's per-window tickets
   // raw perf-record decode (gpuagg_decode.hip)
   uint64_t *d_decode_oor = nullptr;  // out-of-range field counter
   std::vector<std::array<hipEvent_t, 2>> pending_decode;  // decode start, end
@@ -755,6 +756,9 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     s.ipl_nb = c->ipl_all_nb;
     s.ipl_seed = c->ipl_all_seed;
     s.ipl_bytes = c->ipl_all_bytes;
+    s.ipl_radix = c->ipl_all_radix;
+    s.ipl_npfx = c->ipl_all_npfx;
+    for (uint32_t j = 0; j < kIprMaxPfx; ++j) s.ipl_pfx[j] = c->ipl_all_pfx[j];
   }
   // HLL bucketing: fine windows of 2^hll_shift pods (128 KiB of registers, the fold's
   // LDS), super-windows of 2^hll_sshift pods (~16 of them, the scatter's lists); pod bits
@@ -962,7 +966,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 // Launches whose list folds may wait for one fold_pending (see Pending).
 constexpr uint64_t kDeferLaunches = 16;
 // Device memory for the wide-key segment lists of one ctx (32-byte entries).
-constexpr uint64_t kWideListBytes = 2ull << 30;
+constexpr uint64_t kWideListBytes = 8ull << 30;
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
@@ -1142,11 +1146,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       Geom g;
       if (c->dense_len > a.lds_bins) {
         const uint64_t rem = c->dense_len - a.lds_bins;
-        // smallest window (fewest fold partitions per window, so fewest partial copies)
-        // that keeps the windows within the kernels' LDS counters; staged C5 rings need the
-        // windows unchanged (kStage sizes them per window)
-        uint32_t shift = kFoldWindowShiftMin;
-        while (shift < kFoldWindowShift && ((rem + (1ull << shift) - 1) >> shift) > kMaxSpillWindows) ++shift;
+        const uint32_t shift = kFoldWindowShift;
         const uint32_t nwin = (uint32_t)((rem + (1ull << shift) - 1) >> shift);
         const uint64_t cap = ((2 * budget / nwin + 4096) + 3) & ~3ULL;
         if (nwin <= kMaxSpillWindows && cap < (1u << 24)) {  // 24-bit index math in the kernels
@@ -1222,11 +1222,6 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       const size_t nb_stage = (size_t)a.win_blocks << a.win_shift;
       if ((rc = ensure_buf(c, &c->d_stage_b, &c->stage_b_alloc, nb_stage))) return rc;
       a.stage_b = c->d_stage_b;
-      if (!c->d_fold_ticket) {  // per-window tickets, reset by each window's last partition
-        if ((rc = dev_alloc(c, &c->d_fold_ticket, kMaxSpillWindows))) return rc;
-        HIPCHK(c, x_set_async(c, c->d_fold_ticket, 0, kMaxSpillWindows * 4, c->stream));
-      }
-      a.fold_ticket = c->d_fold_ticket;
     }
     a.sp_lists = nullptr;
     a.sp_counts = nullptr;
@@ -1436,7 +1431,6 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c, c->d_stage_b);
   dev_free(c, c->d_sk_lists);
   dev_free(c, c->d_sk_counts);
-  dev_free(c, c->d_fold_ticket);
   dev_free(c, c->d_sp_lists);
   dev_free(c, c->d_sp_counts);
   dev_free(c, c->d_hll_lists);
@@ -1882,17 +1876,25 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     std::vector<std::pair<uint32_t, uint32_t>> ents;
     for (const auto &kv : last) ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
     IplImage im;
-    if (ipl_build(ents, &im)) {
-      const uint32_t bytes = (uint32_t)im.bytes.size();
+    IprImage ir;
+    // radix form when the pod IPs allow one (two dependent u16 reads per source and a
+    // smaller image, leaving LDS for larger staging rings), else the cuckoo image
+    const bool radix = !(c->cfg.flags & GPUAGG_FLAG_LDS_CUCKOO) && ipr_build(ents, &ir);
+    if (radix || ipl_build(ents, &im)) {
+      const std::vector<uint8_t> &img = radix ? ir.bytes : im.bytes;
+      const uint32_t bytes = (uint32_t)img.size();
       if (bytes > c->ipl_all_alloc) {
         dev_free(c, c->d_ipl_all);
         c->ipl_all_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
         c->ipl_all_alloc = bytes;
       }
-      HIPCHK(c, x_copy(c, c->d_ipl_all, im.bytes.data(), bytes, hipMemcpyHostToDevice));
-      c->ipl_all_nb = im.nb;
-      c->ipl_all_seed = im.seed;
+      HIPCHK(c, x_copy(c, c->d_ipl_all, img.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_all_radix = radix;
+      c->ipl_all_nb = radix ? 0 : im.nb;
+      c->ipl_all_seed = radix ? 0 : im.seed;
+      c->ipl_all_npfx = radix ? ir.npfx : 0;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) c->ipl_all_pfx[j] = radix ? ir.pfx[j] : kIprNoPfx;
       c->ipl_all_bytes = bytes;
     }
   }

@@ -22,10 +22,13 @@ def main():
     out, kernel, records, build_id, dirs = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5:]
     parts = [p for p in kernel.split("+") if p]
     vals = {p: defaultdict(list) for p in parts}
+    every = defaultdict(lambda: defaultdict(list))  # every kernel of the step, by name
     names = set()
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
+                short = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("gpuagg::", "")
+                every[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
                 for p in parts:
                     if p in row["Kernel_Name"]:
                         names.add(row["Kernel_Name"])
@@ -55,6 +58,16 @@ def main():
     if "SQ_LDS_IDX_ACTIVE" in avg and avg["SQ_LDS_IDX_ACTIVE"]:
         res.setdefault("derived", {})["lds_bank_conflict_frac"] = (
             avg.get("SQ_LDS_BANK_CONFLICT", 0) / avg["SQ_LDS_IDX_ACTIVE"])
+    # per-kernel averages (every kernel of the step, the fold / reduce passes included), with
+    # the same HBM correction, so a step's traffic can be split by kernel
+    per = {}
+    for k, cv in every.items():
+        a = {c: sum(v) / len(v) for c, v in cv.items()}
+        if "FETCH_SIZE" in a:
+            a["hbm_bytes_corrected"] = 2.0 * a["FETCH_SIZE"] * 1024 + a.get("WRITE_SIZE", 0.0) * 1024
+            a["hbm_bytes_per_record"] = a["hbm_bytes_corrected"] / records
+        per[k] = a
+    res["per_kernel"] = per
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
