@@ -464,6 +464,25 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
   return v;
 }
 
+// One wide-key update (count 1, bytes b) on the list path: no wave de-duplication (its
+// leader loop costs one round per distinct key of a hash-bucket collision -- ~30 rounds
+// per insert under C4's Zipf flows, the whole kernel's time).  Lanes with the same key
+// meet in the LDS hot-key cache or append separately and are summed by the fold.  A key
+// may claim a free cache entry on its second sighting in the workgroup (doorkeeper
+// bitmap), so the long tail of keys seen once does not take the entries.
+__device__ __forceinline__ void wide_insert(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t b) {
+#ifdef EXP_SKIP_INSERT
+  if (k0 != 12345) return;
+#endif
+  const uint64_t kh = key_hash(k0, k1, k2);
+  bool claim = true;
+  if (s.door_log2) {
+    const uint32_t bit = (uint32_t)(kh >> 40) & ((1u << s.door_log2) - 1u);
+    claim = (atomicOr(&s.door[bit >> 5], 1u << (bit & 31u)) >> (bit & 31u)) & 1u;
+  }
+  if (!(s.hot_n && hot_add(s, (uint32_t)kh, k0, k1, k2, 1, b, claim))) wide_append(s, kh, k0, k1, k2, 1, b);
+}
+
 // Wave-level key de-duplication before the global table (BASELINE.json north_star): the
 // lanes of a wave inserting the same key merge into the lowest of them, which inserts the
 // summed count and bytes once -- a Zipf heavy hitter costs one global CAS/add chain per
@@ -483,22 +502,7 @@ __device__ __forceinline__ void sparse_insert(const DevSparse &s, bool valid, ui
     return;
   }
   if (s.lists) {
-    // wide keys through the segment lists: no wave de-duplication (its leader loop costs
-    // one round per distinct key of a hash-bucket collision -- ~30 rounds per insert under
-    // C4's Zipf flows, the whole kernel's time).  Lanes with the same key meet in the LDS
-    // hot-key cache (any key may claim a free entry: the frequent ones arrive first) or
-    // append separately and are summed by the fold.
-    if (!valid) return;
-#ifdef EXP_SKIP_INSERT
-    if (k0 != 12345) return;
-#endif
-    const uint64_t kh = key_hash(k0, k1, k2);
-    bool claim = true;
-    if (s.door_log2) {  // doorkeeper: claim on the second sighting
-      const uint32_t bit = (uint32_t)(kh >> 40) & ((1u << s.door_log2) - 1u);
-      claim = (atomicOr(&s.door[bit >> 5], 1u << (bit & 31u)) >> (bit & 31u)) & 1u;
-    }
-    if (!(s.hot_n && hot_add(s, (uint32_t)kh, k0, k1, k2, 1, b, claim))) wide_append(s, kh, k0, k1, k2, 1, b);
+    if (valid) wide_insert(s, k0, k1, k2, b);
     return;
   }
   const uint64_t vm = __ballot(valid);
@@ -828,6 +832,116 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
     a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
 }
 
+// Sparse-only plans whose 192-bit group-by keys go through the per-segment lists (remote
+// context; local context with ip / port options), without tcpflags groups: the generic
+// kernel's runtime plan walk, dense sink and de-duplication paths cost ~500 VALU and ~6
+// SALU wave-instructions per record there (PMC, profiles/round3/t3b_pmc_c4-remote.json)
+// and spilled VGPRs.  Here the group count and context are compile-time, and with kExcl
+// (the groups' families are pairwise distinct, so their verdict / DNS-type tests are
+// mutually exclusive) a record takes exactly one key build and one insert, whichever
+// group it matches.  Insert: key hash once, doorkeeper, LDS hot-key cache, else the
+// key's segment list (wide_insert).
+template <int NG, bool kRemote, bool kExcl>
+__global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  // LDS: segment-list fill counters, hot-key cache (8-byte aligned), doorkeeper bitmap
+  uint32_t *sctr = (uint32_t *)lds;
+  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
+    const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
+    sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
+  }
+  HotKey *hot = (HotKey *)&lds[(a.sp_nwin + 1) / 2];
+  for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
+  uint32_t *door = (uint32_t *)(hot + a.hot_n);
+  const uint32_t door_words = a.door_log2 ? 1u << (a.door_log2 - 5) : 0u;
+  for (uint32_t i = threadIdx.x; i < door_words; i += blockDim.x) door[i] = 0u;
+  __syncthreads();
+  DevSparse s = a.s;
+  s.lctr = sctr;
+  s.hot = hot;
+  s.hot_n = a.hot_n;
+  s.door = door;
+  s.door_log2 = a.door_log2;
+  s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * kWideEntryWords;
+  s.lcap = a.sp_cap;
+  uint32_t fam[NG], sop[NG], dop[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    fam[g] = g < a.p.ngroups ? a.p.g[g].family : (uint32_t)FAM_COUNT;
+    sop[g] = a.p.g[g].src_opts;
+    dop[g] = a.p.g[g].dst_opts;
+  }
+  for_each_record<true>(a, a.p.need_ports, a.p.need_dns,
+                        [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports, uint32_t dns,
+                            const Lk &ls, const Lk &ld, bool act) {
+    const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta);
+    const uint32_t tdir = meta_tdir(meta), reason = meta_reason(meta), dnstype = meta_dnstype(meta);
+    const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16;
+    // the updates of group g (family f, options o1 / o2) for this record
+    auto update = [&](uint32_t g, uint32_t f, uint32_t o1, uint32_t o2, bool hit) {
+      const uint32_t addb = f <= FAM_DROP ? nb : 0u;
+      if (kRemote) {
+        const SideKey ks = side_key(o1, sip, ls, sport, proto);
+        const SideKey kd = side_key(o2, dip, ld, dport, proto);
+        uint32_t sub = 0, dnsv = 0;
+        if (f == FAM_FWD || f == FAM_RETRANS) sub = tdir << 1;
+        else if (f == FAM_DROP) sub = (reason << 3) | (tdir << 1);
+        else dnsv = dns;
+        if (hit)
+          wide_insert(s, key0(g, sub, ks.slot1, ks.ip), key1(ks.port17, kd.port17, kd.slot1), key2(kd.ip, dnsv),
+                      addb);
+        return;
+      }
+      // getLocalCtxValues (types.go:379-416): src -> egress, dst -> ingress
+      if (o1 == 0 || !hit) return;
+      const bool s_ok = ls.slot >= 0 && !ls.api, d_ok = ld.slot >= 0 && !ld.api;
+      if (f == FAM_DNS_REQ || f == FAM_DNS_RESP) {  // dns.go:506-540: one side
+        const uint32_t side = (s_ok && d_ok) ? ((tdir == 1) ? 0u : 1u) : (d_ok ? 0u : 1u);
+        const SideKey k = side == 0 ? side_key(o1, dip, ld, dport, proto) : side_key(o1, sip, ls, sport, proto);
+        if (s_ok || d_ok) wide_insert(s, key0(g, side, k.slot1, k.ip), key1(k.port17, 0, 0), key2(0, dns), 0);
+        return;
+      }
+      const uint32_t rs = f == FAM_DROP ? reason << 3 : 0u;
+      if (d_ok) {
+        const SideKey k = side_key(o1, dip, ld, dport, proto);
+        wide_insert(s, key0(g, rs, k.slot1, k.ip), key1(k.port17, 0, 0), 0, addb);
+      }
+      if (s_ok) {
+        const SideKey k = side_key(o1, sip, ls, sport, proto);
+        wide_insert(s, key0(g, rs | 1u, k.slot1, k.ip), key1(k.port17, 0, 0), 0, addb);
+      }
+    };
+    if (kExcl) {  // at most one group matches: its descriptors by selects
+      uint32_t gs = 0, f = FAM_COUNT, o1 = 0, o2 = 0;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const bool m = family_matches(fam[g], verdict, proto, dnstype, 0u);
+        gs = m ? (uint32_t)g : gs;
+        f = m ? fam[g] : f;
+        o1 = m ? sop[g] : o1;
+        o2 = m ? dop[g] : o2;
+      }
+      update(gs, f, o1, o2, act && f != FAM_COUNT);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        update((uint32_t)g, fam[g], sop[g], dop[g], act && family_matches(fam[g], verdict, proto, dnstype, 0u));
+    }
+  });
+  __syncthreads();
+  {  // the cached keys, once per workgroup: into the segment lists with their counts
+    DevSparse g = s;
+    g.hot_n = 0;
+    for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) {
+      const HotKey e = hot[i];
+      if (e.tag == 2ULL) wide_append(g, key_hash(e.k0, e.k1, e.k2), e.k0, e.k1, e.k2, e.cnt, e.byt);
+    }
+    __syncthreads();
+  }
+  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
+    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+}
+
 // Workgroup w folds table segment w: its 2^seg_log2 (key, count) slots are loaded into
 // LDS, every aggregation workgroup's list of keys for the segment is inserted with LDS
 // 64-bit CAS + add (the probe sequence of sparse_add_compact), and the segment is
@@ -1000,13 +1114,39 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
   };
   // write each window's staged run [flushed, min(filled, flushed + ring)) (all threads,
   // between barriers; positions past the ring were stored directly)
+  // a wave takes 4 windows at a time and issues all their LDS reads (counters, then the
+  // <= kSpillRing = 2 x 64 staged entries per window) before its global stores
+  static_assert(kSpillRing == 128, "two ring entries per lane and window");
   auto flush = [&]() {
     const uint32_t wv = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-    for (uint32_t w = wv; w < a.nwin; w += nwaves) {
-      const uint32_t f = sfl[w], c = min(ds.ctr[w], ds.spill_cap), e = min(c, f + kSpillRing);
-      uint32_t *dst = ds.spill + mul_u24(w, ds.spill_cap);
-      for (uint32_t p = f + lane; p < e; p += 64) dst[p] = ring[w * kSpillRing + (p & (kSpillRing - 1u))];
-      if (lane == 0) sfl[w] = c;
+    for (uint32_t w0 = wv; w0 < a.nwin; w0 += 4 * nwaves) {
+      uint32_t f[4], c[4], e[4], v[4][2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t w = w0 + q * nwaves;
+        f[q] = w < a.nwin ? sfl[w] : 0u;
+        c[q] = w < a.nwin ? min(ds.ctr[w], ds.spill_cap) : 0u;
+        e[q] = min(c[q], f[q] + kSpillRing);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const uint32_t p = f[q] + lane + 64u * it;
+          v[q][it] = p < e[q] ? ring[(w0 + q * nwaves) * kSpillRing + (p & (kSpillRing - 1u))] : 0u;
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t w = w0 + q * nwaves;
+        if (w >= a.nwin) continue;
+        uint32_t *dst = ds.spill + mul_u24(w, ds.spill_cap);
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const uint32_t p = f[q] + lane + 64u * it;
+          if (p < e[q]) dst[p] = v[q][it];
+        }
+        if (lane == 0) sfl[w] = c[q];
+      }
     }
   };
   // flush every kStageSteps steps: ~100 appends per window on average into the 128-entry
@@ -1382,11 +1522,15 @@ struct IplView {
   __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
     if (kRadix) {
       const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
+      // rows computed for every lane (inactive lanes hold a clamped real record) and the
+      // result masked after: a select on the index made the compiler branch per IP
       uint32_t bi[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) bi[k] = bidx[act ? ipr_row(ip[k], p0, p1, p2, p3, npfx) : npfx << 8];
+      for (int k = 0; k < 8; ++k) bi[k] = bidx[ipr_row(ip[k], p0, p1, p2, p3, npfx)];
 #pragma unroll
       for (int k = 0; k < 8; ++k) sl[k] = blk[(bi[k] << 8) | (ip[k] >> 24)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
       return;
     }
     const uint32_t *keys = (const uint32_t *)smem;
@@ -1395,7 +1539,9 @@ struct IplView {
 #pragma unroll
     for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, act ? j[k] : nb * 2);  // sentinel: no slot
+    for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
   }
 };
 
@@ -1440,31 +1586,14 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
     const uint64_t vlast = vend - 1;  // vn >= 1
     uint64_t vl = vwave + lane < vend ? vwave + lane : vlast;
     uint4 ns = rec_ld(&s4[vl]), nd = rec_ld(&d4[vl]), nbv = rec_ld(&b4[vl]), nm = rec_ld(&m4[vl]);
-#ifdef EXP_PREFETCH2
-    // two steps of record loads in flight (128 B per lane)
-    vl = vwave + blockDim.x + lane < vend ? vwave + blockDim.x + lane : vlast;
-    uint4 ns2 = rec_ld(&s4[vl]), nd2 = rec_ld(&d4[vl]), nb2 = rec_ld(&b4[vl]), nm2 = rec_ld(&m4[vl]);
-#endif
     for (uint64_t vw = vwave; vw < vend; vw += blockDim.x) {
       const bool act = vw + lane < vend;
       const uint4 vs = ns, vd = nd, vb = nbv, vm = nm;
-#ifdef EXP_PREFETCH2
-      ns = ns2;
-      nd = nd2;
-      nbv = nb2;
-      nm = nm2;
-      vl = vw + 2 * blockDim.x + lane < vend ? vw + 2 * blockDim.x + lane : vlast;
-      ns2 = rec_ld(&s4[vl]);
-      nd2 = rec_ld(&d4[vl]);
-      nb2 = rec_ld(&b4[vl]);
-      nm2 = rec_ld(&m4[vl]);
-#else
       vl = vw + blockDim.x + lane < vend ? vw + blockDim.x + lane : vlast;  // clamped: no branch
       ns = rec_ld(&s4[vl]);
       nd = rec_ld(&d4[vl]);
       nbv = rec_ld(&b4[vl]);
       nm = rec_ld(&m4[vl]);
-#endif
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       uint32_t sl[8];
       iv.lookup8(ip, act, sl);
@@ -1871,33 +2000,58 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
     }
   };
   // all threads, between barriers: each window's staged run to its list (positions past
-  // the capacity: the global atomic), then the round counters reset
-  auto flush = [&]() {
+  // the capacity: the global atomic), then the round counters reset.  A wave takes kG
+  // windows at a time and issues every LDS read of them (counters, then up to kIt ring
+  // entries per lane and window) before its global stores, so a flush costs a few LDS
+  // round trips per wave instead of a few per window.
+  auto flush_rings = [&](auto G, auto IT, uint32_t nwin, auto *ring, uint32_t sb, uint32_t *cnt, uint32_t *bas,
+                         auto *list, uint32_t cap, auto &&direct) {
+    constexpr int kG = decltype(G)::value, kIt = decltype(IT)::value;
+    using T = typename std::remove_pointer<decltype(list)>::type;
     const uint32_t wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-    for (uint32_t w = wave; w < nw; w += nwaves) {
-      const uint32_t n = rc[w], b = rb[w], m = min(n, sbc);
-      for (uint32_t p = lane; p < m; p += 64) {
-        const uint16_t e = cst[w * sbc + p];
-        if (b + p < k.cap) mine[(size_t)w * k.cap + b + p] = e;
-        else cms_direct(w, e);
+    for (uint32_t w0 = wave; w0 < nwin; w0 += kG * nwaves) {
+      uint32_t n[kG], b[kG];
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t w = w0 + q * nwaves;
+        n[q] = w < nwin ? cnt[w] : 0u;
+        b[q] = w < nwin ? bas[w] : 0u;
       }
-      if (lane == 0) {
-        rb[w] = b + n;
-        rc[w] = 0u;
+      T v[kG][kIt];
+#pragma unroll
+      for (int q = 0; q < kG; ++q)
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+          const uint32_t p = lane + 64u * it;
+          v[q][it] = p < min(n[q], sb) ? ring[(w0 + q * nwaves) * sb + p] : (T)0;
+        }
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t w = w0 + q * nwaves, m = min(n[q], sb);
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+          const uint32_t p = lane + 64u * it;
+          if (p >= m) continue;
+          if (b[q] + p < cap) list[(size_t)w * cap + b[q] + p] = v[q][it];
+          else direct(w, (uint32_t)v[q][it]);
+        }
+        for (uint32_t p = lane + 64u * kIt; p < m; p += 64) {  // rings longer than kIt * 64
+          const T e = ring[w * sb + p];
+          if (b[q] + p < cap) list[(size_t)w * cap + b[q] + p] = e;
+          else direct(w, (uint32_t)e);
+        }
+        if (lane == 0 && w < nwin) {
+          bas[w] = b[q] + n[q];
+          cnt[w] = 0u;
+        }
       }
     }
-    for (uint32_t w = wave; w < nh; w += nwaves) {
-      const uint32_t n = hc[w], b = hb[w], m = min(n, sbh);
-      for (uint32_t p = lane; p < m; p += 64) {
-        const uint32_t e = hst[w * sbh + p];
-        if (b + p < k.hcap) hmine[(size_t)w * k.hcap + b + p] = e;
-        else hll_direct(w, e);
-      }
-      if (lane == 0) {
-        hb[w] = b + n;
-        hc[w] = 0u;
-      }
-    }
+  };
+  auto flush = [&]() {
+    flush_rings(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{}, nw, cst, sbc, rc, rb, mine,
+                k.cap, cms_direct);
+    flush_rings(std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{}, nh, hst, sbh, hc, hb, hmine,
+                k.hcap, hll_direct);
   };
   const uint64_t start = (uint64_t)blockIdx.x * k.chunk;
   const uint64_t end = start + k.chunk < k.n ? start + k.chunk : k.n;
@@ -2687,6 +2841,52 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
       }
   const uint32_t B = a.blocks, T = a.threads;
   hipError_t e;
+  // sparse-only plans on the wide-key list path (no dense group, no tcpflags, no sketch,
+  // <= 4 groups): wide_kernel
+  bool wide = !a.tier1 && !a.dense_ng && !sketch && a.vec && a.hot_n && k.sp_nwin && !a.sparse.compact &&
+              a.plan.ngroups >= 1 && a.plan.ngroups <= 4;
+  bool excl = true;
+  for (int g = 0; wide && g < a.plan.ngroups; ++g) {
+    wide = a.plan.g[g].sparse && a.plan.g[g].family != FAM_TCPFLAGS;
+    for (int h = 0; h < g; ++h) excl &= a.plan.g[h].family != a.plan.g[g].family;
+  }
+  if (wide) {
+    // LDS: counters, cache, then the largest doorkeeper bitmap that fits
+    size_t lw = (size_t)((k.sp_nwin + 1) / 2) * 8 + (size_t)a.hot_n * kHotKeyBytes;
+    k.door_log2 = 0;
+    for (uint32_t l = 18; l >= 13; --l)
+      if (lw + ((size_t)1 << (l - 3)) <= kLdsBytes) {
+        k.door_log2 = l;
+        lw += (size_t)1 << (l - 3);
+        break;
+      }
+    const bool remote = !a.plan.local, four = a.plan.ngroups > 2;
+    if (kernel) {
+      static thread_local char wname[64];
+      snprintf(wname, sizeof wname, "wide_kernel<%d, %s, %s>", four ? 4 : 2, remote ? "true" : "false",
+               excl ? "true" : "false");
+      *kernel = wname;
+    }
+#define GA_WIDE(NG, R, X) e = launch_k(wide_kernel<NG, R, X>, k, B, T, lw, st)
+    if (four) {
+      if (remote) { if (excl) GA_WIDE(4, true, true); else GA_WIDE(4, true, false); }
+      else { if (excl) GA_WIDE(4, false, true); else GA_WIDE(4, false, false); }
+    } else {
+      if (remote) { if (excl) GA_WIDE(2, true, true); else GA_WIDE(2, true, false); }
+      else { if (excl) GA_WIDE(2, false, true); else GA_WIDE(2, false, false); }
+    }
+#undef GA_WIDE
+    if (e != hipSuccess) return e;
+    if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
+    if (a.defer_folds) {  // lists folded later (launch_folds)
+      LaunchArgs r = a;
+      r.spill = nullptr;
+      r.stage_b = nullptr;
+      r.sp_lists = nullptr;
+      return launch_folds(r, st);
+    }
+    return launch_folds(a, st);
+  }
   int variant = a.tier1 ? 100 + (int)a.dense_ng : (a.dns_compact && a.dense_ng ? 300 : 0) + (int)a.dense_ng;
   if (variant == 304 && a.sig == kSigC5) variant = 305;
   size_t lds_used = lds;

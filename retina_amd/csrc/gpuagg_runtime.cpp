@@ -1105,7 +1105,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   // one 1024-thread workgroup per CU whenever LDS holds bins or spill counters: with
   // dense bins but no LDS prefix (C5: 100k-pod groups) 4x fewer workgroups mean 4x
   // fewer, longer spill lists for the fold (same 16 waves per CU)
-  const bool wide = a.lds_bins || a.tier1 || c->dense_len > 0;
+  // (the hot-key cache alone fills ~2/3 of the LDS: with 256-thread workgroups a CU would
+  // run 4 waves)
+  const bool wide = a.lds_bins || a.tier1 || c->dense_len > 0 || a.hot_n;
   a.blocks = wide ? c->n_cu : c->n_cu * 4;
   a.threads = wide ? 1024 : 256;
   const uint64_t per_launch = (uint64_t)a.blocks * kMaxRecordsPerBlock;
