@@ -161,6 +161,10 @@ constexpr uint64_t kMaxRecordsPerBlock = (1ULL << 20) - 4;  // count field < 2^2
 // (13 bits) | bytes << 13; a packet of >= 2^19 bytes adds its bytes with a global
 // atomic and spills 0.
 constexpr uint32_t kFoldWindowShift = 13, kFoldWindowBins = 1u << kFoldWindowShift;
+// Bit 31 of a spill entry marks a row-mask entry: offset = the first bin of an 8-bin
+// tcpflags row, bits [win_shift, win_shift + 8) = the flags to count (+1 each); plain
+// entries carry < 2^(31 - win_shift) bytes, so the bit is free.
+constexpr uint32_t kSpillRowMask = 1u << 31;
 
 // ---- LDS-resident IP table (tier-1 dense kernel) ------------------------------------
 // Bucketized cuckoo: 2 candidate buckets of 2 keys (8 B, one ds_read_b64 each),

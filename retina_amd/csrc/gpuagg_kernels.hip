@@ -160,6 +160,9 @@ struct KArgs {
   uint32_t accum;
   uint32_t hot_n;  // LDS hot-key cache entries of aggregate_kernel (0: none)
   uint32_t door_log2;  // doorkeeper bits of the hot-key cache (0: every key may claim)
+  uint32_t row_masks;  // spilled tcpflags rows 8-aligned in their windows: one row-mask entry
+  uint32_t *fold_flag;  // wide lists: fullest list of this launch -> fold_flag[fold_parity]
+  uint32_t fold_parity;
   Plan p;
 };
 
@@ -353,10 +356,10 @@ struct DenseSink {
 
   __device__ __forceinline__ uint32_t window(uint32_t bin) const { return (bin - spill_lo) >> win_shift; }
   // 4-byte entry: the bin's offset in its window and the bytes; bytes that do not fit
-  // the field (2^(32 - win_shift)) are added to the global counter here (rare) and the
-  // entry carries 0
+  // the field (2^(31 - win_shift): bit 31 marks a row-mask entry, below) are added to the
+  // global counter here (rare) and the entry carries 0
   __device__ __forceinline__ uint32_t entry(uint32_t bin, uint32_t nbytes) const {
-    const bool fits = (nbytes >> (32u - win_shift)) == 0u;
+    const bool fits = (nbytes >> (31u - win_shift)) == 0u;
     if (!fits) atomicAdd(&d.byt[bin], (unsigned long long)nbytes);
     return ((bin - spill_lo) & ((1u << win_shift) - 1u)) | ((fits ? nbytes : 0u) << win_shift);
   }
@@ -780,6 +783,21 @@ __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds)
   spill_counts_out(a, ds.ctr);
 }
 
+// Stores this workgroup's segment-list fills and, for device-conditional folds, adds
+// its fullest list to the launch's flag (one atomic max per workgroup).
+__device__ __forceinline__ void sp_counts_out(const KArgs &a, const uint32_t *sctr) {
+  uint32_t mx = 0;
+  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x) {
+    const uint32_t c = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = c;
+    mx = c > mx ? c : mx;
+  }
+  if (!a.fold_flag) return;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  if ((threadIdx.x & 63u) == 0 && mx) atomicMax(&a.fold_flag[a.fold_parity], mx);
+}
+
 // Generic aggregation: any plan (dense, sparse, DNS, remote context, sketches).
 template <bool kVec, bool kSketch>
 __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
@@ -828,8 +846,7 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
     }
     __syncthreads();
   }
-  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
-    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+  sp_counts_out(a, sctr);
 }
 
 // Sparse-only plans whose 192-bit group-by keys go through the per-segment lists (remote
@@ -938,8 +955,7 @@ __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
     }
     __syncthreads();
   }
-  for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x)
-    a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
+  sp_counts_out(a, sctr);
 }
 
 // Workgroup w folds table segment w: its 2^seg_log2 (key, count) slots are loaded into
@@ -999,10 +1015,19 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
 // the host sums them) -- and the segment is stored back.  Segments no list reaches are
 // not touched.
 __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, const unsigned long long *lists,
-                                                                const uint32_t *counts, uint32_t n_lists,
-                                                                uint32_t nwin, uint32_t cap) {
+                                                                uint32_t *counts, uint32_t n_lists,
+                                                                uint32_t nwin, uint32_t cap, uint32_t *flag,
+                                                                uint32_t parity, uint32_t thr) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long seg[];
   const uint32_t w = blockIdx.x, N = 1u << s.seg_log2, smask = N - 1u;
+  if (flag) {
+    // device-conditional fold: the next launch's flag starts at 0; while the fullest list
+    // of the launches since the last fold is below thr, the lists keep growing (the next
+    // aggregation launch appends after them).  Atomics: executed at memory, so no XCD's
+    // L2 can hold a stale copy of the flags.
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&flag[parity ^ 1u], 0u);
+    if (thr && atomicOr(&flag[parity], 0u) < thr) return;  // the same value for every workgroup
+  }
   // lanes per list: the workgroup's threads spread over the lists (a power of two <= 64)
   uint32_t lpl = 1;
   while (lpl < 64 && lpl * 2 * n_lists <= blockDim.x) lpl *= 2;
@@ -1063,6 +1088,8 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     const uint32_t slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
     g[j] = seg[f * N + slot];
   }
+  // this segment's lists are folded: empty them for the launches that append next
+  for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) counts[(size_t)l * nwin + w] = 0u;
 }
 
 // Dense local-context fast path: every group is endpoint-keyed (forward / drop /
@@ -1086,54 +1113,74 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
                       a.s.dropped, a.s.mask, a.s.seg_log2};
   }
   // kStage: spill appends are staged in per-window LDS rings (after the segment
-  // counters: [nwin] flushed positions, then [nwin][kSpillRing] entries) and written out
+  // counters: [nwin] round counters, then [nwin][kSpillRing] entries) and written out
   // every few steps as contiguous runs -- C5's ~1.4 appends per record to 220 windows were
-  // scattered 4-byte stores (PMC: 3.2x the list bytes written).
-  uint32_t *sfl = sctr + (kDns ? a.sp_nwin : 0u);
-  uint32_t *ring = sfl + a.nwin;
+  // scattered 4-byte stores (PMC: 3.2x the list bytes written).  rc[w] counts window w's
+  // appends since the last flush, so an append's ring slot is what its LDS atomic returns
+  // (one LDS round trip); ds.ctr[w] holds the list length at the last flush.
+  uint32_t *rc = sctr + (kDns ? a.sp_nwin : 0u);
+  uint32_t *ring = rc + a.nwin;
   if (kStage)
-    for (uint32_t w = threadIdx.x; w < a.nwin; w += blockDim.x) sfl[w] = spill_ctr0(a, w);
-  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and sfl too)
+    for (uint32_t w = threadIdx.x; w < a.nwin; w += blockDim.x) rc[w] = 0u;
+  const DenseSink ds = dense_sink_init(a, lds);  // (its barrier covers sctr and rc too)
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t dummy = a.lds_bins + lane;  // absorbs predicated-off updates, never flushed
+  const uint32_t wmask = (1u << a.win_shift) - 1u;
+  // an entry of window w that cannot be listed: its updates as global atomics (exact)
+  auto entry_global = [&](uint32_t w, uint32_t e) {
+    const uint32_t bin = a.spill_lo + (w << a.win_shift) + (e & wmask);
+    if (e >> 31) {
+      for (uint32_t m = (e >> a.win_shift) & 0xFFu; m; m &= m - 1)
+        atomicAdd(&a.d.cnt[bin + __builtin_ctz(m)], 1ULL);
+      return;
+    }
+    atomicAdd(&a.d.cnt[bin], 1ULL);
+    if (e >> a.win_shift) atomicAdd(&a.d.byt[bin], (unsigned long long)(e >> a.win_shift));
+  };
+  auto spill_e = [&](uint32_t w, uint32_t e) {  // kStage
+    const uint32_t p = atomicAdd(&rc[w], 1u);
+    if (p < kSpillRing) {
+      ring[w * kSpillRing + p] = e;
+      return;
+    }
+    const uint32_t lp = ds.ctr[w] + p;  // past the ring: straight into the list
+    if (lp < ds.spill_cap) ds.spill[mul_u24(w, ds.spill_cap) + lp] = e;
+    else entry_global(w, e);
+  };
   auto spill = [&](uint32_t bin, uint32_t nbytes) {
     if (!kStage) {
       ds.spill_add(bin, nbytes);
       return;
     }
-    const uint32_t w = ds.window(bin);
-    const uint32_t pos = atomicAdd(&ds.ctr[w], 1u);
-    if (pos < ds.spill_cap) {
-      const uint32_t e = ds.entry(bin, nbytes);
-      if (pos - sfl[w] < kSpillRing) ring[w * kSpillRing + (pos & (kSpillRing - 1u))] = e;
-      else ds.spill[mul_u24(w, ds.spill_cap) + pos] = e;  // ring full: direct
-      return;
-    }
-    atomicAdd(&a.d.cnt[bin], 1ULL);  // list full (exact fallback)
-    if (nbytes) atomicAdd(&a.d.byt[bin], (unsigned long long)nbytes);
+    spill_e(ds.window(bin), ds.entry(bin, nbytes));
   };
-  // write each window's staged run [flushed, min(filled, flushed + ring)) (all threads,
-  // between barriers; positions past the ring were stored directly)
-  // a wave takes 4 windows at a time and issues all their LDS reads (counters, then the
-  // <= kSpillRing = 2 x 64 staged entries per window) before its global stores
+  // a spilled tcpflags row (8 bins, 8-aligned in its window): one entry for the whole flag
+  // mask (kSpillRowMask) instead of one per flag
+  const bool rows = kStage && a.row_masks;
+  auto spill_row = [&](uint32_t row, uint32_t m) {
+    spill_e(ds.window(row), ((row - a.spill_lo) & wmask) | (m << a.win_shift) | kSpillRowMask);
+  };
+  // each window's staged run to its list at the length of the last flush (all threads,
+  // between barriers); a wave takes 4 windows at a time and issues all their LDS reads
+  // (counters, then the <= kSpillRing = 2 x 64 staged entries per window) before its
+  // global stores
   static_assert(kSpillRing == 128, "two ring entries per lane and window");
   auto flush = [&]() {
     const uint32_t wv = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     for (uint32_t w0 = wv; w0 < a.nwin; w0 += 4 * nwaves) {
-      uint32_t f[4], c[4], e[4], v[4][2];
+      uint32_t n[4], b[4], v[4][2];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t w = w0 + q * nwaves;
-        f[q] = w < a.nwin ? sfl[w] : 0u;
-        c[q] = w < a.nwin ? min(ds.ctr[w], ds.spill_cap) : 0u;
-        e[q] = min(c[q], f[q] + kSpillRing);
+        n[q] = w < a.nwin ? rc[w] : 0u;
+        b[q] = w < a.nwin ? ds.ctr[w] : 0u;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
-          const uint32_t p = f[q] + lane + 64u * it;
-          v[q][it] = p < e[q] ? ring[(w0 + q * nwaves) * kSpillRing + (p & (kSpillRing - 1u))] : 0u;
+          const uint32_t p = lane + 64u * it;
+          v[q][it] = p < min(n[q], kSpillRing) ? ring[(w0 + q * nwaves) * kSpillRing + p] : 0u;
         }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1142,10 +1189,15 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
         uint32_t *dst = ds.spill + mul_u24(w, ds.spill_cap);
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
-          const uint32_t p = f[q] + lane + 64u * it;
-          if (p < e[q]) dst[p] = v[q][it];
+          const uint32_t p = lane + 64u * it;
+          if (p >= min(n[q], kSpillRing)) continue;
+          if (b[q] + p < ds.spill_cap) dst[b[q] + p] = v[q][it];
+          else entry_global(w, v[q][it]);
         }
-        if (lane == 0) sfl[w] = c[q];
+        if (lane == 0) {
+          ds.ctr[w] = b[q] + n[q];
+          rc[w] = 0u;
+        }
       }
     }
   };
@@ -1218,6 +1270,9 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
             atomicAdd(&lds[v && s_ok ? row_s + bit : dummy], kLdsCountOne);
             m &= m - 1;
           }
+        } else if (rows) {
+          if (m && d_ok) spill_row(row_d, m);
+          if (m && s_ok) spill_row(row_s, m);
         } else {
           for (; m; m &= m - 1) {
             const uint32_t bit = (uint32_t)__builtin_ctz(m);
@@ -1372,6 +1427,21 @@ struct SpillQ {
     e0 = got ? r0 : e0;
     e1 = got ? r1 : e1;
     e2 = got ? r2 : e2;
+    n += cnt;
+    return n >= 64;
+  }
+  // push of two values (the third register is left alone)
+  __device__ __forceinline__ bool push2(bool v, uint32_t lane, uint32_t a0, uint32_t a1) {
+    const uint64_t m = __ballot(v);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const uint32_t pos = v ? n + below : n + cnt + (lane - below);
+    const int addr = (int)((pos & 63u) << 2);
+    r0 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a0);
+    r1 = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)a1);
+    const bool got = lane >= n && lane < n + cnt;
+    e0 = got ? r0 : e0;
+    e1 = got ? r1 : e1;
     n += cnt;
     return n >= 64;
   }
@@ -1563,12 +1633,18 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   const DenseSink ds = make_sink(a, nullptr, 0, bins + L4 + 64);
   const DenseGroups<NG, SIG> G(a.p, L4);
   SpillQ q{};
+  // C2's signature spills only the drop group (group 1): a queued record is its slots and
+  // bytes | reason << 29 -- two registers (one ds_permute fewer per record); the meta word
+  // is rebuilt at the flush.  Bytes >= 2^29 are added to the drop bins at the push.
+  constexpr bool kDropQ = SIG == kSigFwdLdsDropSpill;
+  constexpr uint32_t kQBytes = (1u << 29) - 1u;
   // spill updates of the queued records; lanes >= n (final partial flush) hold no entry
   auto q_flush = [&](bool full) {
     const bool valid = full || lane < q.n;
     const uint32_t s1[1] = {valid ? (q.e0 & 0xFFFFu) : kIplNoSlot};
     const uint32_t d1[1] = {valid ? (q.e0 >> 16) : kIplNoSlot};
-    const uint32_t b1[1] = {q.e1}, m1[1] = {q.e2};
+    const uint32_t b1[1] = {kDropQ ? q.e1 & kQBytes : q.e1};
+    const uint32_t m1[1] = {kDropQ ? (kVerdictDropped << 8) | ((q.e1 >> 29) << 18) : q.e2};
     l4_records<NG, SIG, 1, 2>(G, l4, ds, b1, m1, s1, d1);
   };
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
@@ -1619,7 +1695,19 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
         for (int g = 0; g < NG; ++g)
           if (G.fam[g] != FAM_COUNT && !G.inl[g]) need |= fam_hit(G.fam[g], ver, fm);
         need = need & (x0 != 0xFFFFFFFFu);  // some side is a pod
-        if (q.push(need, lane, x0, y0, z0)) {
+        bool full;
+        if (kDropQ) {
+          if (__builtin_expect(need && y0 > kQBytes, 0)) {  // jumbo bytes: straight to the bins
+            const uint32_t r = meta_reason(z0), sdd = x0 >> 16, sss = x0 & 0xFFFFu;
+            const uint32_t kd = G.keyed[1] ? sdd : 0u, ks = G.keyed[1] ? sss : 0u;
+            if (sdd != kIplNoSlot) atomicAdd(&a.d.byt[G.base[1] + mul_u24(kd * 2u, G.nsub[1]) + r], (unsigned long long)y0);
+            if (sss != kIplNoSlot) atomicAdd(&a.d.byt[G.base[1] + mul_u24(ks * 2u + 1u, G.nsub[1]) + r], (unsigned long long)y0);
+          }
+          full = q.push2(need, lane, x0, (y0 > kQBytes ? 0u : y0) | (meta_reason(z0) << 29));
+        } else {
+          full = q.push(need, lane, x0, y0, z0);
+        }
+        if (full) {
           q_flush(true);
           q.next();
         }
@@ -2500,7 +2588,16 @@ __global__ __launch_bounds__(1024) void spill_window_kernel(
   const bool fast = total < (1ULL << 20);
   const uint32_t off_mask = W - 1, wshift = 31u - (uint32_t)__builtin_clz(W);
   auto add = [&](uint32_t x) {
-    const uint32_t off = x & off_mask, nb = x >> wshift;
+    const uint32_t off = x & off_mask;
+    if (x >> 31) {  // row-mask entry (kSpillRowMask): +1 to each flagged bin of the 8-bin row
+      for (uint32_t m = (x >> wshift) & 0xFFu; m; m &= m - 1) {
+        const uint32_t o = off + (uint32_t)__builtin_ctz(m);
+        if (fast) atomicAdd(&win[o], kLdsCountOne);
+        else lds_add64_exact(&win[o], (uint32_t)lo + o, 0u, d);
+      }
+      return;
+    }
+    const uint32_t nb = x >> wshift;
     if (fast) atomicAdd(&win[off], kLdsCountOne | nb);
     else lds_add64_exact(&win[off], (uint32_t)lo + off, nb, d);
   };
@@ -2824,6 +2921,14 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.sp_cap = a.sp_cap;
   k.accum = a.accum ? 1u : 0u;
   k.hot_n = a.hot_n;
+  k.fold_flag = a.sp_lists ? a.fold_flag : nullptr;
+  // row-mask spill entries need every tcpflags group's 8-bin rows aligned in the windows
+  k.row_masks = a.spill ? 1u : 0u;
+  for (int g = 0; g < a.plan.ngroups; ++g)
+    if (a.plan.g[g].family == FAM_TCPFLAGS && !a.plan.g[g].sparse &&
+        (a.plan.g[g].nsub != 8 || a.plan.g[g].dense_base < a.spill_lo || (a.plan.g[g].dense_base - a.spill_lo) % 8))
+      k.row_masks = 0u;
+  k.fold_parity = a.fold_parity;
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
@@ -2878,11 +2983,11 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
 #undef GA_WIDE
     if (e != hipSuccess) return e;
     if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
-    if (a.defer_folds) {  // lists folded later (launch_folds)
+    if (a.defer_folds) {  // lists folded later (launch_folds), or when the device says so
       LaunchArgs r = a;
       r.spill = nullptr;
       r.stage_b = nullptr;
-      r.sp_lists = nullptr;
+      if (!a.fold_cond) r.sp_lists = nullptr;
       return launch_folds(r, st);
     }
     return launch_folds(a, st);
@@ -2957,11 +3062,12 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   }
   if (e != hipSuccess) return e;
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
-  if (a.defer_folds) {  // lists folded later (launch_folds); the tier-1 copies now
+  if (a.defer_folds) {  // lists folded later (launch_folds), or when the device says so;
+    // the tier-1 copies now
     LaunchArgs r = a;
     r.spill = nullptr;
     r.stage_b = nullptr;
-    r.sp_lists = nullptr;
+    if (!a.fold_cond) r.sp_lists = nullptr;
     return launch_folds(r, st);
   }
   return launch_folds(a, st);
@@ -2998,7 +3104,8 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)seg_lds)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(sparse_fold_wide_kernel, dim3(a.sp_nwin), dim3(1024), seg_lds, st, dev_sparse(a.sparse),
-                       (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap);
+                       (const unsigned long long *)a.sp_lists, a.sp_counts, a.blocks, a.sp_nwin, a.sp_cap,
+                       a.fold_flag, a.fold_parity, a.fold_cond ? a.sp_cap / 2 : 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (!a.spill) return reduce(false);

@@ -75,6 +75,12 @@ struct LaunchArgs {
   // launch_folds (the tier-1 copies are still summed per launch)
   bool accum;
   bool defer_folds;
+  // wide-key lists folded when the device says so: the aggregation kernel records the
+  // fullest list in fold_flag[fold_parity] and the per-launch fold skips itself while that
+  // is below half the capacity (fold_cond); fold_pending folds unconditionally
+  uint32_t *fold_flag;  // [2] u32, zeroed at allocation
+  uint32_t fold_parity;
+  bool fold_cond;
   uint32_t hot_n;  // aggregate_kernel's LDS hot-key cache entries (0: none)
 };
 // The list folds of (possibly several deferred) launches with geometry a: the compact

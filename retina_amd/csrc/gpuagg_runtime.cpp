@@ -289,6 +289,8 @@ struct gpuagg_ctx {
   // staged flushes: per-workgroup LDS bins (tier-1) and per-partition fold windows
   uint32_t *d_stage_a = nullptr;
   size_t stage_a_alloc = 0;
+  uint32_t *d_fold_flag = nullptr;  // device-conditional wide-list folds: [2] fullest list
+  uint32_t fold_parity = 0;
   // Deferred list folds: the spill / segment lists of consecutive launches with one
   // geometry accumulate and are folded once (fold_pending) -- per scrape epoch rather
   // than per batch, so C5's fixed 128 MiB table pass is paid once per sync.
@@ -544,6 +546,7 @@ int fold_pending(gpuagg_ctx *c) {
   LaunchArgs f = c->pend.a;
   f.stage_a = nullptr;  // summed per launch
   f.defer_folds = false;
+  f.fold_cond = false;  // unconditional (the flags are left to the launches)
   std::array<hipEvent_t, 2> ev{};
   if (c->timing) {
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
@@ -1117,6 +1120,15 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.cols = ColsView{sh(cv.src_ip), sh(cv.dst_ip), sh(cv.bytes), sh(cv.meta), sh(cv.ports), sh(cv.dns_id)};
     a.n = m;
     a.chunk = ((m + a.blocks - 1) / a.blocks + 3) & ~3ULL;
+    if (hot) {
+      // the cache is flushed into the lists once per workgroup and launch: at small batches
+      // (the Go plugin's 1M records: 4k per workgroup) a full 2048-entry cache doubled the
+      // appends, so it is sized ~chunk / 8 (256 .. kHotKeys entries; under Zipf(1.2) the
+      // top 256 keys still carry ~70 % of the updates)
+      uint32_t hn = 256;
+      while (hn < kHotKeys && (uint64_t)hn * 16 <= a.chunk) hn <<= 1;
+      a.hot_n = hn;
+    }
     auto al = [](const uint32_t *p) { return ((uintptr_t)p & 15u) == 0; };
     a.vec = al(a.cols.src_ip) && al(a.cols.dst_ip) && al(a.cols.bytes) && al(a.cols.meta) &&
             (!(c->plan.need_ports || c->cms_len) || al(a.cols.ports)) &&
@@ -1162,9 +1174,9 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         const uint64_t mean = budget / sp_nwin;
         g.sp_nwin = (uint32_t)sp_nwin;
         uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
-        if (!c->sv.compact)  // 32-byte entries: at most kWideListBytes of lists per ctx
-          cap = std::max<uint64_t>(16, std::min<uint64_t>(cap, kWideListBytes / (8 * kWideEntryWords) /
-                                                                   ((uint64_t)a.blocks * sp_nwin)));
+        if (!c->sv.compact)  // 32-byte entries: kWideListBytes of lists per ctx
+          cap = std::max<uint64_t>(16, kWideListBytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin)) &
+                ~1ULL;
         g.sp_cap = (uint32_t)cap;
       }
       return g;
@@ -1192,13 +1204,15 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     // ~2 % slower in the tier-1 kernel (profiles/round2/r4f_*).
     const bool lists = sp_lists;
     const bool defer = c->defer_folds && lists;
+    // Wide lists (192-bit keys) are folded when the device says so: every launch's fold
+    // skips itself until some list is half full (sparse_fold_wide_kernel), so the host keeps
+    // appending without a record budget -- under skew the LDS hot-key cache absorbs most
+    // updates and a budget that assumes one entry per record folded ~5x too often.
+    const bool fold_cond = defer && !c->sv.compact;
     uint64_t budget = defer ? std::max<uint64_t>(a.chunk, std::min<uint64_t>(kMaxRecordsPerBlock,
                                                                              kDeferLaunches * a.chunk))
                             : a.chunk;
-    if (defer && !c->sv.compact) {  // wide lists: only as many launches as the list memory holds
-      const uint64_t cap = kWideListBytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin);
-      budget = std::max<uint64_t>(a.chunk, std::min<uint64_t>(budget, cap * sp_nwin * 4 / 5));
-    }
+    if (fold_cond) budget = ~0ull >> 1;
     bool accum = false;
     if (c->pend.active) {
       const LaunchArgs &q = c->pend.a;
@@ -1240,6 +1254,18 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     a.accum = accum;
     a.defer_folds = defer && (a.spill || a.sp_lists);
+    a.fold_cond = false;
+    a.fold_flag = nullptr;
+    if (fold_cond && a.sp_lists) {
+      if (!c->d_fold_flag) {
+        if ((rc = dev_alloc(c, &c->d_fold_flag, 2))) return rc;
+        HIPCHK(c, x_set_async(c, c->d_fold_flag, 0, 8, c->stream));
+      }
+      a.fold_cond = true;
+      a.fold_flag = c->d_fold_flag;
+      a.fold_parity = c->fold_parity;
+      c->fold_parity ^= 1u;
+    }
     a.dense_cnt = c->d_dense_cnt;
     a.dense_byt = c->d_dense_byt;
     std::array<hipEvent_t, 3> ev{};
@@ -1429,6 +1455,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c, c->d_spill);
   dev_free(c, c->d_spill_count);
   dev_free(c, c->d_stage_a);
+  dev_free(c, c->d_fold_flag);
   dev_free(c, c->d_enrich);
   dev_free(c, c->d_stage_b);
   dev_free(c, c->d_sk_lists);

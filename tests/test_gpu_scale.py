@@ -93,7 +93,8 @@ def test_packed_field_overflow_exact(gpu_device, flags):
     f = int(np.flatnonzero((verdict == W.V_FWD) & ok)[0])
     d = int(np.flatnonzero((verdict == W.V_DROP) & ok)[0])
     idx = np.array([f, f, f] + [d] * 7)
-    nbytes = np.array([1_000_000, (1 << 20) - 1, 5_000_000] + [(1 << 24) - 1] * 6 + [20_000_000],
+    # (the last drop exceeds the 29-bit byte field of the tier-1 drop queue: added at the push)
+    nbytes = np.array([1_000_000, (1 << 20) - 1, 5_000_000] + [(1 << 24) - 1] * 5 + [20_000_000, (1 << 31) + 5],
                       np.uint32)
     ten = W.Records(base.src_ip[idx], base.dst_ip[idx], nbytes, base.meta[idx], base.ports[idx],
                     base.dns_id[idx])
