@@ -73,6 +73,8 @@ typedef struct gpuagg_config {
                                           once per gpuagg_sync or state read (diagnostics) */
 #define GPUAGG_FLAG_LDS_CUCKOO 64u     /* tier-1 LDS IP image as the cuckoo table even when the radix
                                           image fits (diagnostics) */
+#define GPUAGG_FLAG_ROW_RADIX 256u     /* LDS IP images in the radix form with its row table even
+                                        when the dense form would do (diagnostics / tests) */
 #define GPUAGG_FLAG_CPU_BACKEND 128u  /* run on host threads and host memory, no device (nodes without
                                           a gfx950 GPU): the same plan, ABI and results; "device"
                                           pointers of this ctx's calls are host pointers          */

@@ -32,8 +32,9 @@ FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table
 FLAG_LDS_CUCKOO = 64  # diagnostics: cuckoo LDS IP image even when the radix image fits
-FLAG_NO_WIDE_LISTS = 32
-FLAG_CPU_BACKEND = 128  # host threads and host memory instead of a device (GPUAGG_FLAG_CPU_BACKEND)  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
+FLAG_NO_WIDE_LISTS = 32  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
+FLAG_CPU_BACKEND = 128  # host threads and host memory instead of a device (GPUAGG_FLAG_CPU_BACKEND)
+FLAG_ROW_RADIX = 256  # diagnostics: radix LDS IP images with the row table even when dense ones fit
 
 
 class MetricOptions(C.Structure):

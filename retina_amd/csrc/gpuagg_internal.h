@@ -227,6 +227,25 @@ GA_HD uint32_t ipr_row(uint32_t ip, uint32_t p0, uint32_t p1, uint32_t p2, uint3
   return (j << 8) | ((ip >> 16) & 0xFFu);
 }
 
+// Dense radix LDS image (the common case of the radix image: every prefix's populated /24s
+// form one run of third octets, as node pod CIDRs carved in order from a cluster /16 do):
+// no row table -- the block of an address is computed, so a lookup is ONE u16 read and a
+// few VALU ops instead of two dependent reads.  Per prefix j a descriptor
+// dr[j] = lo | cnt << 8 | base << 17 (third octets [lo, lo + cnt) map to blocks base ..);
+// the image is blk u16[(nblk + 1) * 256] with block 0 the "no pod" block; holes inside a
+// run get empty blocks of their own.
+GA_HD uint32_t iprd_block(uint32_t ip, uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t d0,
+                          uint32_t d1, uint32_t d2, uint32_t d3) {
+  const uint32_t p = ip & 0xFFFFu;
+  uint32_t d = 0u;
+  d = p == p3 ? d3 : d;
+  d = p == p2 ? d2 : d;
+  d = p == p1 ? d1 : d;
+  d = p == p0 ? d0 : d;
+  const uint32_t rel = ((ip >> 16) & 0xFFu) - (d & 0xFFu);
+  return rel < ((d >> 8) & 0x1FFu) ? (d >> 17) + rel : 0u;
+}
+
 // 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
 // correct the rare carry / wrap exactly with global atomics; count-only families
 // (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).

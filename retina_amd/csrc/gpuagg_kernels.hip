@@ -148,7 +148,8 @@ struct KArgs {
   // tier-1: LDS image of the IP table
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
-  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (dense_lds_kernel kRadix)
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (dense_lds_kernel kIp 1 / 2)
+  uint32_t ipl_dr[kIprMaxPfx];             // dense radix descriptors (kIp 2)
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
   // compact group-by keys bucketed per table segment (generic kernel), or null
@@ -1577,49 +1578,54 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
 
 // One IP through the tier-1 LDS image: slot or kIplNoSlot (inactive lanes: kIplNoSlot).
 // kRadix: the radix image (two dependent u16 reads); else the cuckoo image.
-template <bool kRadix>
+template <int kIp>
 struct IplView {
   const uint8_t *smem;
   uint32_t nb, seed, npfx, p0, p1, p2, p3;
+  uint32_t d0, d1, d2, d3;  // kIp 2: the dense radix descriptors
   __device__ __forceinline__ uint32_t lookup(uint32_t ip) const {
-    if (kRadix) {
+    if (kIp == 2)
+      return ((const uint16_t *)smem)[(iprd_block(ip, p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip >> 24)];
+    if (kIp == 1) {
       const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
       return blk[((uint32_t)bidx[ipr_row(ip, p0, p1, p2, p3, npfx)] << 8) | (ip >> 24)];
     }
     return ipl_slot((const uint16_t *)(smem + ipl_vals_offset(nb)), ipl_probe_index((const uint32_t *)smem, nb, seed, ip));
   }
-  // the 8 IPs of a step, every read of a level issued before the next level
+  // the 8 IPs of a step, every read of a level issued before the next level; lookups run
+  // for every lane (inactive lanes hold a clamped real record) and the result is masked
+  // after: a select on the index made the compiler branch per IP
   __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
-    if (kRadix) {
+    if (kIp == 2) {  // one LDS read per IP
+      const uint16_t *blk = (const uint16_t *)smem;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = blk[(iprd_block(ip[k], p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip[k] >> 24)];
+    } else if (kIp == 1) {
       const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
-      // rows computed for every lane (inactive lanes hold a clamped real record) and the
-      // result masked after: a select on the index made the compiler branch per IP
       uint32_t bi[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) bi[k] = bidx[ipr_row(ip[k], p0, p1, p2, p3, npfx)];
 #pragma unroll
       for (int k = 0; k < 8; ++k) sl[k] = blk[(bi[k] << 8) | (ip[k] >> 24)];
+    } else {
+      const uint32_t *keys = (const uint32_t *)smem;
+      const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+      uint32_t j[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
-      return;
+      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
     }
-    const uint32_t *keys = (const uint32_t *)smem;
-    const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
-    uint32_t j[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
   }
 };
 
-template <int NG, bool kVec, uint32_t SIG, bool kRadix>
+template <int NG, bool kVec, uint32_t SIG, int kIp>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const IplView<kRadix> iv{smem, a.ipl_nb, a.ipl_seed, a.ipl_npfx, a.ipl_pfx[0], a.ipl_pfx[1], a.ipl_pfx[2],
-                           a.ipl_pfx[3]};
+  const IplView<kIp> iv{smem,          a.ipl_nb,     a.ipl_seed,   a.ipl_npfx,   a.ipl_pfx[0], a.ipl_pfx[1],
+                        a.ipl_pfx[2],  a.ipl_pfx[3], a.ipl_dr[0],  a.ipl_dr[1],  a.ipl_dr[2],  a.ipl_dr[3]};
   uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
   const uint32_t L4 = a.lds_bins;
   for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
@@ -1787,7 +1793,8 @@ struct SketchK {
   uint32_t hll_slots; // slots covered by the registers
   const uint8_t *ipl; // LDS image of every pod IP (source lookups), or null: HBM table
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
-  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (sketch_stage_kernel<2, .>)
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];  // radix image (sketch_stage_kernel<2 / 3, .>)
+  uint32_t ipl_dr[kIprMaxPfx];             // dense radix descriptors (<3, .>)
   // LDS staging of list appends (sketch_stage_kernel): per count-min window sbc u16 and
   // per HLL super-window sbh u32 entries (powers of two), flushed every `round` records
   // per lane (2 or 4) as contiguous runs
@@ -1951,7 +1958,8 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
 // flight per lane instead of one after another.  A position past the ring (rare: rings
 // hold 1.5 x a round's mean + 64) is stored straight into the list at rb + pos; a list
 // position past the capacity falls back to the global atomic (exact).
-// kIp: source lookup 0 HBM table, 1 LDS cuckoo image, 2 LDS radix image.
+// kIp: source lookup 0 HBM table, 1 LDS cuckoo image, 2 LDS radix image, 3 LDS dense radix
+// image.
 // kD: count-min depth fixed at compile time (4), or 0 = k.depth.
 __host__ __device__ inline uint32_t stage_words(uint32_t nwin, uint32_t hnsup, uint32_t sbc, uint32_t sbh) {
   // rc, rb per window + hc, hb per super-window; u16 rings (+ one dummy u32); u32 rings
@@ -1980,8 +1988,10 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
   const uint32_t lane = threadIdx.x & 63u;
   uint16_t *mine = k.lists + (size_t)blockIdx.x * nw * k.cap;
   uint32_t *hmine = k.hlists + (size_t)blockIdx.x * nh * k.hcap;
-  const IplView<kIp == 2> iv{img, k.ipl_nb, k.ipl_seed, k.ipl_npfx, k.ipl_pfx[0], k.ipl_pfx[1], k.ipl_pfx[2],
-                             k.ipl_pfx[3]};
+  // kIp 1 / 2 / 3: the cuckoo / radix / dense radix image (IplView kinds 0 / 1 / 2)
+  const IplView<kIp == 3 ? 2 : kIp == 2 ? 1 : 0> iv{img,          k.ipl_nb,     k.ipl_seed,   k.ipl_npfx,
+                                                    k.ipl_pfx[0], k.ipl_pfx[1], k.ipl_pfx[2], k.ipl_pfx[3],
+                                                    k.ipl_dr[0],  k.ipl_dr[1],  k.ipl_dr[2],  k.ipl_dr[3]};
   auto src_slot = [&](uint32_t ip) -> uint32_t {  // slot or >= hll_slots
     if (kIp) return iv.lookup(ip);
     const Lk l = k.p ? ip_lookup(k.t, ip) : Lk{-1, 0};
@@ -2449,10 +2459,13 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   // rings do not fit; sources looked up in the radix image when the pod IPs allow one
   bool staged = false;
   if (vec && (!a.cms_depth || a.nwin) && (!a.hll_p || a.hll_nsup) && (a.nwin || a.hll_nsup)) {
-    const int ip_kind = lds_ip ? (a.ipl_radix ? 2 : 1) : 0;
+    const int ip_kind = lds_ip ? (a.ipl_dense ? 3 : a.ipl_radix ? 2 : 1) : 0;
     if (lds_ip) {
       k.ipl_npfx = a.ipl_npfx;
-      for (uint32_t j = 0; j < kIprMaxPfx; ++j) k.ipl_pfx[j] = a.ipl_pfx[j];
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+        k.ipl_pfx[j] = a.ipl_pfx[j];
+        k.ipl_dr[j] = a.ipl_dr[j];
+      }
     }
     const uint32_t img = lds_ip ? a.ipl_bytes : 0u;
     for (uint32_t round : {4u, 2u}) {
@@ -2470,11 +2483,14 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
       k.sbh = sbh;
       k.round = round;
       const bool d4 = a.cms_depth == 4;
-      const void *fn = ip_kind == 2 ? (d4 ? (const void *)sketch_stage_kernel<2, 4> : (const void *)sketch_stage_kernel<2, 0>)
+      const void *fn = ip_kind == 3 ? (d4 ? (const void *)sketch_stage_kernel<3, 4> : (const void *)sketch_stage_kernel<3, 0>)
+                     : ip_kind == 2 ? (d4 ? (const void *)sketch_stage_kernel<2, 4> : (const void *)sketch_stage_kernel<2, 0>)
                      : ip_kind == 1 ? (d4 ? (const void *)sketch_stage_kernel<1, 4> : (const void *)sketch_stage_kernel<1, 0>)
                                     : (d4 ? (const void *)sketch_stage_kernel<0, 4> : (const void *)sketch_stage_kernel<0, 0>);
       if ((e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess) return e;
-      if (ip_kind == 2 && d4) hipLaunchKernelGGL((sketch_stage_kernel<2, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
+      if (ip_kind == 3 && d4) hipLaunchKernelGGL((sketch_stage_kernel<3, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (ip_kind == 3) hipLaunchKernelGGL((sketch_stage_kernel<3, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
+      else if (ip_kind == 2 && d4) hipLaunchKernelGGL((sketch_stage_kernel<2, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
       else if (ip_kind == 2) hipLaunchKernelGGL((sketch_stage_kernel<2, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
       else if (ip_kind == 1 && d4) hipLaunchKernelGGL((sketch_stage_kernel<1, 4>), dim3(a.blocks), dim3(1024), lds, st, k);
       else if (ip_kind == 1) hipLaunchKernelGGL((sketch_stage_kernel<1, 0>), dim3(a.blocks), dim3(1024), lds, st, k);
@@ -2488,7 +2504,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   }
   if (!staged) {
   // the unstaged kernel probes the cuckoo image only: a radix image is looked up in HBM
-  const bool lds_ip = lds_ip_any && !a.ipl_radix;
+  const bool lds_ip = lds_ip_any && !a.ipl_radix && !a.ipl_dense;
   if (!lds_ip) scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   const void *fn = vec ? (lds_ip ? (const void *)sketch_scatter_kernel<true, true>
                                  : (const void *)sketch_scatter_kernel<true, false>)
@@ -2895,10 +2911,12 @@ static hipError_t launch_k(K kern, const KArgs &k, uint32_t blocks, uint32_t thr
 template <int NG, uint32_t SIG>
 static hipError_t launch_lds(const LaunchArgs &a, const KArgs &k, uint32_t B, uint32_t T, size_t lds, hipStream_t st) {
   if (a.vec)
-    return a.ipl_radix ? launch_k(dense_lds_kernel<NG, true, SIG, true>, k, B, T, lds, st)
-                       : launch_k(dense_lds_kernel<NG, true, SIG, false>, k, B, T, lds, st);
-  return a.ipl_radix ? launch_k(dense_lds_kernel<NG, false, SIG, true>, k, B, T, lds, st)
-                     : launch_k(dense_lds_kernel<NG, false, SIG, false>, k, B, T, lds, st);
+    return a.ipl_dense   ? launch_k(dense_lds_kernel<NG, true, SIG, 2>, k, B, T, lds, st)
+           : a.ipl_radix ? launch_k(dense_lds_kernel<NG, true, SIG, 1>, k, B, T, lds, st)
+                         : launch_k(dense_lds_kernel<NG, true, SIG, 0>, k, B, T, lds, st);
+  return a.ipl_dense   ? launch_k(dense_lds_kernel<NG, false, SIG, 2>, k, B, T, lds, st)
+         : a.ipl_radix ? launch_k(dense_lds_kernel<NG, false, SIG, 1>, k, B, T, lds, st)
+                       : launch_k(dense_lds_kernel<NG, false, SIG, 0>, k, B, T, lds, st);
 }
 
 hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t between, const char **kernel) {
@@ -2924,7 +2942,10 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.ipl_seed = a.ipl_seed;
   k.ipl_bytes = a.ipl_bytes;
   k.ipl_npfx = a.ipl_npfx;
-  for (uint32_t j = 0; j < kIprMaxPfx; ++j) k.ipl_pfx[j] = a.ipl_pfx[j];
+  for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+    k.ipl_pfx[j] = a.ipl_pfx[j];
+    k.ipl_dr[j] = a.ipl_dr[j];
+  }
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
   k.sp_lists = (unsigned long long *)a.sp_lists;
@@ -3024,9 +3045,9 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (kernel) {
     static thread_local char name[64];
     if (a.tier1)
-      snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu, %s>",
+      snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu, %d>",
                variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng, a.vec ? "true" : "false",
-               variant >= 200 ? a.sig : 0u, a.ipl_radix ? "true" : "false");
+               variant >= 200 ? a.sig : 0u, a.ipl_dense ? 2 : a.ipl_radix ? 1 : 0);
     else if (a.dense_ng)
       snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu%s>", a.dense_ng, a.vec ? "true" : "false",
                a.dns_compact ? "true" : "false", variant >= 305 ? a.sig : 0u, variant == 306 ? ", true" : "");

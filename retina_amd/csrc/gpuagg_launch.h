@@ -61,7 +61,8 @@ struct LaunchArgs {
   const uint8_t *ipl;
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   bool ipl_radix;                   // radix image (ipr_build): prefixes below, no nb / seed
-  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];
+  bool ipl_dense;                   // dense radix image (iprd_build): prefixes + descriptors
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx], ipl_dr[kIprMaxPfx];
   // staged flushes (null: flush with global atomics)
   uint32_t *stage_a;        // tier-1: [blocks][stage_a_stride] copies of the u32 LDS bins
   uint32_t stage_a_stride;
@@ -199,7 +200,8 @@ struct SketchArgs {
   const uint8_t *ipl;               // LDS image of every pod IP for the source lookup, or null
   uint32_t ipl_nb, ipl_seed, ipl_bytes;
   bool ipl_radix;                   // the image is the radix form (ipl_npfx / ipl_pfx)
-  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx];
+  bool ipl_dense;                   // ... the dense radix form (ipl_pfx / ipl_dr)
+  uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx], ipl_dr[kIprMaxPfx];
 };
 // *kernels: the pass's kernels in rocprofv3 spelling joined by "+"
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels);

@@ -230,12 +230,12 @@ struct gpuagg_ctx {
   uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
   size_t ipl_all_alloc = 0;
   uint32_t ipl_all_nb = 0, ipl_all_seed = 0, ipl_all_bytes = 0;
-  bool ipl_all_radix = false;  // radix form (<= kIprMaxPfx /16 prefixes), else cuckoo
-  uint32_t ipl_all_npfx = 0, ipl_all_pfx[kIprMaxPfx] = {};
+  bool ipl_all_radix = false, ipl_all_dense = false;  // image form (build_lds_image)
+  uint32_t ipl_all_npfx = 0, ipl_all_pfx[kIprMaxPfx] = {}, ipl_all_dr[kIprMaxPfx] = {};
   uint32_t ipl_nb = 0, ipl_seed = 0, ipl_bytes = 0;
-  // the tier-1 image is the radix form (ipr_build) when the pod IPs allow it
-  bool ipl_radix = false;
-  uint32_t ipl_npfx = 0, ipl_pfx[kIprMaxPfx] = {};
+  // the tier-1 image: dense radix, radix or cuckoo form (build_lds_image)
+  bool ipl_radix = false, ipl_dense = false;
+  uint32_t ipl_npfx = 0, ipl_pfx[kIprMaxPfx] = {}, ipl_dr[kIprMaxPfx] = {};
   uint64_t ip_version = 0;
 
   // dense counters
@@ -760,8 +760,12 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     s.ipl_seed = c->ipl_all_seed;
     s.ipl_bytes = c->ipl_all_bytes;
     s.ipl_radix = c->ipl_all_radix;
+    s.ipl_dense = c->ipl_all_dense;
     s.ipl_npfx = c->ipl_all_npfx;
-    for (uint32_t j = 0; j < kIprMaxPfx; ++j) s.ipl_pfx[j] = c->ipl_all_pfx[j];
+    for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+      s.ipl_pfx[j] = c->ipl_all_pfx[j];
+      s.ipl_dr[j] = c->ipl_all_dr[j];
+    }
   }
   // HLL bucketing: fine windows of 2^hll_shift pods (128 KiB of registers, the fold's
   // LDS), super-windows of 2^hll_sshift pods (~16 of them, the scatter's lists); pod bits
@@ -1101,8 +1105,12 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.ipl_seed = c->ipl_seed;
       a.ipl_bytes = c->ipl_bytes;
       a.ipl_radix = c->ipl_radix;
+      a.ipl_dense = c->ipl_dense;
       a.ipl_npfx = c->ipl_npfx;
-      for (uint32_t j = 0; j < kIprMaxPfx; ++j) a.ipl_pfx[j] = c->ipl_pfx[j];
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+        a.ipl_pfx[j] = c->ipl_pfx[j];
+        a.ipl_dr[j] = c->ipl_dr[j];
+      }
     }
   }
   // one 1024-thread workgroup per CU whenever LDS holds bins or spill counters: with
@@ -1769,6 +1777,46 @@ int gpuagg_slot_intern(gpuagg_ctx *c, const char *ns, const char *pod, const cha
   return GPUAGG_OK;
 }
 
+// An LDS image of (ip, slot) entries in the cheapest form the set allows: dense radix
+// (one u16 read per lookup), radix with its row table (two), else the bucketized cuckoo
+// table.  GPUAGG_FLAG_LDS_CUCKOO / GPUAGG_FLAG_ROW_RADIX force the latter forms
+// (diagnostics and tests).
+struct LdsImage {
+  bool radix = false, dense = false;
+  uint32_t nb = 0, seed = 0, npfx = 0;
+  uint32_t pfx[kIprMaxPfx] = {kIprNoPfx, kIprNoPfx, kIprNoPfx, kIprNoPfx}, dr[kIprMaxPfx] = {};
+  std::vector<uint8_t> bytes;
+};
+bool build_lds_image(const std::vector<std::pair<uint32_t, uint32_t>> &ents, uint32_t flags, LdsImage *out) {
+  if (!(flags & GPUAGG_FLAG_LDS_CUCKOO)) {
+    IprdImage id;
+    if (!(flags & GPUAGG_FLAG_ROW_RADIX) && iprd_build(ents, &id)) {
+      out->radix = out->dense = true;
+      out->npfx = id.npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+        out->pfx[j] = id.pfx[j];
+        out->dr[j] = id.dr[j];
+      }
+      out->bytes = std::move(id.bytes);
+      return true;
+    }
+    IprImage ir;
+    if (ipr_build(ents, &ir)) {
+      out->radix = true;
+      out->npfx = ir.npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) out->pfx[j] = ir.pfx[j];
+      out->bytes = std::move(ir.bytes);
+      return true;
+    }
+  }
+  IplImage im;
+  if (!ipl_build(ents, &im)) return false;
+  out->nb = im.nb;
+  out->seed = im.seed;
+  out->bytes = std::move(im.bytes);
+  return true;
+}
+
 int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slot, size_t n,
                          uint64_t version) {
   if (!c || (n && (!ipv4 || !slot))) return GPUAGG_EINVAL;
@@ -1877,24 +1925,25 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     for (const auto &kv : last)
       if (!((kv.second >> 53) & 1))
         ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
-    IplImage im;
-    IprImage ir;
-    const bool radix = !(c->cfg.flags & GPUAGG_FLAG_LDS_CUCKOO) && ipr_build(ents, &ir);
-    if (radix || ipl_build(ents, &im)) {
-      const std::vector<uint8_t> &img = radix ? ir.bytes : im.bytes;
-      const uint32_t bytes = (uint32_t)img.size();
+    LdsImage im;
+    if (build_lds_image(ents, c->cfg.flags, &im)) {
+      const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_alloc) {
         dev_free(c, c->d_ipl);
         c->ipl_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl, bytes))) return rc;
         c->ipl_alloc = bytes;
       }
-      HIPCHK(c, x_copy(c, c->d_ipl, img.data(), bytes, hipMemcpyHostToDevice));
-      c->ipl_radix = radix;
-      c->ipl_nb = radix ? 0 : im.nb;
-      c->ipl_seed = radix ? 0 : im.seed;
-      c->ipl_npfx = radix ? ir.npfx : 0;
-      for (uint32_t j = 0; j < kIprMaxPfx; ++j) c->ipl_pfx[j] = radix ? ir.pfx[j] : kIprNoPfx;
+      HIPCHK(c, x_copy(c, c->d_ipl, im.bytes.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_radix = im.radix;
+      c->ipl_dense = im.dense;
+      c->ipl_nb = im.nb;
+      c->ipl_seed = im.seed;
+      c->ipl_npfx = im.npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+        c->ipl_pfx[j] = im.pfx[j];
+        c->ipl_dr[j] = im.dr[j];
+      }
       c->ipl_bytes = bytes;
     }
   }
@@ -1904,26 +1953,25 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
   if (c->cfg.hll_precision && !(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
     std::vector<std::pair<uint32_t, uint32_t>> ents;
     for (const auto &kv : last) ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
-    IplImage im;
-    IprImage ir;
-    // radix form when the pod IPs allow one (two dependent u16 reads per source and a
-    // smaller image, leaving LDS for larger staging rings), else the cuckoo image
-    const bool radix = !(c->cfg.flags & GPUAGG_FLAG_LDS_CUCKOO) && ipr_build(ents, &ir);
-    if (radix || ipl_build(ents, &im)) {
-      const std::vector<uint8_t> &img = radix ? ir.bytes : im.bytes;
-      const uint32_t bytes = (uint32_t)img.size();
+    LdsImage im;
+    if (build_lds_image(ents, c->cfg.flags, &im)) {
+      const uint32_t bytes = (uint32_t)im.bytes.size();
       if (bytes > c->ipl_all_alloc) {
         dev_free(c, c->d_ipl_all);
         c->ipl_all_alloc = 0;
         if ((rc = dev_alloc(c, &c->d_ipl_all, bytes))) return rc;
         c->ipl_all_alloc = bytes;
       }
-      HIPCHK(c, x_copy(c, c->d_ipl_all, img.data(), bytes, hipMemcpyHostToDevice));
-      c->ipl_all_radix = radix;
-      c->ipl_all_nb = radix ? 0 : im.nb;
-      c->ipl_all_seed = radix ? 0 : im.seed;
-      c->ipl_all_npfx = radix ? ir.npfx : 0;
-      for (uint32_t j = 0; j < kIprMaxPfx; ++j) c->ipl_all_pfx[j] = radix ? ir.pfx[j] : kIprNoPfx;
+      HIPCHK(c, x_copy(c, c->d_ipl_all, im.bytes.data(), bytes, hipMemcpyHostToDevice));
+      c->ipl_all_radix = im.radix;
+      c->ipl_all_dense = im.dense;
+      c->ipl_all_nb = im.nb;
+      c->ipl_all_seed = im.seed;
+      c->ipl_all_npfx = im.npfx;
+      for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+        c->ipl_all_pfx[j] = im.pfx[j];
+        c->ipl_all_dr[j] = im.dr[j];
+      }
       c->ipl_all_bytes = bytes;
     }
   }

@@ -142,4 +142,63 @@ inline uint32_t ipr_probe(const IprImage &im, uint32_t ip) {
   return blk[((uint32_t)bidx[row] << 8) | (ip >> 24)];
 }
 
+// ---- dense radix LDS image (gpuagg_internal.h, "Dense radix LDS image") ---------------
+struct IprdImage {
+  uint32_t npfx = 0, nblk = 0;
+  uint32_t pfx[kIprMaxPfx] = {kIprNoPfx, kIprNoPfx, kIprNoPfx, kIprNoPfx};
+  uint32_t dr[kIprMaxPfx] = {0, 0, 0, 0};
+  std::vector<uint8_t> bytes;  // blk u16[(nblk + 1) * 256]
+};
+
+// Returns false when the set needs more than kIprMaxPfx /16 prefixes, a slot >= 0xFFFF, or
+// more than max_bytes of image once each prefix's third-octet run [min, max] is filled
+// (holes included); the caller then tries the radix image with its row table.
+inline bool iprd_build(const std::vector<std::pair<uint32_t, uint32_t>> &ents, IprdImage *out,
+                       uint32_t max_bytes = kIplMaxBytes) {
+  IprdImage im;
+  uint32_t lo[kIprMaxPfx] = {255, 255, 255, 255}, hi[kIprMaxPfx] = {0, 0, 0, 0};
+  auto pfx_of = [&](uint32_t ip) {
+    uint32_t j = 0;
+    while (j < im.npfx && im.pfx[j] != (ip & 0xFFFFu)) ++j;
+    return j;
+  };
+  for (const auto &e : ents) {
+    if (e.second >= kIplNoSlot) return false;
+    uint32_t j = pfx_of(e.first);
+    if (j == im.npfx) {
+      if (im.npfx == kIprMaxPfx) return false;
+      im.pfx[im.npfx++] = e.first & 0xFFFFu;
+    }
+    const uint32_t o3 = (e.first >> 16) & 0xFFu;
+    lo[j] = o3 < lo[j] ? o3 : lo[j];
+    hi[j] = o3 > hi[j] ? o3 : hi[j];
+  }
+  uint32_t base = 1;
+  for (uint32_t j = 0; j < im.npfx; ++j) {
+    const uint32_t cnt = hi[j] - lo[j] + 1;
+    im.dr[j] = lo[j] | (cnt << 8) | (base << 17);
+    base += cnt;
+  }
+  im.nblk = base - 1;
+  if ((size_t)(im.nblk + 1) * 512 > max_bytes) return false;
+  std::vector<uint16_t> blk((size_t)(im.nblk + 1) * 256, (uint16_t)kIplNoSlot);
+  for (const auto &e : ents) {
+    const uint32_t b = iprd_block(e.first, im.pfx[0], im.pfx[1], im.pfx[2], im.pfx[3], im.dr[0], im.dr[1],
+                                  im.dr[2], im.dr[3]);
+    blk[((size_t)b << 8) | (e.first >> 24)] = (uint16_t)e.second;
+  }
+  im.bytes.assign(blk.size() * 2, 0);
+  memcpy(im.bytes.data(), blk.data(), blk.size() * 2);
+  *out = std::move(im);
+  return true;
+}
+
+// Host mirror of the kernel's dense radix probe: slot or kIplNoSlot.
+inline uint32_t iprd_probe(const IprdImage &im, uint32_t ip) {
+  const uint16_t *blk = (const uint16_t *)im.bytes.data();
+  const uint32_t b = iprd_block(ip, im.pfx[0], im.pfx[1], im.pfx[2], im.pfx[3], im.dr[0], im.dr[1], im.dr[2],
+                                im.dr[3]);
+  return blk[(b << 8) | (ip >> 24)];
+}
+
 }  // namespace gpuagg

@@ -52,9 +52,27 @@ int main() {
         rabsent += ipr_probe(ir, ip) != kIplNoSlot;  // wrong answers
       }
     }
-    printf("%d %u %u %zu %.1f %ld %ld %d %u %u %zu %ld %ld\n", ok ? 1 : 0, im.nb, im.seed, im.bytes.size(),
-           ok ? 100.0 * n / (im.nb * kIplWays) : 0.0, found, absent_ok, rok ? 1 : 0, ir.npfx, ir.nblk,
-           ir.bytes.size(), rfound, rabsent);
+    // the dense radix image (per-prefix third-octet runs): same answers
+    IprdImage id;
+    const bool dok = iprd_build(ents, &id);
+    long dfound = 0, dabsent = 0;
+    if (dok) {
+      for (const auto &e : ents) dfound += iprd_probe(id, e.first) == e.second;
+      std::mt19937 rng(s + 2000);
+      std::vector<uint32_t> sorted;
+      for (const auto &e : ents) sorted.push_back(e.first);
+      std::sort(sorted.begin(), sorted.end());
+      for (int i = 0; i < 100000; ++i) {
+        uint32_t ip = rng();
+        if (i & 1 && !sorted.empty()) ip = (sorted[rng() % sorted.size()] & 0x00FFFFFFu) | (rng() & 0xFF000000u);
+        if (i % 3 == 0 && !sorted.empty()) ip = (sorted[rng() % sorted.size()] & 0xFF00FFFFu) | (rng() & 0x00FF0000u);
+        if (std::binary_search(sorted.begin(), sorted.end(), ip)) continue;
+        dabsent += iprd_probe(id, ip) != kIplNoSlot;  // wrong answers
+      }
+    }
+    printf("%d %u %u %zu %.1f %ld %ld %d %u %u %zu %ld %ld %d %u %zu %ld %ld\n", ok ? 1 : 0, im.nb, im.seed,
+           im.bytes.size(), ok ? 100.0 * n / (im.nb * kIplWays) : 0.0, found, absent_ok, rok ? 1 : 0, ir.npfx,
+           ir.nblk, ir.bytes.size(), rfound, rabsent, dok ? 1 : 0, id.nblk, id.bytes.size(), dfound, dabsent);
   }
   return 0;
 }

@@ -18,6 +18,7 @@ MID = [
     ("c1-remote", W.C1_REMOTE, True, 10_000, {}),
     ("c2-local", W.LOCAL_FWD_DROP, False, 10_000, {}),
     ("c2-local-lds-cuckoo", W.LOCAL_FWD_DROP, False, 10_000, {"flags": 64}),  # FLAG_LDS_CUCKOO
+    ("c2-local-row-radix", W.LOCAL_FWD_DROP, False, 10_000, {"flags": 256}),  # FLAG_ROW_RADIX
     ("c4-zipf", W.LOCAL_FWD_DROP, False, 10_000, {"zipf": 1.2}),
     ("c4-flows", W.LOCAL_FWD_DROP, False, 10_000, dict(W.CONFIGS["c4"]["gen"])),
     ("c4-flows-remote", W.C1_REMOTE, True, 10_000, dict(W.CONFIGS["c4"]["gen"])),
@@ -77,7 +78,8 @@ def test_host_fed_equals_device_and_chunking(gpu_device):
     assert a == b, diff_series(a, b)
 
 
-@pytest.mark.parametrize("flags", [0, 64, 1], ids=["tier1-radix", "tier1-cuckoo", "no-lds-ip-table"])
+@pytest.mark.parametrize("flags", [0, 256, 64, 1],
+                         ids=["tier1-dense-radix", "tier1-row-radix", "tier1-cuckoo", "no-lds-ip-table"])
 def test_packed_field_overflow_exact(gpu_device, flags):
     """Packed LDS counters (u32 count:12|bytes:20 in tier-1, u64 count:20|bytes:44 in the
     other kernels and the fold windows) must carry exactly.  One hot pod pair, 60M

@@ -23,9 +23,9 @@ pytestmark = pytest.mark.gpu
 SPEC = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
 
 
-def _run(recs, pods, gpu_device, d=4, w=20, p=14):
+def _run(recs, pods, gpu_device, d=4, w=20, p=14, flags=0):
     from retina_amd import GpuAgg
-    g = make_engine(pods, SPEC, False, gpu_device, cms_depth=d, cms_width_log2=w, hll_precision=p)
+    g = make_engine(pods, SPEC, False, gpu_device, cms_depth=d, cms_width_log2=w, hll_precision=p, flags=flags)
     try:
         g.submit_device(GpuAgg.device_columns(*to_device(recs, gpu_device)), len(recs))
         g.sync()
@@ -45,8 +45,11 @@ def _src_slots(pods, src):
     return np.where(lut_ips[pos] == src, lut_slot[pos], -1)
 
 
+# source lookups through each LDS image form: dense radix (default), radix with its row
+# table (FLAG_ROW_RADIX), bucketized cuckoo (FLAG_LDS_CUCKOO)
+@pytest.mark.parametrize("flags", [0, 256, 64], ids=["dense-radix", "row-radix", "cuckoo"])
 @pytest.mark.parametrize("zipf", [None, 1.2], ids=["uniform", "zipf"])
-def test_c3_shape_bit_exact(gpu_device, zipf):
+def test_c3_shape_bit_exact(gpu_device, zipf, flags):
     pods = W.make_pods(200, seed=41)
     recs = W.gen_records(3_000_000, pods, seed=42, udp_frac=0.2, zipf=zipf)
     if zipf:  # heavy 5-tuples: repeat a few flows so some count-min windows overflow
@@ -54,7 +57,7 @@ def test_c3_shape_bit_exact(gpu_device, zipf):
         recs.dst_ip[hot] = recs.dst_ip[0]
         recs.src_ip[hot] = recs.src_ip[0]
         recs.ports[hot] = recs.ports[0]
-    cms, hll = _run(recs, pods, gpu_device)
+    cms, hll = _run(recs, pods, gpu_device, flags=flags)
     want = np.zeros((4, 1 << 20), np.uint32)
     S.cms_update(want, recs.src_ip, recs.dst_ip, recs.ports, recs.meta & np.uint32(0xFF))
     assert np.array_equal(cms, want)

@@ -31,10 +31,13 @@ def run_sets(exe, sets):
     res = []
     for ln in out:
         if ln.strip():
-            built, nb, seed, nbytes, load, found, absent, rbuilt, npfx, nblk, rbytes, rfound, rabsent = ln.split()
+            (built, nb, seed, nbytes, load, found, absent, rbuilt, npfx, nblk, rbytes, rfound, rabsent,
+             dbuilt, dnblk, dbytes, dfound, dabsent) = ln.split()
             res.append(dict(built=int(built), nb=int(nb), bytes=int(nbytes), load=float(load),
                             found=int(found), absent=int(absent), rbuilt=int(rbuilt), npfx=int(npfx),
-                            nblk=int(nblk), rbytes=int(rbytes), rfound=int(rfound), rabsent=int(rabsent)))
+                            nblk=int(nblk), rbytes=int(rbytes), rfound=int(rfound), rabsent=int(rabsent),
+                            dbuilt=int(dbuilt), dnblk=int(dnblk), dbytes=int(dbytes), dfound=int(dfound),
+                            dabsent=int(dabsent)))
     return res
 
 
@@ -84,3 +87,27 @@ def test_radix_image_matches(harness):
     # more than 4 prefixes, or a reserved slot id, refuse
     r = run_sets(harness, [[(0x0A00 + k | (i << 24), i) for k in range(5) for i in range(3)], [(1, 0xFFFF)]])
     assert [x["rbuilt"] for x in r] == [0, 0]
+
+
+def test_dense_radix_image_matches(harness):
+    """The dense radix image (each prefix's /24s one run of third octets, no row table):
+    every key found with its slot, absent IPs -- random, next to pod IPs, and in the
+    pods' /16s outside their /24 runs -- miss; C2's 10k pods: 2 runs of <= 40 /24s."""
+    sets = pod_sets()
+    res = run_sets(harness, sets)
+    for ents, r in zip(sets, res):
+        if not r["dbuilt"]:
+            continue
+        assert r["dfound"] == len(ents)
+        assert r["dabsent"] == 0
+        assert r["dbytes"] <= 112 * 1024
+    c2 = res[4]
+    assert c2["dbuilt"] == 1 and 78 <= c2["dnblk"] <= 80 and c2["dbytes"] == (c2["dnblk"] + 1) * 512
+    assert res[5]["dbuilt"] == 0  # random IPs: far more than 4 prefixes
+    # a run with holes gets empty blocks for them; a run too long for the budget refuses
+    holes = [(0x0A0A | (o3 << 16) | (7 << 24), o3) for o3 in (3, 9, 200)]
+    wide = [(0x0A0A | (o3 << 16) | (k << 24), o3 * 256 + k) for o3 in range(256) for k in (1, 2)] + \
+           [(0x0B0A | (o3 << 16) | (1 << 24), 7) for o3 in range(0, 256, 2)]
+    r = run_sets(harness, [holes, wide])
+    assert r[0]["dbuilt"] == 1 and r[0]["dnblk"] == 198 and r[0]["dfound"] == 3 and r[0]["dabsent"] == 0
+    assert r[1]["dbuilt"] == 0  # 512 blocks of 512 B: more than 112 KiB
