@@ -2180,18 +2180,6 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
         nm = rec_ld(&m4[vn]);
         np = need_ports ? rec_ld(&p4[vn]) : z4;
       }
-#ifdef EXP_NR4
-      if (k.round == 4) {  // all four records' updates in flight together
-        const bool act4[4] = {a, a, a, a};
-        const uint32_t s[4] = {vs.x, vs.y, vs.z, vs.w}, d[4] = {vd.x, vd.y, vd.z, vd.w};
-        const uint32_t pt[4] = {vp.x, vp.y, vp.z, vp.w}, mt[4] = {vm.x, vm.y, vm.z, vm.w};
-        records(std::integral_constant<int, 4>{}, s, d, pt, mt, act4);
-        __syncthreads();
-        flush();
-        __syncthreads();
-        continue;
-      }
-#endif
       const bool act[2] = {a, a};
       {
         const uint32_t s[2] = {vs.x, vs.y}, d[2] = {vd.x, vd.y}, pt[2] = {vp.x, vp.y}, mt[2] = {vm.x, vm.y};

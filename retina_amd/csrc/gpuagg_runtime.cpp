@@ -280,6 +280,11 @@ struct gpuagg_ctx {
   gpuagg_stats stats{};
   bool timing = false;
   std::vector<std::array<hipEvent_t, 3>> pending_events;  // start, after aggregate, after fold
+  // Timing events cost ~4 us of idle GPU each (a barrier packet): consecutive launches share
+  // one -- a launch's start is the previous launch's end event when nothing else was
+  // enqueued on the stream in between (tm_chain; ENQ() clears it at every other enqueue).
+  hipEvent_t tm_end = nullptr;
+  bool tm_chain = false;
   uint32_t n_cu = 256;
   // dense spill lists (per workgroup) for bins beyond the LDS window
   uint32_t *d_spill = nullptr;
@@ -350,6 +355,9 @@ int fail(gpuagg_ctx *c, int code, const char *fmt, ...) {
       return fail((c), GPUAGG_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(_e));   \
   } while (0)
 
+// Marks the stream as used by something other than launch()'s timed kernels.
+#define ENQ(c) ((c)->tm_chain = false)
+
 int bind(gpuagg_ctx *c) {
   if (c->cpu) return GPUAGG_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -364,11 +372,13 @@ hipError_t x_copy(gpuagg_ctx *c, void *dst, const void *src, size_t n, hipMemcpy
   return hipSuccess;
 }
 hipError_t x_copy_async(gpuagg_ctx *c, void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t st) {
+  ENQ(c);
   if (!c->cpu) return hipMemcpyAsync(dst, src, n, k, st);
   if (n) memmove(dst, src, n);
   return hipSuccess;
 }
 hipError_t x_set_async(gpuagg_ctx *c, void *p, int v, size_t n, hipStream_t st) {
+  ENQ(c);
   if (!c->cpu) return hipMemsetAsync(p, v, n, st);
   if (n) memset(p, v, n);
   return hipSuccess;
@@ -552,6 +562,7 @@ int fold_pending(gpuagg_ctx *c) {
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
+  ENQ(c);
   HIPCHK(c, launch_folds(f, c->stream));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -575,7 +586,10 @@ int reset_state(gpuagg_ctx *c) {
   if (c->sparse_slots) {
     HIPCHK(c, x_set_async(c, c->sv.dropped, 0, 8, c->stream));
     if (c->cpu) cpu::sparse_init(c->sv, c->sparse_slots);
-    else HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+    else {
+      ENQ(c);
+      HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
+    }
   }
   if (c->cms_len) HIPCHK(c, x_set_async(c, c->d_cms, 0, c->cms_len * 4, c->stream));
   if (c->hll_len) HIPCHK(c, x_set_async(c, c->d_hll, 0, c->hll_len, c->stream));
@@ -694,9 +708,17 @@ void drain_timing(gpuagg_ctx *c) {
       c->stats.fold_ms += fold;
       c->stats.kernel_launches += 1;
     }
-    for (hipEvent_t e : ev) hipEventDestroy(e);
+  }
+  // (a chained launch's start is the previous launch's end: each event destroyed once)
+  for (size_t i = 0; i < c->pending_events.size(); ++i) {
+    const auto &ev = c->pending_events[i];
+    if (i == 0 || ev[0] != c->pending_events[i - 1][2]) hipEventDestroy(ev[0]);
+    hipEventDestroy(ev[1]);
+    hipEventDestroy(ev[2]);
   }
   c->pending_events.clear();
+  c->tm_end = nullptr;
+  c->tm_chain = false;
   for (auto &ev : c->pending_decode) {
     float ms = 0.f;
     if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) {
@@ -833,6 +855,7 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       s.hll_lists2 = c->d_hll_lists2;
       s.hll_counts2 = c->d_hll_counts2;
     }
+    ENQ(c);
     HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
   }
   if (c->timing) {
@@ -938,6 +961,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8 * kLatReadWords, hipHostMallocDefault) != hipSuccess)
     return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", 8 * kLatReadWords);
   a.carry_in = c->d_lat_carry[c->lat_carry_cur];  // copied into the events by the front
+  ENQ(c);
   HIPCHK(c, launch_latency_front(a, c->stream));
   HIPCHK(c, x_copy_async(c, c->h_lat_n, c->d_lat + kLatPending, 8 * kLatReadWords, hipMemcpyDeviceToHost,
                            c->stream));
@@ -1278,8 +1302,14 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.dense_byt = c->d_dense_byt;
     std::array<hipEvent_t, 3> ev{};
     if (c->timing) {
-      for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
-      HIPCHK(c, hipEventRecord(ev[0], c->stream));
+      if (c->tm_chain && c->tm_end) {
+        ev[0] = c->tm_end;  // the previous launch's end: nothing ran in between
+      } else {
+        HIPCHK(c, hipEventCreateWithFlags(&ev[0], kTimingEventFlags));
+        HIPCHK(c, hipEventRecord(ev[0], c->stream));
+      }
+      HIPCHK(c, hipEventCreateWithFlags(&ev[1], kTimingEventFlags));
+      HIPCHK(c, hipEventCreateWithFlags(&ev[2], kTimingEventFlags));
     }
     const char *kname = nullptr;
     HIPCHK(c, launch_aggregate(a, c->stream, c->timing ? ev[1] : nullptr, &kname));
@@ -1293,6 +1323,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     if (c->timing) {
       HIPCHK(c, hipEventRecord(ev[2], c->stream));
       c->pending_events.push_back(ev);
+      c->tm_end = ev[2];
+      c->tm_chain = true;
     }
   }
   if ((c->cms_len || c->hll_len) && (rc = launch_sketches(c, cv, n))) return rc;
@@ -1327,6 +1359,7 @@ int decode(gpuagg_ctx *c, int kind, const void *dev_raw, size_t n, const OutCols
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
   DecodeArgs a{kind, dev_raw, n, out, c->d_decode_oor, c->n_cu, (uint64_t)c->time_offset};
+  ENQ(c);
   HIPCHK(c, launch_decode(a, c->stream));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -2114,6 +2147,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
       cpu::zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
                       c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan);
     else if (e == hipSuccess)
+      ENQ(c);
       e = launch_zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
                             c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan, c->stream);
     if (e == hipSuccess) e = x_sync(c, c->stream);
@@ -2150,10 +2184,12 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
         cpu::sparse_init(c->sv, c->sparse_slots);
         cpu::sparse_import(c->sv, ent.data(), keep);
       } else {
+        ENQ(c);
         HIPCHK(c, launch_sparse_init(c->sv, c->sparse_slots, c->stream));
         if (keep) {
           HIPCHK(c, x_copy_async(c, c->d_export, ent.data(), keep * kSparseEntryWords * 8, hipMemcpyHostToDevice,
                                    c->stream));
+          ENQ(c);
           HIPCHK(c, launch_sparse_import(c->sv, c->d_export, keep, c->stream));
         }
       }
@@ -2266,7 +2302,10 @@ int enrich_launch(gpuagg_ctx *c, const uint32_t *src, const uint32_t *dst, size_
   a.o_src = os;
   a.o_dst = od;
   if (c->cpu) c->cpu->enrich(a);
-  else HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
+  else {
+    ENQ(c);
+    HIPCHK(c, launch_enrich(a, c->n_cu, c->stream));
+  }
   return GPUAGG_OK;
 }
 
@@ -2793,6 +2832,7 @@ int gpuagg_sparse_export(gpuagg_ctx *c, uint64_t *dev_out, size_t cap, size_t *n
     return GPUAGG_OK;
   }
   HIPCHK(c, x_set_async(c, c->d_counter, 0, 8, c->stream));
+  ENQ(c);
   HIPCHK(c, launch_sparse_export(c->sv, c->sparse_slots, dev_out, cap, c->d_counter, c->stream));
   uint64_t n = 0;
   HIPCHK(c, x_copy_async(c, &n, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
@@ -2813,6 +2853,7 @@ int gpuagg_sparse_import(gpuagg_ctx *c, const uint64_t *dev_in, size_t n) {
     cpu::sparse_import(c->sv, dev_in, n);
     return GPUAGG_OK;
   }
+  ENQ(c);
   HIPCHK(c, launch_sparse_import(c->sv, dev_in, n, c->stream));
   HIPCHK(c, x_sync(c, c->stream));
   return GPUAGG_OK;
@@ -2925,6 +2966,8 @@ int merge_rccl(gpuagg_ctx *const *ctxs, size_t n, const std::vector<int> &devs) 
 }  // namespace
 
 int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
+  for (size_t i = 0; ctxs && i < n; ++i)
+    if (ctxs[i]) ENQ(ctxs[i]);
   if (!ctxs || !n || !ctxs[0]) return GPUAGG_EINVAL;
   gpuagg_ctx *c0 = ctxs[0];
   int rc;
@@ -3144,7 +3187,10 @@ int gpuagg_hubble_decode_device(gpuagg_ctx *c, const gpuagg_columns *in, size_t 
   a.o_kind = out->summary_kind;
   a.o_arg = out->summary_arg;
   if (c->cpu) c->cpu->hubble(a);
-  else HIPCHK(c, launch_hubble(a, c->n_cu, c->stream));
+  else {
+    ENQ(c);
+    HIPCHK(c, launch_hubble(a, c->n_cu, c->stream));
+  }
   return GPUAGG_OK;
 }
 
@@ -3200,6 +3246,7 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   if (!c) return GPUAGG_EINVAL;
   if (c->cpu) c->host_timing = enabled != 0;  // host wall time of the launches (no HIP events)
   else c->timing = enabled != 0;
+  c->tm_chain = false;
   if (!enabled) {
     c->stats.kernel_ms = 0;
     c->stats.fold_ms = 0;
