@@ -475,9 +475,6 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
 // may claim a free cache entry on its second sighting in the workgroup (doorkeeper
 // bitmap), so the long tail of keys seen once does not take the entries.
 __device__ __forceinline__ void wide_insert(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t b) {
-#ifdef EXP_SKIP_INSERT
-  if (k0 != 12345) return;
-#endif
   const uint64_t kh = key_hash(k0, k1, k2);
   bool claim = true;
   if (s.door_log2) {
@@ -2068,12 +2065,12 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
           if (!kD && (uint32_t)r >= D) break;
           const uint32_t w = we[j][r] >> 16, p = pos[j][r];
           const bool ring = p < sbc;
-          cst[ring ? w * sbc + p : cdummy] = (uint16_t)we[j][r];
+          cst[ring ? mul_u24(w, sbc) + p : cdummy] = (uint16_t)we[j][r];  // 24-bit: full-rate multiply
           slow |= act[j] & !ring;
         }
       }
       const bool hring = hp[j] < sbh;
-      hst[hring ? hw[j] * sbh + hp[j] : hdummy + lane] = he[j];
+      hst[hring ? mul_u24(hw[j], sbh) + hp[j] : hdummy + lane] = he[j];
       slow |= hv[j] & !hring;
     }
     if (__builtin_expect(__ballot(slow) != 0, 0)) {  // past a ring: list at rb + pos, or global
@@ -2121,7 +2118,7 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
           const uint32_t p = lane + 64u * it;
-          v[q][it] = p < min(n[q], sb) ? ring[(w0 + q * nwaves) * sb + p] : (T)0;
+          v[q][it] = p < min(n[q], sb) ? ring[mul_u24(w0 + q * nwaves, sb) + p] : (T)0;
         }
 #pragma unroll
       for (int q = 0; q < kG; ++q) {
