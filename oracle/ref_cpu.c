@@ -710,7 +710,7 @@ static void *tuned_worker(void *p) {
    * rehashing while the range streams through */
   size_t want = 4096;
   const size_t est = 4 * (j->b - j->a) / (size_t)(j->nparts > 0 ? j->nparts : 1);
-  while (want < est && want < ((size_t)1 << 22)) want <<= 1;
+  while (want < est && want < ((size_t)1 << 16)) want <<= 1;  /* grows by rehash beyond */
   for (int q = 0; q < j->nparts; ++q) {
     imap_t *m = &j->maps[q];
     m->cap = want;

@@ -303,9 +303,11 @@ constexpr uint32_t kSparseSegLog2 = 13, kSparseMaxSegLists = 4096;
 // (sparse_fold_wide_kernel); tables of up to 2^24 slots (4096 segments) take the
 // per-segment lists, bigger ones probe the whole table with memory-side atomics.
 constexpr uint32_t kWideSegLog2 = 12, kWideMaxLog2 = kWideSegLog2 + 12;
-// A wide list entry: k0 k1 k2 and count << 40 | bytes (updates that do not fit go to the
-// table directly)
-constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40;
+// A wide list entry: k0 k1 k2 and home << 52 | count << 40 | bytes -- home = the key's slot
+// in its segment (key_hash & (2^kWideSegLog2 - 1)), so the fold does not hash the key again;
+// updates whose count or bytes do not fit the fields go to the table directly
+constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40, kWideHomeShift = 52;
+static_assert(kWideHomeShift + kWideSegLog2 == 64, "home field fills the word");
 constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------

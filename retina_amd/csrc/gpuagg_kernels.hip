@@ -314,13 +314,14 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
 // sum too wide for the entry, goes to the table directly (exact).  kh = key_hash(k0, k1, k2).
 __device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t kh, uint64_t k0, uint64_t k1, uint64_t k2,
                                             uint64_t c, uint64_t b) {
-  if (c < (1ULL << (64 - kWideCountShift)) && b < (1ULL << kWideCountShift)) {
+  if (c < (1ULL << (kWideHomeShift - kWideCountShift)) && b < (1ULL << kWideCountShift)) {
     const uint32_t w = ((uint32_t)kh & s.mask) >> s.seg_log2;
     const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
     if (pos < s.lcap) {
+      const uint64_t home = (uint64_t)((uint32_t)kh & ((1u << s.seg_log2) - 1u));
       ulonglong2 *e = (ulonglong2 *)(s.lists + ((size_t)w * s.lcap + pos) * kWideEntryWords);
       e[0] = make_ulonglong2(k0, k1);
-      e[1] = make_ulonglong2(k2, (c << kWideCountShift) | b);
+      e[1] = make_ulonglong2(k2, (home << kWideHomeShift) | (c << kWideCountShift) | b);
       return;
     }
   }
@@ -1048,8 +1049,7 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     seg[f * N + slot] = g[j];
   }
   __syncthreads();
-  auto insert = [&](uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {
-    const uint32_t h = (uint32_t)key_hash(x0, x1, x2) & smask;
+  auto insert = [&](uint32_t h, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {  // h: home slot
     for (uint32_t probe = 0; probe < N; ++probe) {
       const uint32_t i = (h + probe) & smask;
       const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
@@ -1078,7 +1078,9 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     const ulonglong2 *e = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap * kWideEntryWords);
     for (uint32_t k = sub; k < cnt; k += lpl) {
       const ulonglong2 a0 = e[2 * k], a1 = e[2 * k + 1];
-      insert(a0.x, a0.y, a1.x, a1.y >> kWideCountShift, a1.y & ((1ULL << kWideCountShift) - 1));
+      insert((uint32_t)(a1.y >> kWideHomeShift) & smask, a0.x, a0.y, a1.x,
+             (a1.y >> kWideCountShift) & ((1ULL << (kWideHomeShift - kWideCountShift)) - 1),
+             a1.y & ((1ULL << kWideCountShift) - 1));
     }
   }
   __syncthreads();
