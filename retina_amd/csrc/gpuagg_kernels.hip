@@ -679,6 +679,21 @@ __device__ __forceinline__ uint4 rec_ld(const uint4 *p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Workgroup copy of n 16-byte words from global memory into LDS with 4 loads in flight per
+// lane before their LDS stores (a plain loop waits on each load: the compiler cannot move a
+// load of a generic pointer above the previous iteration's LDS store).
+__device__ __forceinline__ void fill_lds_u4(uint4 *dst, const uint4 *src, uint32_t n) {
+  uint32_t i = threadIdx.x;
+  for (; i + 3 * blockDim.x < n; i += 4 * blockDim.x) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = src[i + q * blockDim.x];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[i + q * blockDim.x] = v[q];
+  }
+  for (; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
 struct NoRounds {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -967,7 +982,7 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
   extern __shared__ __attribute__((aligned(16))) unsigned long long seg[];
   const uint32_t w = blockIdx.x, nslot = 1u << s.seg_log2, smask = nslot - 1u;
   ulonglong2 *g = (ulonglong2 *)(s.k0 + 2ull * ((size_t)w << s.seg_log2));
-  for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) ((ulonglong2 *)seg)[i] = g[i];
+  fill_lds_u4((uint4 *)seg, (const uint4 *)g, nslot);
   __syncthreads();
   auto insert = [&](unsigned long long key) {
     const uint32_t h = compact_home(s, key);
@@ -1044,9 +1059,22 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   if (!work) return;
   unsigned long long *K0 = seg, *K1 = seg + N, *K2 = seg + 2 * N, *CN = seg + 3 * N, *BY = seg + 4 * N;
   unsigned long long *g = s.k0 + (size_t)kSparseSlotWords * ((size_t)w << s.seg_log2);
-  for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {  // coalesced words
-    const uint32_t slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
-    seg[f * N + slot] = g[j];
+  // coalesced words, 4 loads in flight per lane before their LDS stores
+  const uint32_t nw5 = kSparseSlotWords * N;
+  uint32_t j0 = threadIdx.x;
+  for (; j0 + 3 * blockDim.x < nw5; j0 += 4 * blockDim.x) {
+    unsigned long long v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = g[j0 + q * blockDim.x];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t j = j0 + q * blockDim.x, slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
+      seg[f * N + slot] = v[q];
+    }
+  }
+  for (; j0 < nw5; j0 += blockDim.x) {
+    const uint32_t slot = j0 / kSparseSlotWords, f = j0 - slot * kSparseSlotWords;
+    seg[f * N + slot] = g[j0];
   }
   __syncthreads();
   auto insert = [&](uint32_t h, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {  // h: home slot
@@ -1070,18 +1098,31 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     }
     atomicAdd(s.dropped, (unsigned long long)c);
   };
-  // lpl lanes per list, each taking every lpl-th entry (two 16-byte loads per entry)
+  // lpl lanes per list, each taking every lpl-th entry (two 16-byte loads per entry); a
+  // lane loads 4 entries before inserting any, so the list reads are in flight together
+  // instead of one HBM round trip per entry
+  auto ins = [&](const ulonglong2 &a0, const ulonglong2 &a1) {
+    insert((uint32_t)(a1.y >> kWideHomeShift) & smask, a0.x, a0.y, a1.x,
+           (a1.y >> kWideCountShift) & ((1ULL << (kWideHomeShift - kWideCountShift)) - 1),
+           a1.y & ((1ULL << kWideCountShift) - 1));
+  };
   for (uint32_t l0 = 0; l0 < n_lists; l0 += lists_per_round) {
     const uint32_t l = l0 + threadIdx.x / lpl;
     if (l >= n_lists) continue;
     const uint32_t cnt = counts[(size_t)l * nwin + w];
     const ulonglong2 *e = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap * kWideEntryWords);
-    for (uint32_t k = sub; k < cnt; k += lpl) {
-      const ulonglong2 a0 = e[2 * k], a1 = e[2 * k + 1];
-      insert((uint32_t)(a1.y >> kWideHomeShift) & smask, a0.x, a0.y, a1.x,
-             (a1.y >> kWideCountShift) & ((1ULL << (kWideHomeShift - kWideCountShift)) - 1),
-             a1.y & ((1ULL << kWideCountShift) - 1));
+    uint32_t k = sub;
+    for (; k + 3 * lpl < cnt; k += 4 * lpl) {
+      ulonglong2 v[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] = e[2 * (k + q * lpl)];
+        v[2 * q + 1] = e[2 * (k + q * lpl) + 1];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ins(v[2 * q], v[2 * q + 1]);
     }
+    for (; k < cnt; k += lpl) ins(e[2 * k], e[2 * k + 1]);
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {
@@ -1627,8 +1668,7 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
                         a.ipl_pfx[2],  a.ipl_pfx[3], a.ipl_dr[0],  a.ipl_dr[1],  a.ipl_dr[2],  a.ipl_dr[3]};
   uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
   const uint32_t L4 = a.lds_bins;
-  for (uint32_t i = threadIdx.x; i < a.ipl_bytes / 16; i += blockDim.x)
-    ((uint4 *)smem)[i] = ((const uint4 *)a.ipl)[i];
+  fill_lds_u4((uint4 *)smem, (const uint4 *)a.ipl, a.ipl_bytes / 16);
   for (uint32_t i = threadIdx.x; i < L4 + 64; i += blockDim.x) bins[i] = 0u;
   for (uint32_t w = threadIdx.x; w < kMaxSpillWindows; w += blockDim.x)
     bins[L4 + 64 + w] = a.spill && w < a.nwin ? spill_ctr0(a, w) : 0u;
@@ -1978,9 +2018,7 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
   const uint32_t img_off = stage_words(nw, nh, sbc, sbh);
   const uint8_t *img = (const uint8_t *)(sm + img_off);
   for (uint32_t i = threadIdx.x; i < 2u * (nw + nh); i += blockDim.x) sm[i] = 0u;
-  if (kIp)
-    for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
-      ((uint4 *)(sm + img_off))[i] = ((const uint4 *)k.ipl)[i];
+  if (kIp) fill_lds_u4((uint4 *)(sm + img_off), (const uint4 *)k.ipl, k.ipl_bytes / 16);
   __syncthreads();
   const uint32_t D = kD ? (uint32_t)kD : k.depth;
   const uint32_t wmask = (1u << k.wlog2) - 1u, hi_bits = k.wlog2 - k.wshift, omask = (1u << k.wshift) - 1u;
@@ -2324,7 +2362,7 @@ __global__ __launch_bounds__(1024) void hll_fold_kernel(SketchK k) {
   const uint32_t npods = min(1u << k.hshift, k.hll_slots - pod0);
   const size_t bytes = (size_t)npods << k.p;  // multiple of 16 (p >= 4)
   uint4 *g = (uint4 *)((uint8_t *)k.hll + ((size_t)pod0 << k.p));
-  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) ((uint4 *)regs)[i] = g[i];
+  fill_lds_u4((uint4 *)regs, g, (uint32_t)(bytes / 16));
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
   const uint32_t imask = (1u << k.p) - 1u;
