@@ -1,0 +1,46 @@
+"""Rows of BASELINE.md's results table from bench lines (one JSON per config).
+
+    python scripts/baseline_table.py profiles/round3/f3b_bench_c1.json [...]
+"""
+
+import json
+import sys
+
+LABEL = {
+    "c1": "C1 (1M, local ip/ns/pod/workload keys)",
+    "c2": "C2 (100M, 10k pods, fwd + drop)",
+    "c3": "C3 (2^27 per GPU, + CMS d=4 w=2^20 + HLL p=14)",
+    "c4": "C4 (Zipf 1.2 5-tuples)",
+    "c4-remote": "C4 remote context (sparse keys)",
+    "c5": "C5 (10M, 100k pods, tcpflags + retrans + DNS)",
+}
+
+
+def rows(path):
+    d = json.load(open(path))
+    cfg = path.rsplit("_bench_", 1)[-1].replace(".json", "")
+    r = d["roofline"]
+    cpu = d.get("cpu_baseline") or {}
+    out = []
+    for mode, key in (("ref_cpu go-shaped", "go_shaped"), ("ref_cpu tuned", "tuned")):
+        m = cpu.get("modes", {}).get(key)
+        if m:
+            out.append("| %s | %s | %d | %.3g | — | — | pinned to oracle |" % (LABEL[cfg], mode, m["threads"], m["value"]))
+    traffic = ("; PMC %.1f B/rec" % (r["traffic"] / d["config"]["records_per_gpu"])) if r.get("traffic") else ""
+    out.append("| %s | HIP `%s` | 1 GPU | %.3g | %.0f kernel (%.3f ms) | %.1f %% kernel, %.1f %% step%s | bit-exact (tests) |" % (
+        LABEL[cfg], r["kernel"].split("<")[0] if "+" not in r["kernel"] else "sketch pass", d["value"],
+        r["achieved"], r["kernel_ms"], 100 * r["frac"],
+        100 * r["step_bytes_per_record"] * d["config"]["records_per_gpu"] / (d["ms_per_step"] * 1e-3) / 8e12,
+        traffic))
+    hf = d.get("host_fed")
+    if hf:
+        out.append("| %s | HIP, host-fed 2^20-record pinned batches (PCIe H2D incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
+            LABEL[cfg], hf["value"]))
+    return out
+
+
+if __name__ == "__main__":
+    print("| Config | Mode | Cores / GPUs | records/s | GB/s (alg.) | % of 8 TB/s | Parity |")
+    print("|---|---|---|---|---|---|---|")
+    for p in sys.argv[1:]:
+        print("\n".join(rows(p)))
