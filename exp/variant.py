@@ -15,8 +15,12 @@ sys.path.insert(0, ROOT)
 from retina_amd import build as B  # noqa: E402
 
 out, patches = sys.argv[1], sys.argv[2:]
-src = "/tmp/gpuagg_src_" + os.path.basename(out).replace(".so", "")
-shutil.rmtree(src, ignore_errors=True)
+# same depth as retina_amd/csrc so the sources' "../../include" resolves
+top = "/tmp/gpuagg_src_" + os.path.basename(out).replace(".so", "")
+src = top + "/pkg/csrc"
+shutil.rmtree(top, ignore_errors=True)
+os.makedirs(top)
+os.symlink(os.path.join(ROOT, "include"), top + "/include")
 shutil.copytree(B.CSRC, src, ignore=shutil.ignore_patterns("*.o", "*.so"))
 for p in patches:
     subprocess.run([sys.executable, p, src], check=True)

@@ -146,9 +146,16 @@ constexpr uint32_t kLdsBytes = 160 * 1024;
 // 256 windows x 2^13 bins: dense spaces up to ~2M bins beyond the LDS prefix (C5's
 // 100k-pod tcpflags + retransmit groups) still fold in LDS instead of global atomics
 constexpr uint32_t kMaxSpillWindows = 256;
-constexpr uint32_t kSpillRing = 128;
+constexpr uint32_t kSpillRing = 128;  // staged spill appends per window (dense_local_kernel kStage)
 constexpr uint32_t kHotKeyBytes = 48;    // LDS hot-key cache entry (aggregate_kernel)
-constexpr uint32_t kHotKeys = 2048;      // entries when the plan has HBM-table keys  // staged spill appends per window (dense_local_kernel kStage)
+constexpr uint32_t kHotKeys = 2048;      // entries when the plan has HBM-table keys
+// wide_kernel (remote context) takes the LDS image of every pod IP when it fits next to a
+// hot-key cache of >= kWideIplMinHot entries and a 2^kWideIplMinDoor-bit doorkeeper.  C4
+// remote, 100M records: 2048 entries + image + 2^15-bit doorkeeper 1.14 ms, 1024 entries
+// + image + 2^17 bits 1.34 ms, no image (2048 + 2^18 bits) 1.32 ms
+// (profiles/round3/exp/v3_wide_ipl.jsonl)
+constexpr uint32_t kWideIplMinHot = 2048;
+constexpr uint32_t kWideIplMinDoor = 13;
 constexpr uint32_t kLdsExtraWords = 64 + kMaxSpillWindows / 2;  // 64 dummies + u32 spill-window counters
 constexpr uint32_t kLdsMaxBins = kLdsBytes / 8 - kLdsExtraWords;
 constexpr uint32_t kLdsCountShift = 44;

@@ -694,15 +694,90 @@ __device__ __forceinline__ void fill_lds_u4(uint4 *dst, const uint4 *src, uint32
   for (; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+// Probe of the LDS cuckoo image: two 8-byte bucket reads and 4 compares give the index
+// of the matching key (or ~0u); the u16 slot id is read separately so all key reads of
+// a thread's records can be in flight together.
+__device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32_t nb, uint32_t seed,
+                                                    uint32_t ip) {
+  uint32_t b1, b2;
+  ipl_buckets(ip, seed, nb, b1, b2);
+  const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
+  uint32_t j = nb * 2;  // sentinel entry: kIplNoSlot
+  j = k1.x == ip ? b1 * 2 : j;
+  j = k1.y == ip ? b1 * 2 + 1 : j;
+  j = k2.x == ip ? b2 * 2 : j;
+  j = k2.y == ip ? b2 * 2 + 1 : j;
+  return j;
+}
+
+// slot id, or kIplNoSlot (not a pod, or the apiserver pseudo pod)
+__device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
+
+// One IP through the tier-1 LDS image: slot or kIplNoSlot (inactive lanes: kIplNoSlot).
+// kRadix: the radix image (two dependent u16 reads); else the cuckoo image.
+template <int kIp>
+struct IplView {
+  const uint8_t *smem;
+  uint32_t nb, seed, npfx, p0, p1, p2, p3;
+  uint32_t d0, d1, d2, d3;  // kIp 2: the dense radix descriptors
+  __device__ __forceinline__ uint32_t lookup(uint32_t ip) const {
+    if (kIp == 2)
+      return ((const uint16_t *)smem)[(iprd_block(ip, p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip >> 24)];
+    if (kIp == 1) {
+      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
+      return blk[((uint32_t)bidx[ipr_row(ip, p0, p1, p2, p3, npfx)] << 8) | (ip >> 24)];
+    }
+    return ipl_slot((const uint16_t *)(smem + ipl_vals_offset(nb)), ipl_probe_index((const uint32_t *)smem, nb, seed, ip));
+  }
+  // the 8 IPs of a step, every read of a level issued before the next level; lookups run
+  // for every lane (inactive lanes hold a clamped real record) and the result is masked
+  // after: a select on the index made the compiler branch per IP
+  __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
+    if (kIp == 2) {  // one LDS read per IP
+      const uint16_t *blk = (const uint16_t *)smem;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = blk[(iprd_block(ip[k], p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip[k] >> 24)];
+    } else if (kIp == 1) {
+      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
+      uint32_t bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bi[k] = bidx[ipr_row(ip[k], p0, p1, p2, p3, npfx)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = blk[(bi[k] << 8) | (ip[k] >> 24)];
+    } else {
+      const uint32_t *keys = (const uint32_t *)smem;
+      const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
+      uint32_t j[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
+  }
+};
+
+// IP lookups of for_each_record: the HBM table, or an LDS image of every pod IP (LdsIp:
+// the slot only -- the remote context never reads the apiserver flag)
+struct HbmIp {
+  static constexpr bool kLds = false;
+};
+template <int kIp>
+struct LdsIp {
+  static constexpr bool kLds = true;
+  IplView<kIp> iv;
+};
+
 struct NoRounds {
   __device__ __forceinline__ void operator()() const {}
 };
 // kRounds: the vector loop is block-uniform (waves past the end process inactive lanes)
 // and calls round_end() after every step, so the caller can flush LDS staging between
 // barriers.
-template <bool kVec, bool kRounds = false, class F, class RE = NoRounds>
+template <bool kVec, bool kRounds = false, class F, class RE = NoRounds, class IP = HbmIp>
 __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports, bool need_dns, F &&f,
-                                                RE &&round_end = RE{}) {
+                                                RE &&round_end = RE{}, const IP &ipv = IP{}) {
   const bool need_bytes = a.p.need_bytes;  // no forward / drop group: the column is not read
   const uint64_t start = (uint64_t)blockIdx.x * a.chunk;
   const uint64_t end = start + a.chunk < a.n ? start + a.chunk : a.n;
@@ -724,7 +799,12 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
       const uint4 vq = need_dns ? rec_ld(&q4[v]) : make_uint4(0, 0, 0, 0);
       const uint32_t ip[8] = {vs.x, vs.y, vs.z, vs.w, vd.x, vd.y, vd.z, vd.w};
       Lk lk[8];
-      if (a.t.pre) {  // radix table: 8 prefix loads, then 8 entry loads
+      if constexpr (IP::kLds) {  // 8 LDS image reads
+        uint32_t sl[8];
+        ipv.iv.lookup8(ip, true, sl);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lk[k] = sl[k] == kIplNoSlot ? none : Lk{(int32_t)sl[k], 0u};
+      } else if (a.t.pre) {  // radix table: 8 prefix loads, then 8 entry loads
         uint32_t bi[8], e[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) bi[k] = radix_block(a.t, ip[k]);
@@ -764,12 +844,20 @@ __device__ __forceinline__ void for_each_record(const KArgs &a, bool need_ports,
     }
     tail = start + ((end - start) & ~3ULL);
   }
+  auto lk1 = [&](uint32_t ip) -> Lk {
+    if constexpr (IP::kLds) {
+      const uint32_t v = ipv.iv.lookup(ip);
+      return v == kIplNoSlot ? none : Lk{(int32_t)v, 0u};
+    } else {
+      return ip_lookup(a.t, ip);
+    }
+  };
   for (uint64_t i0 = tail + wave0; i0 < end; i0 += blockDim.x) {
     const bool act = i0 + lane < end;
     const uint64_t i = act ? i0 + lane : end - 1;
     const uint32_t sip = a.c.src[i], dip = a.c.dst[i];
     f(sip, dip, need_bytes ? a.c.bytes[i] : 0u, act ? a.c.meta[i] : kInactiveMeta, need_ports ? a.c.ports[i] : 0u,
-      need_dns ? a.c.dns[i] : 0u, act ? ip_lookup(a.t, sip) : none, act ? ip_lookup(a.t, dip) : none, act);
+      need_dns ? a.c.dns[i] : 0u, act ? lk1(sip) : none, act ? lk1(dip) : none, act);
   }
 }
 
@@ -872,16 +960,19 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
 // mutually exclusive) a record takes exactly one key build and one insert, whichever
 // group it matches.  Insert: key hash once, doorkeeper, LDS hot-key cache, else the
 // key's segment list (wide_insert).
-template <int NG, bool kRemote, bool kExcl>
+template <int NG, bool kRemote, bool kExcl, int kIp>
 __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
-  // LDS: segment-list fill counters, hot-key cache (8-byte aligned), doorkeeper bitmap
-  uint32_t *sctr = (uint32_t *)lds;
+  // LDS: (kIp >= 0) the image of every pod IP, segment-list fill counters, hot-key cache
+  // (8-byte aligned), doorkeeper bitmap
+  const uint32_t img_words = kIp >= 0 ? a.ipl_bytes / 8 : 0u;
+  if (kIp >= 0) fill_lds_u4((uint4 *)lds, (const uint4 *)a.ipl, a.ipl_bytes / 16);
+  uint32_t *sctr = (uint32_t *)(lds + img_words);
   for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
     const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
     sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
   }
-  HotKey *hot = (HotKey *)&lds[(a.sp_nwin + 1) / 2];
+  HotKey *hot = (HotKey *)&lds[img_words + (a.sp_nwin + 1) / 2];
   for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
   uint32_t *door = (uint32_t *)(hot + a.hot_n);
   const uint32_t door_words = a.door_log2 ? 1u << (a.door_log2 - 5) : 0u;
@@ -902,9 +993,8 @@ __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
     sop[g] = a.p.g[g].src_opts;
     dop[g] = a.p.g[g].dst_opts;
   }
-  for_each_record<true>(a, a.p.need_ports, a.p.need_dns,
-                        [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports, uint32_t dns,
-                            const Lk &ls, const Lk &ld, bool act) {
+  auto body = [&](uint32_t sip, uint32_t dip, uint32_t nb, uint32_t meta, uint32_t ports, uint32_t dns,
+                  const Lk &ls, const Lk &ld, bool act) {
     const uint32_t proto = meta_proto(meta), verdict = meta_verdict(meta);
     const uint32_t tdir = meta_tdir(meta), reason = meta_reason(meta), dnstype = meta_dnstype(meta);
     const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16;
@@ -958,7 +1048,14 @@ __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
       for (int g = 0; g < NG; ++g)
         update((uint32_t)g, fam[g], sop[g], dop[g], act && family_matches(fam[g], verdict, proto, dnstype, 0u));
     }
-  });
+  };
+  if constexpr (kIp >= 0) {
+    const LdsIp<kIp> ipv{{(const uint8_t *)lds, a.ipl_nb, a.ipl_seed, a.ipl_npfx, a.ipl_pfx[0], a.ipl_pfx[1],
+                          a.ipl_pfx[2], a.ipl_pfx[3], a.ipl_dr[0], a.ipl_dr[1], a.ipl_dr[2], a.ipl_dr[3]}};
+    for_each_record<true>(a, a.p.need_ports, a.p.need_dns, body, NoRounds{}, ipv);
+  } else {
+    for_each_record<true>(a, a.p.need_ports, a.p.need_dns, body);
+  }
   __syncthreads();
   {  // the cached keys, once per workgroup: into the segment lists with their counts
     DevSparse g = s;
@@ -1354,25 +1451,6 @@ __global__ __launch_bounds__(1024) void dense_local_kernel(KArgs a) {
 }
 
 // ---- tier-1: IP table and 32-bit bins both in LDS -------------------------------------
-// Probe of the LDS cuckoo image: two 8-byte bucket reads and 4 compares give the index
-// of the matching key (or ~0u); the u16 slot id is read separately so all key reads of
-// a thread's records can be in flight together.
-__device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32_t nb, uint32_t seed,
-                                                    uint32_t ip) {
-  uint32_t b1, b2;
-  ipl_buckets(ip, seed, nb, b1, b2);
-  const uint2 k1 = *(const uint2 *)&keys[b1 * 2], k2 = *(const uint2 *)&keys[b2 * 2];
-  uint32_t j = nb * 2;  // sentinel entry: kIplNoSlot
-  j = k1.x == ip ? b1 * 2 : j;
-  j = k1.y == ip ? b1 * 2 + 1 : j;
-  j = k2.x == ip ? b2 * 2 : j;
-  j = k2.y == ip ? b2 * 2 + 1 : j;
-  return j;
-}
-
-// slot id, or kIplNoSlot (not a pod, or the apiserver pseudo pod)
-__device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
-
 struct L4Ctx {
   uint32_t *bins;  // [L4] u32 bins, then 64 dummies, then the spill-window counters
   uint32_t dummy;  // this lane's dummy word: absorbs predicated-off updates
@@ -1615,51 +1693,6 @@ __device__ __forceinline__ void l4_records(const DenseGroups<NG, SIG> &G, const 
     }
   }
 }
-
-// One IP through the tier-1 LDS image: slot or kIplNoSlot (inactive lanes: kIplNoSlot).
-// kRadix: the radix image (two dependent u16 reads); else the cuckoo image.
-template <int kIp>
-struct IplView {
-  const uint8_t *smem;
-  uint32_t nb, seed, npfx, p0, p1, p2, p3;
-  uint32_t d0, d1, d2, d3;  // kIp 2: the dense radix descriptors
-  __device__ __forceinline__ uint32_t lookup(uint32_t ip) const {
-    if (kIp == 2)
-      return ((const uint16_t *)smem)[(iprd_block(ip, p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip >> 24)];
-    if (kIp == 1) {
-      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
-      return blk[((uint32_t)bidx[ipr_row(ip, p0, p1, p2, p3, npfx)] << 8) | (ip >> 24)];
-    }
-    return ipl_slot((const uint16_t *)(smem + ipl_vals_offset(nb)), ipl_probe_index((const uint32_t *)smem, nb, seed, ip));
-  }
-  // the 8 IPs of a step, every read of a level issued before the next level; lookups run
-  // for every lane (inactive lanes hold a clamped real record) and the result is masked
-  // after: a select on the index made the compiler branch per IP
-  __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
-    if (kIp == 2) {  // one LDS read per IP
-      const uint16_t *blk = (const uint16_t *)smem;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = blk[(iprd_block(ip[k], p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip[k] >> 24)];
-    } else if (kIp == 1) {
-      const uint16_t *bidx = (const uint16_t *)smem, *blk = (const uint16_t *)(smem + ipr_blk_offset(npfx));
-      uint32_t bi[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) bi[k] = bidx[ipr_row(ip[k], p0, p1, p2, p3, npfx)];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = blk[(bi[k] << 8) | (ip[k] >> 24)];
-    } else {
-      const uint32_t *keys = (const uint32_t *)smem;
-      const uint16_t *vals = (const uint16_t *)(smem + ipl_vals_offset(nb));
-      uint32_t j[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) j[k] = ipl_probe_index(keys, nb, seed, ip[k]);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = ipl_slot(vals, j[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sl[k] = act ? sl[k] : kIplNoSlot;
-  }
-};
 
 template <int NG, bool kVec, uint32_t SIG, int kIp>
 __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
@@ -3014,8 +3047,22 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     for (int h = 0; h < g; ++h) excl &= a.plan.g[h].family != a.plan.g[g].family;
   }
   if (wide) {
-    // LDS: counters, cache, then the largest doorkeeper bitmap that fits
-    size_t lw = (size_t)((k.sp_nwin + 1) / 2) * 8 + (size_t)a.hot_n * kHotKeyBytes;
+    const bool remote = !a.plan.local, four = a.plan.ngroups > 2;
+    // LDS: (remote context) the image of every pod IP when it fits next to a cache of
+    // >= kWideIplMinHot entries and a 2^kWideIplMinDoor-bit doorkeeper (the cache halves
+    // until it does), counters, cache, then the largest doorkeeper bitmap that fits
+    const size_t ctr = (size_t)((k.sp_nwin + 1) / 2) * 8, img = remote && a.ipl ? ((size_t)a.ipl_bytes + 15) & ~15ull : 0;
+    int kip = -1;
+    if (img) {
+      uint32_t hn = k.hot_n;
+      while (hn > kWideIplMinHot && img + ctr + (size_t)hn * kHotKeyBytes + ((size_t)1 << (kWideIplMinDoor - 3)) > kLdsBytes)
+        hn >>= 1;
+      if (img + ctr + (size_t)hn * kHotKeyBytes + ((size_t)1 << (kWideIplMinDoor - 3)) <= kLdsBytes) {
+        kip = a.ipl_dense ? 2 : a.ipl_radix ? 1 : 0;
+        k.hot_n = hn;
+      }
+    }
+    size_t lw = (kip >= 0 ? img : 0) + ctr + (size_t)k.hot_n * kHotKeyBytes;
     k.door_log2 = 0;
     for (uint32_t l = 18; l >= 13; --l)
       if (lw + ((size_t)1 << (l - 3)) <= kLdsBytes) {
@@ -3023,21 +3070,28 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
         lw += (size_t)1 << (l - 3);
         break;
       }
-    const bool remote = !a.plan.local, four = a.plan.ngroups > 2;
     if (kernel) {
       static thread_local char wname[64];
-      snprintf(wname, sizeof wname, "wide_kernel<%d, %s, %s>", four ? 4 : 2, remote ? "true" : "false",
-               excl ? "true" : "false");
+      snprintf(wname, sizeof wname, "wide_kernel<%d, %s, %s, %d>", four ? 4 : 2, remote ? "true" : "false",
+               excl ? "true" : "false", kip);
       *kernel = wname;
     }
-#define GA_WIDE(NG, R, X) e = launch_k(wide_kernel<NG, R, X>, k, B, T, lw, st)
+#define GA_WIDE(NG, R, X, I) e = launch_k(wide_kernel<NG, R, X, I>, k, B, T, lw, st)
+#define GA_WIDE_IP(NG, X)                \
+  switch (kip) {                          \
+    case 2: GA_WIDE(NG, true, X, 2); break; \
+    case 1: GA_WIDE(NG, true, X, 1); break; \
+    case 0: GA_WIDE(NG, true, X, 0); break; \
+    default: GA_WIDE(NG, true, X, -1);     \
+  }
     if (four) {
-      if (remote) { if (excl) GA_WIDE(4, true, true); else GA_WIDE(4, true, false); }
-      else { if (excl) GA_WIDE(4, false, true); else GA_WIDE(4, false, false); }
+      if (remote) { if (excl) { GA_WIDE_IP(4, true) } else { GA_WIDE_IP(4, false) } }
+      else { if (excl) GA_WIDE(4, false, true, -1); else GA_WIDE(4, false, false, -1); }
     } else {
-      if (remote) { if (excl) GA_WIDE(2, true, true); else GA_WIDE(2, true, false); }
-      else { if (excl) GA_WIDE(2, false, true); else GA_WIDE(2, false, false); }
+      if (remote) { if (excl) { GA_WIDE_IP(2, true) } else { GA_WIDE_IP(2, false) } }
+      else { if (excl) GA_WIDE(2, false, true, -1); else GA_WIDE(2, false, false, -1); }
     }
+#undef GA_WIDE_IP
 #undef GA_WIDE
     if (e != hipSuccess) return e;
     if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;

@@ -306,6 +306,7 @@ struct gpuagg_ctx {
     uint64_t rpb = 0;       // records per workgroup appended so far
   } pend;
   bool defer_folds = true;
+  uint64_t wide_list_bytes = 0;  // wide-key list budget (gpuagg_create)
   std::vector<std::array<hipEvent_t, 2>> pending_fold;  // deferred fold start, end
   int32_t *d_enrich = nullptr;  // gpuagg_submit_enrich: [2][cap] endpoint slots
   size_t enrich_alloc = 0;
@@ -997,7 +998,11 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 // Launches whose list folds may wait for one fold_pending (see Pending).
 constexpr uint64_t kDeferLaunches = 16;
 // Device memory for the wide-key segment lists of one ctx (32-byte entries).
-constexpr uint64_t kWideListBytes = 8ull << 30;
+// Wide-key lists per context: 32 GiB (1024 entries per workgroup and segment at 2^24
+// slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
+// atomics, and under C4's skew 8 GiB (256 entries) overflowed within one launch: 1.74 ->
+// 1.32 ms per 100M records (profiles/round3/exp/v2_wide_list_bytes.jsonl).
+constexpr uint64_t kWideListBytes = 32ull << 30;
 
 int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc = 0;
@@ -1137,6 +1142,21 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       }
     }
   }
+  // remote context on the wide-key path: the LDS image of every pod IP (wide_kernel takes
+  // it when it fits next to the hot-key cache; the context never reads the apiserver flag)
+  if (hot && c->remote && !a.tier1 && c->ipl_all_bytes) {
+    a.ipl = c->d_ipl_all;
+    a.ipl_nb = c->ipl_all_nb;
+    a.ipl_seed = c->ipl_all_seed;
+    a.ipl_bytes = c->ipl_all_bytes;
+    a.ipl_radix = c->ipl_all_radix;
+    a.ipl_dense = c->ipl_all_dense;
+    a.ipl_npfx = c->ipl_all_npfx;
+    for (uint32_t j = 0; j < kIprMaxPfx; ++j) {
+      a.ipl_pfx[j] = c->ipl_all_pfx[j];
+      a.ipl_dr[j] = c->ipl_all_dr[j];
+    }
+  }
   // one 1024-thread workgroup per CU whenever LDS holds bins or spill counters: with
   // dense bins but no LDS prefix (C5: 100k-pod groups) 4x fewer workgroups mean 4x
   // fewer, longer spill lists for the fold (same 16 waves per CU)
@@ -1206,8 +1226,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         const uint64_t mean = budget / sp_nwin;
         g.sp_nwin = (uint32_t)sp_nwin;
         uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
-        if (!c->sv.compact)  // 32-byte entries: kWideListBytes of lists per ctx
-          cap = std::max<uint64_t>(16, kWideListBytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin)) &
+        if (!c->sv.compact)  // 32-byte entries: wide_list_bytes of lists per ctx
+          cap = std::max<uint64_t>(16, c->wide_list_bytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin)) &
                 ~1ULL;
         g.sp_cap = (uint32_t)cap;
       }
@@ -1438,6 +1458,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
     return GPUAGG_EDEVICE;
   }
   c->n_cu = (uint32_t)prop.multiProcessorCount;
+  c->wide_list_bytes = std::min<uint64_t>(kWideListBytes, (uint64_t)prop.totalGlobalMem / 8);
   c->defer_folds = !(cfg->flags & GPUAGG_FLAG_FOLD_PER_BATCH);
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
@@ -1981,9 +2002,9 @@ int gpuagg_set_endpoints(gpuagg_ctx *c, const uint32_t *ipv4, const int32_t *slo
     }
   }
   // LDS image of every pod IP (the apiserver pseudo pod included: it is a source pod for
-  // the HLL) for the sketch pass
+  // the HLL) for the sketch pass and the remote context's wide_kernel
   c->ipl_all_bytes = 0;
-  if (c->cfg.hll_precision && !(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
+  if ((c->cfg.hll_precision || c->remote) && !(c->cfg.flags & GPUAGG_FLAG_NO_LDS_IP_TABLE)) {
     std::vector<std::pair<uint32_t, uint32_t>> ents;
     for (const auto &kv : last) ents.emplace_back(kv.first, (uint32_t)((kv.second >> 32) & ((1u << kSlotBits) - 1)));
     LdsImage im;
