@@ -1250,17 +1250,20 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     // Deferred folds: while the geometry holds, launches keep appending to the same lists
     // (their counters start from the stored fill) for up to kDeferLaunches (16) launches' worth
     // of records per workgroup, and fold_pending folds them once.
-    // Only plans with compact-key lists defer: their fold pays a fixed pass over the
-    // group-by table.  Spill-only plans (C2, C4) fold per batch -- their fold is
-    // proportional to the entries, and appending past earlier launches' entries measured
-    // ~2 % slower in the tier-1 kernel (profiles/round2/r4f_*).
-    const bool lists = sp_lists;
+    // Plans with compact-key lists always defer: their fold pays a fixed pass over the
+    // group-by table.  Spill-only plans (C2, C4) defer only small launches (at most
+    // kMaxRecordsPerBlock / kDeferLaunches records per workgroup, e.g. the Go plugin's 2^20
+    // records): there the spill fold's fixed pass over the windows cost more than the
+    // tier-1 kernel itself; at full-size launches appending past earlier launches' entries
+    // measured ~2 % slower in the tier-1 kernel (profiles/round2/r4f_*), so they fold per batch.
+    const bool small_spill = c->dense_len > a.lds_bins && a.chunk * kDeferLaunches <= kMaxRecordsPerBlock;
+    const bool lists = sp_lists || small_spill;
     const bool defer = c->defer_folds && lists;
     // Wide lists (192-bit keys) are folded when the device says so: every launch's fold
     // skips itself until some list is half full (sparse_fold_wide_kernel), so the host keeps
     // appending without a record budget -- under skew the LDS hot-key cache absorbs most
     // updates and a budget that assumes one entry per record folded ~5x too often.
-    const bool fold_cond = defer && !c->sv.compact;
+    const bool fold_cond = defer && sp_lists && !c->sv.compact;
     uint64_t budget = defer ? std::max<uint64_t>(a.chunk, std::min<uint64_t>(kMaxRecordsPerBlock,
                                                                              kDeferLaunches * a.chunk))
                             : a.chunk;
