@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define GPUAGG_ABI_VERSION 2u  /* 2: columns tcp_id/time_ns, stats, state latency words */
+#define GPUAGG_ABI_VERSION 3u  /* 2: columns tcp_id/time_ns, stats, state latency words;
+                                   3: gpuagg_config.wide_list_mib, latency_limit */
 
 /* error codes */
 #define GPUAGG_OK 0
@@ -62,6 +63,12 @@ typedef struct gpuagg_config {
   uint32_t cms_width_log2;       /* count-min columns = 2^this                       */
   uint32_t hll_precision;        /* HyperLogLog p (registers 2^p per source pod; 0=off) */
   uint32_t flags;                /* GPUAGG_FLAG_* (0 = defaults)                     */
+  uint32_t wide_list_mib;        /* device memory for the 192-bit-key segment lists of
+                                    this ctx, MiB (0: min(32 GiB, device memory / 8));
+                                    a full list falls back to exact memory-side atomics */
+  uint32_t latency_limit;        /* node-apiserver latency: live pending requests kept,
+                                    ttlcache.WithCapacity (latency.go:35,120-121);
+                                    0 = the reference's LIMIT, 100000                 */
 } gpuagg_config;
 
 /* gpuagg_config.flags */

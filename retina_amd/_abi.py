@@ -13,7 +13,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPUAGG_LIB") or os.path.join(HERE, "libgpuagg.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, EINVAL, ENOMEM, EDEVICE, ECAPACITY, ESTATE, EDUPLICATE, ERANGE, ENOTFOUND = 0, -1, -2, -3, -4, -5, -6, -7, -8
 ERR_NAMES = {EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE", ECAPACITY: "ECAPACITY",
              ESTATE: "ESTATE", EDUPLICATE: "EDUPLICATE", ERANGE: "ERANGE", ENOTFOUND: "ENOTFOUND"}
@@ -27,7 +27,7 @@ class Config(C.Structure):
                 ("max_slots", C.c_uint32), ("max_ips", C.c_uint32),
                 ("sparse_capacity_log2", C.c_uint32), ("cms_depth", C.c_uint32),
                 ("cms_width_log2", C.c_uint32), ("hll_precision", C.c_uint32),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("wide_list_mib", C.c_uint32), ("latency_limit", C.c_uint32)]
 FLAG_NO_LDS_IP_TABLE = 1
 FLAG_FOLD_PER_BATCH = 8  # diagnostics: fold the lists after every batch
 FLAG_NO_HOT_KEYS = 16  # diagnostics: no LDS hot-key cache in front of the group-by table

@@ -997,8 +997,8 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 
 // Launches whose list folds may wait for one fold_pending (see Pending).
 constexpr uint64_t kDeferLaunches = 16;
-// Device memory for the wide-key segment lists of one ctx (32-byte entries).
-// Wide-key lists per context: 32 GiB (1024 entries per workgroup and segment at 2^24
+// Default device memory for the wide-key segment lists of one ctx (32-byte entries;
+// gpuagg_config.wide_list_mib overrides it): 32 GiB (1024 entries per workgroup and segment at 2^24
 // slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
 // atomics, and under C4's skew 8 GiB (256 entries) overflowed within one launch: 1.74 ->
 // 1.32 ms per 100M records (profiles/round3/exp/v2_wide_list_bytes.jsonl).
@@ -1461,7 +1461,8 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
     return GPUAGG_EDEVICE;
   }
   c->n_cu = (uint32_t)prop.multiProcessorCount;
-  c->wide_list_bytes = std::min<uint64_t>(kWideListBytes, (uint64_t)prop.totalGlobalMem / 8);
+  c->wide_list_bytes = cfg->wide_list_mib ? (uint64_t)cfg->wide_list_mib << 20
+                                          : std::min<uint64_t>(kWideListBytes, (uint64_t)prop.totalGlobalMem / 8);
   c->defer_folds = !(cfg->flags & GPUAGG_FLAG_FOLD_PER_BATCH);
   if (cfg->cms_depth) {
     c->cms_len = (size_t)cfg->cms_depth << cfg->cms_width_log2;
@@ -2167,13 +2168,15 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
     uint32_t *d = nullptr;
     if ((rc = dev_alloc(c, &d, dead_dev.size()))) return rc;
     hipError_t e = x_copy_async(c, d, dead_dev.data(), dead_dev.size() * 4, hipMemcpyHostToDevice, c->stream);
-    if (c->cpu)
-      cpu::zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
-                      c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan);
-    else if (e == hipSuccess)
+    if (c->cpu) {
+      if (e == hipSuccess)
+        cpu::zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
+                        c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan);
+    } else if (e == hipSuccess) {
       ENQ(c);
       e = launch_zero_slots(c->dense_len ? c->d_dense_cnt : nullptr, c->d_dense_byt, c->hll_len ? c->d_hll : nullptr,
                             c->cfg.hll_precision, d, (uint32_t)dead_dev.size(), c->plan, c->stream);
+    }
     if (e == hipSuccess) e = x_sync(c, c->stream);
     dev_free(c, d);
     if (e != hipSuccess) return fail(c, GPUAGG_EDEVICE, "retire: %s", hipGetErrorString(e));

@@ -85,11 +85,12 @@ class GpuAgg:
 
     def __init__(self, device: int = 0, remote_context: bool = False, max_slots: int = 1 << 14,
                  max_ips: int = 1 << 16, sparse_capacity_log2: int = 22, cms_depth: int = 0,
-                 cms_width_log2: int = 20, hll_precision: int = 0, flags: int = 0):
+                 cms_width_log2: int = 20, hll_precision: int = 0, flags: int = 0,
+                 wide_list_mib: int = 0, latency_limit: int = 0):
         self.lib = _abi.load()
         cfg = _abi.Config(_abi.ABI_VERSION, device, 1 if remote_context else 0, max_slots, max_ips,
                           sparse_capacity_log2, cms_depth, cms_width_log2 if cms_depth else 0,
-                          hll_precision, flags)
+                          hll_precision, flags, wide_list_mib, latency_limit)
         h = C.c_void_p()
         rc = self.lib.gpuagg_create(C.byref(cfg), C.byref(h))
         if rc != _abi.OK:

@@ -61,7 +61,7 @@ kat = {
                     ip={"source": "10.0.0.1", "destination": ""}),
          "values": ["", "unknown", "unknown"]},
     ],
-    # pkg/module/metrics/dns_test.go:165-234 (TestGetLabels)
+    # pkg/module/metrics/dns_test.go:24-93 (TestGetLabels)
     "dns_labels": [
         {"name": "basic context request labels", "local_opts": None, "kind": "request",
          "want": ["query_type", "query"]},
@@ -73,7 +73,7 @@ kat = {
          "want": ["query_type", "query", "ip", "namespace", "podname", "workload_kind",
                   "workload_name", "service", "port"]},
     ],
-    # pkg/module/metrics/dns_test.go:236-335 (TestValues); flows built with AddDNSInfo
+    # pkg/module/metrics/dns_test.go:95-194 (TestValues); flows built with AddDNSInfo
     # (qtype, rcode 0, "bing.com", ["A"], num_answers, ips)
     "dns_values": [
         {"name": "basic context", "metric_name": "", "input": None, "call": "response", "want": None},
@@ -90,7 +90,7 @@ kat = {
         {"name": "Response/RequestMetric", "metric_name": "dns_request_count",
          "input": ["R", 1, ["1.1.1.1"]], "call": "response", "want": None},
     ],
-    # pkg/module/metrics/dns_test.go:337-456 (TestProcessLocalCtx): getLocalCtxValues mocked
+    # pkg/module/metrics/dns_test.go:196-315 (TestProcessLocalCtx): getLocalCtxValues mocked
     "dns_local_ctx": [
         {"name": "No context labels", "tdir": None, "local_values": None, "want": None},
         {"name": "Only ingress labels", "tdir": 0,

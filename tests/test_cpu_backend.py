@@ -116,6 +116,42 @@ def test_latency_matches_oracle():
     assert want["latency_count"] > 0 and want["no_response"] > 0
 
 
+def test_retire_slots_pod_churn():
+    """Pod churn past max_slots on the CPU backend (the retirement must
+    zero the dead slots' bins on the host and never reach a device launch): three
+    generations of 100 pods in 128 slots; each retirement frees exactly the old
+    generation, its series vanish and the slots are reused."""
+    from .test_gpu_lifecycle import FWD_DROP, _oracle
+    from .helpers import oracle_cache
+    g, prev = None, None
+    try:
+        for gen in range(3):
+            pods = W.make_pods(100, seed=50 + gen, apiserver=False)
+            pods.endpoints[:] = [W.Endpoint("gen%d" % gen, e.name, e.ips, e.owner_refs) for e in pods.endpoints]
+            if g is None:
+                g = make_engine(pods, FWD_DROP, False, flags=CPU, max_slots=128, max_ips=512, hll_precision=8)
+            else:
+                for e in prev.endpoints:
+                    g.cache_delete_endpoint(e.namespace, e.name)
+                g.cache_commit(version=2 * gen)
+                assert g.retire_slots() == 100
+                assert g.snapshot() == {}  # every counter of the dead generation cleared
+                assert not g.hll_array().any()
+                assert g.retire_slots() == 0
+                g.load_endpoints(pods.endpoints, version=2 * gen + 1)
+            recs = W.gen_records(20_000, pods, seed=60 + gen)
+            g.submit_numpy(recs)
+            got = g.snapshot()
+            want = _oracle(recs, oracle_cache(pods), FWD_DROP)
+            assert got == want, diff_series(got, want)
+            assert {dict(k[1])["namespace"] for k in got} == {"gen%d" % gen}
+            assert g.stats()["records"] == 20_000 * (gen + 1)
+            prev = pods
+    finally:
+        if g is not None:
+            g.close()
+
+
 def test_merge_and_enrich():
     """Two CPU contexts fed the direction-free shards and merged equal one context;
     enriched-flow slots equal the IP cache's pods."""
