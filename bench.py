@@ -226,6 +226,46 @@ def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, 
                     "- the same records at the full-size launch's rate" % n}
 
 
+# Prometheus' default scrape interval: the engine's snapshot + text rendering is a host cost
+# paid once per scrape epoch (prometheusexporter.go:19,29-31 serve the registry per scrape).
+SCRAPE_EPOCH_S = 15.0
+
+
+def scrape_cost(g, reps: int = 3):
+    """Host-side cost of one scrape on the state the timed region left: gpuagg_snapshot
+    (device sync, table compaction and D2H, label rendering of every series) and
+    gpuagg_result_render_text (client_golang's text exposition), median of `reps`.  The
+    walk a Go publish does over the result is not included (it is the caller's)."""
+    snap, rend, nser, nbytes = [], [], 0, 0
+    for _ in range(reps):
+        r = C.c_void_p()
+        t0 = time.perf_counter()
+        rc = g.lib.gpuagg_snapshot(g.h, C.byref(r))
+        t1 = time.perf_counter()
+        if rc != 0:
+            raise RuntimeError("gpuagg_snapshot: %d" % rc)
+        try:
+            nser = int(g.lib.gpuagg_result_count(r))
+            ln = C.c_size_t()
+            t2 = time.perf_counter()
+            g.lib.gpuagg_result_render_text(r, None, 0, C.byref(ln))
+            buf = C.create_string_buffer(ln.value + 1)
+            rc = g.lib.gpuagg_result_render_text(r, buf, ln.value + 1, C.byref(ln))
+            t3 = time.perf_counter()
+            if rc != 0:
+                raise RuntimeError("gpuagg_result_render_text: %d" % rc)
+            nbytes = int(ln.value)
+        finally:
+            g.lib.gpuagg_result_free(r)
+        snap.append((t1 - t0) * 1e3)
+        rend.append((t3 - t2) * 1e3)
+    sm, rm = float(np.median(snap)), float(np.median(rend))
+    return {"series": nser, "text_bytes": nbytes, "snapshot_ms": sm, "render_ms": rm,
+            "epoch_frac": (sm + rm) / (SCRAPE_EPOCH_S * 1e3), "epoch_s": SCRAPE_EPOCH_S,
+            "note": "gpuagg_snapshot + gpuagg_result_render_text on the timed region's state, median of %d; "
+                    "host cost per scrape epoch, outside `value`" % reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +277,7 @@ def main():
                     help="records in the tuned CPU baseline sample (go-shaped: 1/8 of it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
+    ap.add_argument("--no-scrape", action="store_true", help="skip the snapshot / render timing")
     ap.add_argument("--no-production", action="store_true",
                     help="skip the Go-batch-size (1M-record) device-resident launches")
     args = ap.parse_args()
@@ -362,6 +403,8 @@ def main():
         },
         "build_id": build_id,
     }
+    if rank == 0 and not args.no_scrape:
+        result["scrape"] = scrape_cost(g)
     if rank == 0 and world == 1 and not args.no_production and n > GO_BATCH:
         result["production"] = production_geometry(g, cols, n, bpr, stats["kernel_ms"] / max(1, stats["kernel_launches"]))
     if rank == 0 and world == 1 and not args.no_host_fed:

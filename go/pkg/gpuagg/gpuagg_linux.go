@@ -58,6 +58,7 @@ import (
 const (
 	name          = "gpuagg"
 	batchCapacity = 1 << 20
+	rawPiece      = 1 << 16 // raw samples buffered in Go before each gpuagg_raw_feed_put
 	flushInterval = 100 * time.Millisecond
 	scrapeEpoch   = 5 * time.Second
 	maxSlots      = 1 << 20 // hard cap; dense counters grow with the pods actually seen
@@ -107,9 +108,8 @@ type gpuAgg struct {
 	// guards the fields below.
 	mu       sync.Mutex
 	devs     []*device
-	rawBuf   map[int][]byte // per kind: back-to-back raw records awaiting submit
-	rawShard []uint32       // per raw record of a submit: its device (gpuagg_shard_raw)
-	rawPart  [][]byte       // per device: its raw records of a submit
+	rawBuf   map[int][]byte                // per kind: back-to-back raw records awaiting submit
+	feeds    map[int]*C.gpuagg_raw_feed    // per kind: shard + scatter into pinned per-device staging
 	spec     *api.MetricsSpec
 	vecs     map[string]*prometheus.GaugeVec
 	ctrs     map[string]*prometheus.CounterVec
@@ -360,6 +360,23 @@ func (g *gpuAgg) Init() error {
 		C.gpuagg_set_time_offset(d.ctx, C.int64_t(ktime.MonotonicOffset.Nanoseconds()))
 		g.devs = append(g.devs, d)
 	}
+	// raw perf samples: one library-side feed per kind shards each handed-over buffer over
+	// the devices and copies it into their pinned staging (no per-record Go append, no
+	// pageable H2D copy)
+	ctxs := make([]*C.gpuagg_ctx, len(g.devs))
+	for i, d := range g.devs {
+		ctxs[i] = d.ctx
+	}
+	g.feeds = map[int]*C.gpuagg_raw_feed{}
+	for kind := range rawSize {
+		var f *C.gpuagg_raw_feed
+		if err := check(ctxs[0], C.gpuagg_raw_feed_create(&ctxs[0], C.size_t(len(ctxs)), C.int(kind),
+			batchCapacity, &f), "gpuagg_raw_feed_create"); err != nil {
+			g.destroyLocked()
+			return err
+		}
+		g.feeds[kind] = f
+	}
 	g.stopping = false
 	g.spec = nil
 	g.apiIPs = map[string]uint32{}
@@ -586,55 +603,31 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		d.n = 0
 		return err
 	}
-	submitRaw := func(kind int) error {
+	// submitRaw hands the kind's buffered samples to its feed: the library shards them by
+	// the 5-tuple at the records' fixed offsets (conntrack.c:34-49, drop_reason.c:39-54;
+	// the function of shardOf and dist.shard_of, so a flow's raw and decoded records meet
+	// on one device) and copies each into its device's pinned staging, submitting the
+	// stagings that fill; flush also submits the partial ones (flushInterval, Stop).
+	submitRaw := func(kind int, flush bool) error {
 		buf := g.rawBuf[kind]
-		if len(buf) == 0 {
-			return nil
-		}
 		g.mu.Lock()
 		defer g.mu.Unlock()
 		if err := g.commitLocked(); err != nil {
 			return err
 		}
-		sz := rawSize[kind]
-		n := len(buf) / sz
-		defer func() { g.rawBuf[kind] = buf[:0] }()
-		if len(devs) == 1 {
-			return check(devs[0].ctx, C.gpuagg_submit_raw(devs[0].ctx, C.int(kind), unsafe.Pointer(&buf[0]),
-				C.size_t(n)), "gpuagg_submit_raw")
-		}
-		// shard by the 5-tuple read at the records' fixed offsets (conntrack.c:34-49,
-		// drop_reason.c:39-54) -- the same function as shardOf and dist.shard_of, so a
-		// flow's raw and decoded records meet on one device -- then one submit per device
-		if cap(g.rawShard) < n {
-			g.rawShard = make([]uint32, n)
-		}
-		shards := g.rawShard[:n]
-		if err := check(devs[0].ctx, C.gpuagg_shard_raw(C.int(kind), unsafe.Pointer(&buf[0]), C.size_t(n),
-			C.uint32_t(len(devs)), (*C.uint32_t)(unsafe.Pointer(&shards[0]))), "gpuagg_shard_raw"); err != nil {
-			return err
-		}
-		if len(g.rawPart) != len(devs) {
-			g.rawPart = make([][]byte, len(devs))
-		}
-		for i := range g.rawPart {
-			g.rawPart[i] = g.rawPart[i][:0]
-		}
-		for i, d := range shards {
-			g.rawPart[d] = append(g.rawPart[d], buf[i*sz:(i+1)*sz]...)
-		}
-		var err error
-		for i, d := range devs {
-			part := g.rawPart[i]
-			if len(part) == 0 {
-				continue
-			}
-			if e := check(d.ctx, C.gpuagg_submit_raw(d.ctx, C.int(kind), unsafe.Pointer(&part[0]),
-				C.size_t(len(part)/sz)), "gpuagg_submit_raw"); e != nil && err == nil {
-				err = e
+		f := g.feeds[kind]
+		if len(buf) > 0 {
+			n := len(buf) / rawSize[kind]
+			g.rawBuf[kind] = buf[:0]
+			if err := check(g.devs[0].ctx, C.gpuagg_raw_feed_put(f, unsafe.Pointer(&buf[0]), C.size_t(n)),
+				"gpuagg_raw_feed_put"); err != nil {
+				return err
 			}
 		}
-		return err
+		if flush {
+			return check(g.devs[0].ctx, C.gpuagg_raw_feed_flush(f), "gpuagg_raw_feed_flush")
+		}
+		return nil
 	}
 	submitAll := func() error {
 		var err error
@@ -644,7 +637,7 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 			}
 		}
 		for kind := range rawSize {
-			if e := submitRaw(kind); e != nil && err == nil {
+			if e := submitRaw(kind, true); e != nil && err == nil {
 				err = e
 			}
 		}
@@ -676,8 +669,10 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 			}
 		case s := <-g.raw:
 			g.rawBuf[s.kind] = append(g.rawBuf[s.kind], s.b...)
-			if len(g.rawBuf[s.kind]) >= batchCapacity*rawSize[s.kind] {
-				if err := submitRaw(s.kind); err != nil {
+			// hand over in pieces of 64k samples: the feed submits a device's staging
+			// whenever it holds batchCapacity records
+			if len(g.rawBuf[s.kind]) >= rawPiece*rawSize[s.kind] {
+				if err := submitRaw(s.kind, false); err != nil {
 					g.l.Error("raw submit failed", zap.Error(err))
 				}
 			}
@@ -815,6 +810,10 @@ func (g *gpuAgg) Stop() error {
 }
 
 func (g *gpuAgg) destroyLocked() {
+	for kind, f := range g.feeds {
+		C.gpuagg_raw_feed_destroy(f) // before the contexts: it frees their pinned staging
+		delete(g.feeds, kind)
+	}
 	for _, d := range g.devs {
 		C.gpuagg_destroy(d.ctx) // frees the pinned batch too
 	}

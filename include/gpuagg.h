@@ -274,6 +274,24 @@ int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uin
 int gpuagg_shard_columns(const uint32_t *src_ip, const uint32_t *dst_ip, const uint32_t *ports,
                          const uint32_t *meta, size_t n, uint32_t n_shards, uint32_t *shard_out);
 
+/* Node-wide raw ingestion (the Go plugin's raw path, gpuagg_linux.go Start/submitRaw):
+ * one call shards a buffer of back-to-back raw samples over the node's contexts (one per
+ * device; the gpuagg_shard_raw function) and copies each sample into its context's
+ * pinned staging of `capacity` records; a full staging is submitted on the spot
+ * (gpuagg_submit_raw from pinned memory: the H2D copy is a DMA, and the call returns once
+ * it is done, so staging refills while the device decodes and aggregates).  Replaces
+ * the per-record Go re-append into per-device slices and the pageable H2D copy of the
+ * packetparser_linux.go:556-654 reader loop's batches.  _flush submits every partial
+ * staging (the plugin's flushInterval tick and Stop); _submitted reports the records
+ * handed to each context.  Not thread-safe: one feed per reader goroutine. */
+typedef struct gpuagg_raw_feed gpuagg_raw_feed;
+int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
+                           gpuagg_raw_feed **out);
+int gpuagg_raw_feed_put(gpuagg_raw_feed *feed, const void *raw, size_t n);
+int gpuagg_raw_feed_flush(gpuagg_raw_feed *feed);
+int gpuagg_raw_feed_submitted(const gpuagg_raw_feed *feed, uint64_t *per_ctx, size_t n_ctx);
+void gpuagg_raw_feed_destroy(gpuagg_raw_feed *feed);
+
 /* Wait for every submitted batch. */
 int gpuagg_sync(gpuagg_ctx *ctx);
 

@@ -2,6 +2,6 @@
 advanced-metrics path.  The compute path is ``libgpuagg.so``
 (hand-written gfx950 HIP kernels behind the C ABI in ``include/gpuagg.h``)."""
 
-from .engine import ContextOptions, Endpoint, GpuAgg, GpuAggError, HostBatch  # noqa: F401
+from .engine import ContextOptions, Endpoint, GpuAgg, GpuAggError, HostBatch, RawFeed  # noqa: F401
 
-__all__ = ["ContextOptions", "Endpoint", "GpuAgg", "GpuAggError", "HostBatch"]
+__all__ = ["ContextOptions", "Endpoint", "GpuAgg", "GpuAggError", "HostBatch", "RawFeed"]

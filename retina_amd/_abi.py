@@ -157,6 +157,12 @@ SIGNATURES = [
                                               C.POINTER(HubbleCols)]),
     ("gpuagg_enrich_device", C.c_int, [C.c_void_p, C.POINTER(Columns), C.c_size_t, C.c_void_p, C.c_void_p]),
     ("gpuagg_submit_enrich", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    ("gpuagg_raw_feed_create", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.c_size_t,
+                                         C.POINTER(C.c_void_p)]),
+    ("gpuagg_raw_feed_put", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("gpuagg_raw_feed_flush", C.c_int, [C.c_void_p]),
+    ("gpuagg_raw_feed_submitted", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t]),
+    ("gpuagg_raw_feed_destroy", None, [C.c_void_p]),
 ]
 
 _lib = None

@@ -3321,6 +3321,125 @@ int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uin
   }
   return GPUAGG_OK;
 }
+// ---- node-wide raw ingestion: shard + scatter into pinned per-device staging ------------
+}  // extern "C"
+
+struct gpuagg_raw_feed {
+  std::vector<gpuagg_ctx *> ctxs;
+  int kind = 0;
+  size_t rec = 0, cap = 0;         // bytes per record, records per device staging
+  std::vector<uint8_t *> buf;      // pinned (CPU backend: host) staging, one per context
+  std::vector<size_t> fill;        // records staged per context
+  std::vector<uint32_t> shard;     // scratch: the device of each record of one piece
+  std::vector<uint64_t> submitted; // records handed to each context so far
+};
+
+namespace {
+int feed_submit(gpuagg_raw_feed *f, size_t d) {
+  if (!f->fill[d]) return GPUAGG_OK;
+  // gpuagg_submit_raw returns once the H2D copy (a DMA: the staging is pinned) is done,
+  // so the staging is refilled while the device decodes and aggregates it
+  const int rc = gpuagg_submit_raw(f->ctxs[d], f->kind, f->buf[d], f->fill[d]);
+  if (rc == GPUAGG_OK) f->submitted[d] += f->fill[d];
+  f->fill[d] = 0;
+  return rc;
+}
+
+void feed_free(gpuagg_raw_feed *f) {
+  for (size_t d = 0; d < f->buf.size(); ++d)
+    if (f->buf[d]) x_host_free(f->ctxs[d], f->buf[d]);
+  delete f;
+}
+}  // namespace
+
+extern "C" {
+
+int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
+                           gpuagg_raw_feed **out) {
+  if (!ctxs || !n_ctx || !out || !capacity || (kind != kRawPacket && kind != kRawDrop)) return GPUAGG_EINVAL;
+  *out = nullptr;
+  for (size_t d = 0; d < n_ctx; ++d)
+    if (!ctxs[d]) return GPUAGG_EINVAL;
+  auto *f = new gpuagg_raw_feed();
+  f->ctxs.assign(ctxs, ctxs + n_ctx);
+  f->kind = kind;
+  f->rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
+  f->cap = capacity;
+  f->buf.assign(n_ctx, nullptr);
+  f->fill.assign(n_ctx, 0);
+  f->submitted.assign(n_ctx, 0);
+  for (size_t d = 0; d < n_ctx; ++d) {
+    gpuagg_ctx *c = ctxs[d];
+    if (bind(c) || x_host_alloc(c, (void **)&f->buf[d], capacity * f->rec) != hipSuccess) {
+      fail(c, GPUAGG_ENOMEM, "raw feed staging (%zu records)", capacity);
+      feed_free(f);
+      return GPUAGG_ENOMEM;
+    }
+    if (!c->cpu) {  // device staging sized once, not at the first submit
+      if (int rc = ensure_staging(c, capacity)) {
+        feed_free(f);
+        return rc;
+      }
+    }
+  }
+  *out = f;
+  return GPUAGG_OK;
+}
+
+int gpuagg_raw_feed_put(gpuagg_raw_feed *f, const void *raw, size_t n) {
+  if (!f || (n && !raw)) return GPUAGG_EINVAL;
+  const uint8_t *p = (const uint8_t *)raw;
+  const size_t nd = f->ctxs.size(), rec = f->rec;
+  int err = GPUAGG_OK;
+  if (nd == 1) {  // one device: straight into its staging
+    while (n) {
+      const size_t m = std::min(n, f->cap - f->fill[0]);
+      memcpy(f->buf[0] + f->fill[0] * rec, p, m * rec);
+      f->fill[0] += m;
+      p += m * rec;
+      n -= m;
+      if (f->fill[0] == f->cap)
+        if (int rc = feed_submit(f, 0)) err = err ? err : rc;
+    }
+    return err;
+  }
+  // pieces of <= 2^16 records: the device of each (gpuagg_shard_raw), then one copy of
+  // each record into its device's staging (a full staging is submitted on the spot)
+  constexpr size_t kPiece = 1u << 16;
+  if (f->shard.size() < std::min(n, kPiece)) f->shard.resize(std::min(n, kPiece));
+  while (n) {
+    const size_t m = std::min(n, kPiece);
+    gpuagg_shard_raw(f->kind, p, m, (uint32_t)nd, f->shard.data());
+    for (size_t i = 0; i < m; ++i) {
+      const uint32_t d = f->shard[i];
+      memcpy(f->buf[d] + f->fill[d] * rec, p + i * rec, rec);
+      if (++f->fill[d] == f->cap)
+        if (int rc = feed_submit(f, d)) err = err ? err : rc;
+    }
+    p += m * rec;
+    n -= m;
+  }
+  return err;
+}
+
+int gpuagg_raw_feed_flush(gpuagg_raw_feed *f) {
+  if (!f) return GPUAGG_EINVAL;
+  int err = GPUAGG_OK;
+  for (size_t d = 0; d < f->ctxs.size(); ++d)
+    if (int rc = feed_submit(f, d)) err = err ? err : rc;
+  return err;
+}
+
+int gpuagg_raw_feed_submitted(const gpuagg_raw_feed *f, uint64_t *per_ctx, size_t n_ctx) {
+  if (!f || !per_ctx || n_ctx < f->ctxs.size()) return GPUAGG_EINVAL;
+  for (size_t d = 0; d < f->ctxs.size(); ++d) per_ctx[d] = f->submitted[d];
+  return GPUAGG_OK;
+}
+
+void gpuagg_raw_feed_destroy(gpuagg_raw_feed *f) {
+  if (f) feed_free(f);
+}
+
 const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }
 const char *gpuagg_sketch_kernel_name(const gpuagg_ctx *c) { return c ? c->sketch_kernel_name.c_str() : ""; }
 

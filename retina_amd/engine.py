@@ -464,3 +464,47 @@ class GpuAgg:
 
     def set_timing(self, enabled: bool) -> None:
         self._check(self.lib.gpuagg_set_timing(self.h, 1 if enabled else 0))
+
+
+class RawFeed:
+    """Node-wide raw ingestion over one context per device (gpuagg_raw_feed_*): samples are
+    sharded by the 5-tuple (gpuagg_shard_raw's function) and copied into each context's
+    pinned staging in the library; full stagings are submitted as they fill."""
+
+    def __init__(self, engines, kind: int, capacity: int = 1 << 20):
+        self.engines = list(engines)
+        self.lib = self.engines[0].lib
+        self.kind = kind
+        self.size = _abi.RAW_SIZE[kind]
+        arr = (C.c_void_p * len(self.engines))(*[e.h for e in self.engines])
+        h = C.c_void_p()
+        rc = self.lib.gpuagg_raw_feed_create(arr, len(self.engines), kind, capacity, C.byref(h))
+        if rc != _abi.OK:
+            msg = self.lib.gpuagg_last_error(self.engines[0].h)
+            raise GpuAggError(rc, "gpuagg_raw_feed_create: %s" % (msg.decode() if msg else ""))
+        self.h = h
+
+    def put(self, raw: np.ndarray) -> None:
+        raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
+        if raw.size % self.size:
+            raise ValueError("raw buffer is not a whole number of %d-byte records" % self.size)
+        rc = self.lib.gpuagg_raw_feed_put(self.h, raw.ctypes.data_as(C.c_void_p), raw.size // self.size)
+        if rc != _abi.OK:
+            raise GpuAggError(rc, "gpuagg_raw_feed_put")
+
+    def flush(self) -> None:
+        rc = self.lib.gpuagg_raw_feed_flush(self.h)
+        if rc != _abi.OK:
+            raise GpuAggError(rc, "gpuagg_raw_feed_flush")
+
+    def submitted(self) -> list:
+        a = (C.c_uint64 * len(self.engines))()
+        rc = self.lib.gpuagg_raw_feed_submitted(self.h, a, len(self.engines))
+        if rc != _abi.OK:
+            raise GpuAggError(rc, "gpuagg_raw_feed_submitted")
+        return list(a)
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.gpuagg_raw_feed_destroy(self.h)
+            self.h = None

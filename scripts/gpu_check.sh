@@ -37,7 +37,7 @@ for s in $STEPS; do
       rc=$?; echo "bench rc=$rc" >> "$OUT/${TAG}_bench_${cfg}.err"; [ $rc -ne 0 ] && exit $rc ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_${cfg}" -o run \
-        -- python3 "$R/bench.py" --config "$cfg" --steps 5 --warmup 1 --no-cpu-baseline --no-host-fed --no-production \
+        -- python3 "$R/bench.py" --config "$cfg" --steps 5 --warmup 1 --no-cpu-baseline --no-host-fed --no-production --no-scrape \
         > "$OUT/${TAG}_prof_${cfg}.log" 2>&1
       rc=$?; echo "prof rc=$rc" >> "$OUT/${TAG}_prof_${cfg}.log"; [ $rc -ne 0 ] && exit $rc
       find "$OUT/${TAG}_prof_${cfg}" -name "*kernel_stats.csv" -exec cp {} "$OUT/${TAG}_${cfg}_kernel_stats.csv" \; ;;
@@ -51,7 +51,7 @@ for s in $STEPS; do
                  "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_ATOMIC_sum"; do
         i=$((i+1))
         timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d "$OUT/${TAG}_pmc_${cfg}_$i" -o run \
-          -- python3 "$R/bench.py" --config "$cfg" --steps 2 --warmup 1 --no-cpu-baseline --no-host-fed --no-production \
+          -- python3 "$R/bench.py" --config "$cfg" --steps 2 --warmup 1 --no-cpu-baseline --no-host-fed --no-production --no-scrape \
           > "$OUT/${TAG}_pmc_${cfg}_$i.log" 2>&1
         rc=$?; echo "pmc$i rc=$rc" >> "$OUT/${TAG}_pmc_${cfg}_$i.log"
         [ $rc -ne 0 ] && exit $rc

@@ -66,3 +66,49 @@ def test_bad_arguments(lib):
     raw = np.zeros(72, np.uint8)
     assert lib.gpuagg_shard_raw(99, raw.ctypes.data_as(C.c_void_p), 1, 2, _u32p(out)) == _abi.EINVAL
     assert lib.gpuagg_shard_raw(_abi.RAW_PACKET, raw.ctypes.data_as(C.c_void_p), 1, 0, _u32p(out)) == _abi.EINVAL
+
+
+@pytest.mark.parametrize("world,cap", [(1, 5_000), (3, 4_096), (8, 1_000)])
+def test_raw_feed_scatter(lib, world, cap):
+    """gpuagg_raw_feed_* (the Go plugin's node-wide raw path) on CPU-backend contexts:
+    every context receives exactly the records gpuagg_shard_raw assigns it, its series
+    equal the oracle over that shard, and the merged state equals one context fed
+    everything.  Capacities smaller than the input force submits in the middle of a put."""
+    from retina_amd import RawFeed, _abi
+    from .helpers import diff_series, make_engine, oracle_series
+    pods = W.make_pods(300, seed=21)
+    sp = [{"metric_name": m, "source_labels": ["namespace", "podname"]}
+          for m in ("forward_count", "forward_bytes", "drop_count", "drop_bytes")]
+    for kind, raw, dec in ((_abi.RAW_PACKET, W.gen_raw_packets(12_000, pods, seed=22), D.decode_packets),
+                           (_abi.RAW_DROP, W.gen_raw_drops(9_000, pods, seed=23), D.decode_drops)):
+        b, _ = dec(raw)
+        n = len(b.src_ip)
+        shard = np.zeros(n, np.uint32)
+        assert lib.gpuagg_shard_raw(kind, raw.ctypes.data_as(C.c_void_p), n, world, _u32p(shard)) == 0
+        engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(world)]
+        feed = RawFeed(engines, kind, capacity=cap)
+        try:
+            step = 2_500  # several puts, unaligned with the capacity
+            for a in range(0, n, step):
+                feed.put(raw[a * feed.size:min(n, a + step) * feed.size])
+            feed.flush()
+            assert feed.submitted() == [int((shard == d).sum()) for d in range(world)]
+            for d, g in enumerate(engines):
+                m = shard == d
+                part = W.Records(b.src_ip[m], b.dst_ip[m], b.bytes[m], b.meta[m], b.ports[m], b.dns_id[m])
+                want = oracle_series(part, pods, sp, False)
+                got = g.snapshot()
+                assert got == want, diff_series(got, want)
+        finally:
+            feed.close()
+            for g in engines:
+                g.close()
+
+
+def test_raw_feed_rejects_bad_args(lib):
+    from retina_amd import _abi
+    h = C.c_void_p()
+    arr = (C.c_void_p * 1)(None)
+    assert lib.gpuagg_raw_feed_create(arr, 1, _abi.RAW_PACKET, 16, C.byref(h)) == _abi.EINVAL
+    assert lib.gpuagg_raw_feed_put(None, None, 0) == _abi.EINVAL
+    assert lib.gpuagg_raw_feed_flush(None) == _abi.EINVAL
