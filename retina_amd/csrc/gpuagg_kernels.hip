@@ -1873,6 +1873,9 @@ struct SketchK {
   uint32_t sbc, sbh, round;
   uint32_t sbs;  // hll_split_kernel staging ring per fine window (0: unstaged)
   uint32_t sbs_every;  // hll_split_kernel: rounds between flushes of the rings
+  // deferred folds: the scatter appends after the fill earlier launches stored in
+  // counts / hcounts (their lists are folded later, once, by the fold kernels)
+  uint32_t accum;
 };
 
 // Walks n4 16-byte list words starting at lane t with stride `stride`, four loads in
@@ -1946,7 +1949,10 @@ __global__ __launch_bounds__(1024) void sketch_scatter_kernel(SketchK k) {
   const uint32_t img_off = (k.nwin + k.hnsup + 3u) & ~3u;
   const uint32_t *keys = wcnt + img_off;
   const uint16_t *vals = (const uint16_t *)((const uint8_t *)keys + ipl_vals_offset(k.ipl_nb));
-  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnsup; i += blockDim.x) wcnt[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < k.nwin + k.hnsup; i += blockDim.x)
+    wcnt[i] = !k.accum ? 0u
+              : i < k.nwin ? k.counts[(size_t)blockIdx.x * k.nwin + i]
+                           : k.hcounts[(size_t)blockIdx.x * k.hnsup + (i - k.nwin)];
   if (kLdsIp)
     for (uint32_t i = threadIdx.x; i < k.ipl_bytes / 16; i += blockDim.x)
       ((uint4 *)(wcnt + img_off))[i] = ((const uint4 *)k.ipl)[i];
@@ -2050,7 +2056,14 @@ __global__ __launch_bounds__(1024) void sketch_stage_kernel(SketchK k) {
   const uint32_t hdummy = nh * sbh;  // 64 u32 dummies follow the HLL rings
   const uint32_t img_off = stage_words(nw, nh, sbc, sbh);
   const uint8_t *img = (const uint8_t *)(sm + img_off);
-  for (uint32_t i = threadIdx.x; i < 2u * (nw + nh); i += blockDim.x) sm[i] = 0u;
+  // rc / hc (this round's appends) start at 0; rb / hb (list fill) at 0, or with deferred
+  // folds at the fill the previous launches stored
+  for (uint32_t i = threadIdx.x; i < 2u * (nw + nh); i += blockDim.x) {
+    uint32_t v = 0u;
+    if (k.accum && i >= nw && i < 2u * nw) v = k.counts[(size_t)blockIdx.x * nw + (i - nw)];
+    if (k.accum && i >= 2u * nw + nh) v = k.hcounts[(size_t)blockIdx.x * nh + (i - 2u * nw - nh)];
+    sm[i] = v;
+  }
   if (kIp) fill_lds_u4((uint4 *)(sm + img_off), (const uint4 *)k.ipl, k.ipl_bytes / 16);
   __syncthreads();
   const uint32_t D = kD ? (uint32_t)kD : k.depth;
@@ -2465,7 +2478,8 @@ __global__ __launch_bounds__(1024) void cms_fold_kernel(SketchK k, uint32_t n_li
 }
 
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels) {
-  if (a.n == 0) return hipSuccess;
+  const bool scatter = a.passes != kSketchFolds, folds = a.passes != kSketchScatter;
+  if (a.n == 0 && scatter) return hipSuccess;
   std::string names;
   SketchK k{};
   k.src = a.cols.src_ip;
@@ -2497,6 +2511,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   k.hlists2 = a.hll_lists2;
   k.hcounts2 = a.hll_counts2;
   k.hll_slots = a.hll_slots;
+  k.accum = a.accum ? 1u : 0u;
   hipError_t e;
   size_t scatter_lds = (size_t)((a.nwin + a.hll_nsup + 3u) & ~3u) * 4;
   // source lookups in an LDS image of the IP table when it fits next to the counters
@@ -2515,8 +2530,8 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   // staged scatter: rings sized for a round's mean appends x 1.5 + 64 (the overflow goes
   // straight to the list), flushed every 4 records per lane, or every 2 when the 4-record
   // rings do not fit; sources looked up in the radix image when the pod IPs allow one
-  bool staged = false;
-  if (vec && (!a.cms_depth || a.nwin) && (!a.hll_p || a.hll_nsup) && (a.nwin || a.hll_nsup)) {
+  bool staged = !scatter;  // a fold-only call launches no scatter
+  if (scatter && vec && (!a.cms_depth || a.nwin) && (!a.hll_p || a.hll_nsup) && (a.nwin || a.hll_nsup)) {
     const int ip_kind = lds_ip ? (a.ipl_dense ? 3 : a.ipl_radix ? 2 : 1) : 0;
     if (lds_ip) {
       k.ipl_npfx = a.ipl_npfx;
@@ -2578,8 +2593,12 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
   if ((e = hipGetLastError()) != hipSuccess) return e;
     names = std::string("sketch_scatter_kernel<") + (vec ? "true" : "false") + ", " + (lds_ip ? "true" : "false") + ">";
   }  // unstaged
+  if (!folds) {
+    if (kernels) *kernels = names;
+    return hipSuccess;
+  }
   if (a.nwin && a.cms_depth) {
-    names += "+cms_fold_kernel";
+    names += names.empty() ? "cms_fold_kernel" : "+cms_fold_kernel";
     const size_t lds = (size_t)4 << a.win_shift;
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2589,7 +2608,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (a.hll_nsup && a.hll_p) {
-    names += "+hll_split_kernel+hll_fold_kernel";
+    names += names.empty() ? "hll_split_kernel+hll_fold_kernel" : "+hll_split_kernel+hll_fold_kernel";
     // staging rings: a round (4096 entries) over nfine windows, x 2 + 64, when they fit;
     // larger rings where LDS allows, flushed every few rounds (each flush is a barrier
     // pair for the workgroup): C3's 128 fine windows take 256-entry rings, every 3 rounds

@@ -202,7 +202,12 @@ struct SketchArgs {
   bool ipl_radix;                   // the image is the radix form (ipl_npfx / ipl_pfx)
   bool ipl_dense;                   // ... the dense radix form (ipl_pfx / ipl_dr)
   uint32_t ipl_npfx, ipl_pfx[kIprMaxPfx], ipl_dr[kIprMaxPfx];
+  // which kernels run: the scatter, the folds, or both (kSketchBoth, the default 0); a
+  // scatter with accum appends after the fill earlier scatters stored (deferred folds)
+  uint32_t passes;
+  bool accum;
 };
+constexpr uint32_t kSketchBoth = 0, kSketchScatter = 1, kSketchFolds = 2;
 // *kernels: the pass's kernels in rocprofv3 spelling joined by "+"
 hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels);
 

@@ -305,6 +305,14 @@ struct gpuagg_ctx {
     uint64_t budget = 0;    // records per workgroup the lists were sized for
     uint64_t rpb = 0;       // records per workgroup appended so far
   } pend;
+  // Deferred sketch folds: small launches' count-min / HLL scatter lists accumulate (the
+  // scatter starts from the stored fill) and cms_fold / hll_split / hll_fold run once.
+  struct SketchPending {
+    bool active = false;
+    SketchArgs s{};       // geometry and lists of the waiting scatters
+    uint64_t budget = 0;  // records per scatter workgroup the lists were sized for
+    uint64_t rpb = 0;     // records per workgroup appended so far
+  } sk_pend;
   bool defer_folds = true;
   uint64_t wide_list_bytes = 0;  // wide-key list budget (gpuagg_create)
   std::vector<std::array<hipEvent_t, 2>> pending_fold;  // deferred fold start, end
@@ -547,11 +555,14 @@ constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 // Folds the lists of the deferred launches (no-op when none are waiting).  Every reader
 // of the counters or the group-by table calls it first: gpuagg_sync (and through it the
 // snapshot), state export, merge, slot retirement and dense re-layout.
+int fold_pending_sketch(gpuagg_ctx *c);
+
 int fold_pending(gpuagg_ctx *c) {
   if (c->cpu) {  // the host threads' accumulators into the ctx's counters and table
     c->cpu->flush();
     return GPUAGG_OK;
   }
+  if (int rc = fold_pending_sketch(c)) return rc;
   if (!c->pend.active) return GPUAGG_OK;
   c->pend.active = false;
   LaunchArgs f = c->pend.a;
@@ -575,6 +586,7 @@ int fold_pending(gpuagg_ctx *c) {
 // The state is being cleared: the waiting lists are discarded with it.
 void drop_pending(gpuagg_ctx *c) {
   c->pend.active = false;
+  c->sk_pend.active = false;
   if (c->cpu) c->cpu->drop();
 }
 
@@ -754,6 +766,49 @@ constexpr uint32_t kCmsWindowShift = 15, kCmsMaxWindows = 4096;
 // pod-in-window in 8 bits and the register index in 18, so p <= 17 and shift <= 8)
 constexpr uint32_t kHllWindowLog2Bytes = 17, kHllMaxWindows = 8192;
 
+// Records per scatter workgroup between deferred sketch folds (64 launches of the Go
+// plugin's 2^20-record batches over 256 workgroups).
+constexpr uint64_t kSketchDeferRecords = 1ull << 18;
+
+// HLL level-2 (split) lists for `records` scatter entries at most: m / (nsup * b2 * nfine)
+// per list, +25 % + 64 of headroom (a full list applies the update with the global CAS).
+int size_hll_level2(gpuagg_ctx *c, SketchArgs &s, uint64_t records) {
+  const uint64_t nfine = (uint64_t)1 << (s.hll_sshift - s.hll_shift);
+  const uint64_t mean2 = records / ((uint64_t)s.hll_nsup * s.hll_b2 * nfine);
+  const uint64_t cap2 = (mean2 + mean2 / 4 + 64 + 15) & ~15ULL;
+  const size_t n2 = (size_t)s.hll_nsup * s.hll_b2 * nfine;
+  int rc;
+  if ((rc = ensure_buf(c, &c->d_hll_lists2, &c->hll_lists2_alloc, n2 * cap2))) return rc;
+  if ((rc = ensure_buf(c, &c->d_hll_counts2, &c->hll_counts2_alloc, n2))) return rc;
+  s.hll_cap2 = (uint32_t)cap2;
+  s.hll_lists2 = c->d_hll_lists2;
+  s.hll_counts2 = c->d_hll_counts2;
+  return GPUAGG_OK;
+}
+
+// The deferred sketch scatters' lists folded into the count-min rows and HLL registers.
+int fold_pending_sketch(gpuagg_ctx *c) {
+  if (!c->sk_pend.active) return GPUAGG_OK;
+  c->sk_pend.active = false;
+  SketchArgs s = c->sk_pend.s;
+  s.passes = kSketchFolds;
+  s.accum = false;
+  int rc;
+  if (s.hll_nsup && (rc = size_hll_level2(c, s, c->sk_pend.rpb * s.blocks))) return rc;
+  std::array<hipEvent_t, 2> ev{};
+  if (c->timing) {
+    for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+  }
+  ENQ(c);
+  HIPCHK(c, launch_sketch(s, c->stream, nullptr));
+  if (c->timing) {
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->pending_fold.push_back(ev);
+  }
+  return GPUAGG_OK;
+}
+
 // The sketch pass over n records: count-min scatter + fold, HLL direct (SketchArgs).
 int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc;
@@ -807,10 +862,59 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   }
   const uint64_t nwin = s.cms_depth ? ((uint64_t)s.cms_depth << (s.cms_wlog2 - s.win_shift)) : 0;
   const uint64_t per_launch = (uint64_t)s.blocks << 20;  // <= 2^20 records per scatter workgroup
+  // Lists sized for `rpb` records per scatter workgroup (one launch's chunk, or the deferral
+  // budget).  CMS: expected entries per list = rpb * depth / nwin, +12.5 % + 2048 of headroom;
+  // HLL level 1: at most one entry per record, rpb / nsup per list, +25 % + 64 (a full list
+  // falls back to the exact global atomic / CAS).
+  auto size_lists = [&](SketchArgs &x, uint64_t rpb) -> int {
+    int r;
+    x.nwin = 0;
+    if (!direct && nwin && nwin <= kCmsMaxWindows) {
+      const uint64_t mean = rpb * x.cms_depth / nwin;
+      const uint64_t cap = (mean + mean / 8 + 2048 + 7) & ~7ULL;
+      if ((r = ensure_buf(c, &c->d_sk_lists, &c->sk_lists_alloc, (size_t)x.blocks * nwin * cap))) return r;
+      if ((r = ensure_buf(c, &c->d_sk_counts, &c->sk_counts_alloc, (size_t)x.blocks * nwin))) return r;
+      x.nwin = (uint32_t)nwin;
+      x.cap = (uint32_t)cap;
+      x.lists = c->d_sk_lists;
+      x.counts = c->d_sk_counts;
+      x.fold_blocks = (uint32_t)nwin * std::max<uint32_t>(1u, c->n_cu / (uint32_t)nwin);
+    }
+    x.hll_nwin = x.hll_nsup = 0;
+    if (hnsup) {
+      const uint64_t mean = rpb / hnsup;
+      const uint64_t cap = (mean + mean / 4 + 64 + 15) & ~15ULL;
+      if ((r = ensure_buf(c, &c->d_hll_lists, &c->hll_lists_alloc, (size_t)x.blocks * hnsup * cap))) return r;
+      if ((r = ensure_buf(c, &c->d_hll_counts, &c->hll_counts_alloc, (size_t)x.blocks * hnsup))) return r;
+      x.hll_nsup = (uint32_t)hnsup;
+      x.hll_nwin = (uint32_t)hnwin;
+      x.hll_cap = (uint32_t)cap;
+      x.hll_lists = c->d_hll_lists;
+      x.hll_counts = c->d_hll_counts;
+    }
+    return GPUAGG_OK;
+  };
   std::array<hipEvent_t, 2> ev{};
   if (c->timing) {
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
+  }
+  // Deferred folds (small launches, e.g. the Go plugin's 2^20 records: chunk 4096): the
+  // folds' fixed passes -- every count-min row and the whole HLL register array (164 MB at
+  // C3's 10k pods, p = 14) are read and rewritten -- cost ~20x the scatter of such a launch,
+  // so launches keep appending to one set of lists sized for kSketchDeferRecords records per
+  // workgroup and fold_pending folds them once (gpuagg_sync, state reads, merge, relayout,
+  // or when the next launch would not fit).
+  const uint64_t chunk1 = ((std::min<uint64_t>(n, per_launch) + s.blocks - 1) / s.blocks + 3) & ~3ULL;
+  const bool defer = c->defer_folds && !direct && n <= per_launch && 2 * chunk1 <= kSketchDeferRecords &&
+                     (nwin || hnsup);
+  if (c->sk_pend.active) {
+    const SketchArgs &q = c->sk_pend.s;
+    const bool fits = defer && c->sk_pend.rpb + chunk1 <= c->sk_pend.budget && q.blocks == s.blocks &&
+                      q.cms == s.cms && q.hll == s.hll && q.hll_slots == s.hll_slots &&
+                      q.hll_shift == s.hll_shift && q.hll_sshift == s.hll_sshift && q.hll_b2 == s.hll_b2 &&
+                      q.lists == c->d_sk_lists && q.hll_lists == c->d_hll_lists;
+    if (!fits && (rc = fold_pending_sketch(c))) return rc;
   }
   for (uint64_t off = 0; off < n; off += per_launch) {
     const uint64_t m = std::min<uint64_t>(per_launch, n - off);
@@ -818,44 +922,37 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
                       cv.ports ? cv.ports + off : nullptr, nullptr};
     s.n = m;
     s.chunk = ((m + s.blocks - 1) / s.blocks + 3) & ~3ULL;  // whole 4-record vectors
-    s.nwin = 0;
-    if (!direct && nwin && nwin <= kCmsMaxWindows) {
-      // expected entries per list = chunk * depth / nwin; +12.5 % + 2048 of headroom
-      // (overflow is exact but slow: it falls back to a global atomic)
-      const uint64_t mean = s.chunk * s.cms_depth / nwin;
-      const uint64_t cap = (mean + mean / 8 + 2048 + 7) & ~7ULL;
-      if ((rc = ensure_buf(c, &c->d_sk_lists, &c->sk_lists_alloc, (size_t)s.blocks * nwin * cap))) return rc;
-      if ((rc = ensure_buf(c, &c->d_sk_counts, &c->sk_counts_alloc, (size_t)s.blocks * nwin))) return rc;
-      s.nwin = (uint32_t)nwin;
-      s.cap = (uint32_t)cap;
-      s.lists = c->d_sk_lists;
-      s.counts = c->d_sk_counts;
-      s.fold_blocks = (uint32_t)nwin * std::max<uint32_t>(1u, c->n_cu / (uint32_t)nwin);
+    if (defer) {
+      const bool accum = c->sk_pend.active;
+      if (accum) {  // the waiting lists' geometry
+        const SketchArgs &q = c->sk_pend.s;
+        s.nwin = q.nwin;
+        s.cap = q.cap;
+        s.lists = q.lists;
+        s.counts = q.counts;
+        s.fold_blocks = q.fold_blocks;
+        s.hll_nsup = q.hll_nsup;
+        s.hll_nwin = q.hll_nwin;
+        s.hll_cap = q.hll_cap;
+        s.hll_lists = q.hll_lists;
+        s.hll_counts = q.hll_counts;
+      } else if ((rc = size_lists(s, kSketchDeferRecords))) {
+        return rc;
+      }
+      s.passes = kSketchScatter;
+      s.accum = accum;
+      ENQ(c);
+      HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
+      c->sk_pend.rpb = (accum ? c->sk_pend.rpb : 0) + s.chunk;
+      c->sk_pend.budget = kSketchDeferRecords;
+      c->sk_pend.s = s;
+      c->sk_pend.active = true;
+      continue;
     }
-    s.hll_nwin = s.hll_nsup = 0;
-    if (hnsup) {
-      // at most one entry per record; uniform pods give chunk / nsup per scatter list and
-      // m / (nsup * b2 * nfine) per split list: +25 % + 64 of headroom each (a full list
-      // applies the update with the global CAS, exact)
-      const uint64_t nfine = (uint64_t)1 << (s.hll_sshift - s.hll_shift);
-      const uint64_t mean = s.chunk / hnsup;
-      const uint64_t cap = (mean + mean / 4 + 64 + 15) & ~15ULL;
-      const uint64_t mean2 = m / (hnsup * s.hll_b2 * nfine);
-      const uint64_t cap2 = (mean2 + mean2 / 4 + 64 + 15) & ~15ULL;
-      if ((rc = ensure_buf(c, &c->d_hll_lists, &c->hll_lists_alloc, (size_t)s.blocks * hnsup * cap))) return rc;
-      if ((rc = ensure_buf(c, &c->d_hll_counts, &c->hll_counts_alloc, (size_t)s.blocks * hnsup))) return rc;
-      const size_t n2 = (size_t)hnsup * s.hll_b2 * nfine;
-      if ((rc = ensure_buf(c, &c->d_hll_lists2, &c->hll_lists2_alloc, n2 * cap2))) return rc;
-      if ((rc = ensure_buf(c, &c->d_hll_counts2, &c->hll_counts2_alloc, n2))) return rc;
-      s.hll_nsup = (uint32_t)hnsup;
-      s.hll_nwin = (uint32_t)hnwin;
-      s.hll_cap = (uint32_t)cap;
-      s.hll_lists = c->d_hll_lists;
-      s.hll_counts = c->d_hll_counts;
-      s.hll_cap2 = (uint32_t)cap2;
-      s.hll_lists2 = c->d_hll_lists2;
-      s.hll_counts2 = c->d_hll_counts2;
-    }
+    if ((rc = size_lists(s, s.chunk))) return rc;
+    if (hnsup && (rc = size_hll_level2(c, s, m))) return rc;
+    s.passes = kSketchBoth;
+    s.accum = false;
     ENQ(c);
     HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
   }
@@ -2761,6 +2858,7 @@ int gpuagg_sketch_refresh(gpuagg_ctx *c) {
   if (!c) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, x_sync(c, c->stream));
   c->h_cms.resize(c->cms_len);
   c->h_hll.resize(c->hll_len);
@@ -2807,6 +2905,7 @@ int gpuagg_cms_copy(gpuagg_ctx *c, uint32_t *out, size_t n) {
   if (!c || !out || n < c->cms_len) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, x_sync(c, c->stream));
   if (c->cms_len) HIPCHK(c, x_copy(c, out, c->d_cms, c->cms_len * 4, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
@@ -2816,6 +2915,7 @@ int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
   if (!c || !out || n < c->hll_len) return GPUAGG_EINVAL;
   int rc = bind(c);
   if (rc) return rc;
+  if ((rc = fold_pending(c))) return rc;
   HIPCHK(c, x_sync(c, c->stream));
   if (c->hll_len) HIPCHK(c, x_copy(c, out, c->d_hll, c->hll_len, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
@@ -2824,7 +2924,7 @@ int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
 // ---- multi-GPU merge hooks -----------------------------------------------------------
 int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   if (!c || !o) return GPUAGG_EINVAL;
-  if (c->pend.active) {  // the arrays below are read by the caller: fold what is waiting
+  if (c->pend.active || c->sk_pend.active) {  // the arrays below are read by the caller: fold what is waiting
     int rc = bind(c);
     if (rc || (rc = fold_pending(c))) return rc;
     HIPCHK(c, x_sync(c, c->stream));

@@ -136,3 +136,61 @@ def test_c3_full_shape_bit_exact(gpu_device):
     assert np.array_equal(cms, want_c)
     assert np.array_equal(hll[:len(pods.endpoints)], want_h)
     assert int(cms[0].sum()) == n
+
+
+@pytest.mark.parametrize("flags", [0, 8], ids=["deferred", "per-batch"])
+def test_deferred_sketch_folds_exact(gpu_device, flags):
+    """Small launches (the Go plugin's batch geometry) defer their count-min / HLL folds:
+    the scatters append to one set of lists sized for 2^18 records per workgroup and
+    fold_pending folds them once.  Exact against the restatement across mid-stream reads
+    (cms_array / hll_array fold what waits), 66 launches of 2^20 records (the 64-launch
+    budget overflows and folds; the batch is resubmitted, so count-min is linear in the
+    repeats and HLL idempotent), ragged launches and a slot-table growth (relayout folds).
+    FLAG_FOLD_PER_BATCH (8) keeps per-launch folds as the reference point."""
+    from retina_amd import GpuAgg
+    pods = W.make_pods(300, seed=51)
+    more = W.make_pods(900, seed=51)  # same IPs for the first 300: the slot table grows
+    g = make_engine(pods, W.LOCAL_FWD_DROP, False, gpu_device, cms_depth=4, cms_width_log2=16,
+                    hll_precision=12, flags=flags, max_slots=2048, max_ips=4096)
+    want_c = np.zeros((4, 1 << 16), np.uint32)
+    want_h = np.zeros((len(more.endpoints), 1 << 12), np.uint8)
+
+    def expect(r, src_pods, times=1):
+        one = np.zeros_like(want_c)
+        S.cms_update(one, r.src_ip, r.dst_ip, r.ports, r.meta & np.uint32(0xFF))
+        want_c[:] += one * np.uint32(times)
+        S.hll_update(want_h, _src_slots(src_pods, r.src_ip), r.dst_ip, 12)
+
+    def check(tag):
+        assert np.array_equal(g.cms_array(), want_c), tag
+        assert np.array_equal(g.hll_array()[:len(more.endpoints)], want_h), tag
+
+    total = 0
+    try:
+        for k in range(6):  # distinct small batches, ragged sizes
+            m = (1 << 16) + 1000 * k + k
+            r = W.gen_records(m, pods, seed=5200 + k, udp_frac=0.2)
+            g.submit_device(GpuAgg.device_columns(*to_device(r, gpu_device)), m)
+            expect(r, pods)
+            total += m
+        check("after 6 small launches")
+        big = W.gen_records(1 << 20, pods, seed=5300, udp_frac=0.2)
+        cols = GpuAgg.device_columns(*to_device(big, gpu_device))
+        for _ in range(66):
+            g.submit_device(cols, 1 << 20)
+        expect(big, pods, 66)
+        total += 66 << 20
+        check("after 66 launches of 2^20")
+        g.load_endpoints(more.endpoints[len(pods.endpoints):], version=2)
+        for k in range(3):
+            r = W.gen_records(50_000, more, seed=5400 + k, udp_frac=0.2)
+            g.submit_device(GpuAgg.device_columns(*to_device(r, gpu_device)), 50_000)
+            expect(r, more)
+            total += 50_000
+            if k == 0:
+                g.load_endpoints([], version=3)  # a commit between launches
+        g.sync()
+        check("final")
+        assert g.stats()["records"] == total
+    finally:
+        g.close()
