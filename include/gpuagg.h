@@ -400,10 +400,15 @@ typedef struct gpuagg_latency_state {
   uint64_t no_response;             /* entries that expired unanswered                   */
   uint64_t pending;                 /* requests waiting for a reply (carried over)        */
   uint64_t peak_pending;            /* most requests carried across a batch boundary since
-                                       the last reconcile: a lower bound of the live peak.
-                                       The reference's TTL cache holds at most 100000
-                                       (latency.go:35,121); past that its results differ
-                                       (it drops entries), this engine keeps them all     */
+                                       the last reconcile                                  */
+  uint64_t peak_live;               /* most requests live at any event since the reset   */
+  uint64_t capacity_evictions;      /* requests evicted because `limit` were live when a
+                                       new one arrived: ttlcache.WithCapacity(LIMIT)
+                                       (latency.go:35,120-121), EvictionReasonCapacityReached,
+                                       not a no_response                                 */
+  uint64_t capacity_batches;        /* batches in which the capacity bound (replayed in
+                                       event order by the sequential pass)              */
+  uint64_t limit;                   /* gpuagg_config.latency_limit or 100000             */
 } gpuagg_latency_state;
 
 int gpuagg_latency_read(gpuagg_ctx *ctx, gpuagg_latency_state *out);

@@ -13,16 +13,24 @@ Follows pkg/module/metrics/latency.go of the reference:
     observe round((Nanos - t) / 1e6) ms, observe the handshake latency when the stored
     packet had SYN and this one SYN+ACK, and delete the entry;
   * the ttlcache (:118-132): TTL 500 ms, an entry that expires unanswered counts one
-    no_response (EvictionReasonExpired); deletions do not count.
+    no_response (EvictionReasonExpired); deletions do not count;
+  * the cache is github.com/jellydator/ttlcache/v3 v3.3.0 (go.mod:306; not vendored in the
+    reference, so its published behaviour is restated here -- parity unpinned, the
+    reference's tests never fill the cache): `Get` of a live key "touches" it (its
+    expiry becomes now + TTL and it moves to the front of the LRU list, unless
+    WithDisableTouchOnHit, which latency.go does not set), so a repeated TO_NETWORK packet
+    (same TSval) keeps its request alive; `WithCapacity(LIMIT)` makes `Set` of a new key
+    with LIMIT live entries first evict the LRU back (EvictionReasonCapacityReached: no
+    no_response).  Every touch happens at the current clock, so LRU order is expiry order.
 
 The reference's TTL clock is the agent's wall clock; a batch replay has none, so this
 restatement uses the record timestamps as the clock: before a record is processed every
 entry whose expiry (insert clock + 500 ms) lies before the running maximum of the record
 times seen so far is evicted (and counted).  The ttlcache capacity (LIMIT = 100000 live
-entries, capacity evictions do not count) is tracked and reported as `peak_live`; the
-engine has no such limit, so parity holds whenever fewer than 100000 requests are
-pending at once (tests assert it).  The latency arithmetic (Nanos only, so a pair that
-straddles a second boundary gives a negative latency) is the reference's.
+entries, capacity evictions do not count) is enforced: a new request that finds LIMIT
+live entries evicts the least recently touched one (`capacity_evictions` counts them).
+The latency arithmetic (Nanos only, so a pair that straddles a second boundary gives a
+negative latency) is the reference's.
 """
 
 from __future__ import annotations
@@ -80,7 +88,7 @@ class _Entry:
 
 
 class LatencyMetrics:
-    def __init__(self, metric_names: Set[str]):
+    def __init__(self, metric_names: Set[str], limit: int = LIMIT):
         self.latency = Histogram() if LATENCY in metric_names else None
         self.handshake = Histogram() if HANDSHAKE in metric_names else None
         self.no_response: Optional[int] = 0 if NO_RESPONSE in metric_names else None
@@ -88,6 +96,8 @@ class LatencyMetrics:
         self.cache: "OrderedDict[Tuple, _Entry]" = OrderedDict()
         self.clock = 0
         self.peak_live = 0
+        self.limit = limit
+        self.capacity_evictions = 0
 
     # apiserverWatcherCallbackFn (:307-333)
     def add_ips(self, ips: List[str]) -> None:
@@ -98,7 +108,8 @@ class LatencyMetrics:
             self.apiserver_ips.discard(ip)
 
     def _expire(self) -> None:
-        # insert clocks never decrease, so insertion order is expiry order
+        # touch clocks never decrease, so the LRU order of the OrderedDict (front = least
+        # recently touched) is expiry order
         while self.cache:
             k, e = next(iter(self.cache.items()))
             if not self.clock > e.expires:
@@ -126,7 +137,14 @@ class LatencyMetrics:
         flags = f.l4.flags
         if f.trace_observation_point == O.OBS_TO_NETWORK:
             k = (f.ip.source, f.ip.destination, f.l4.source_port, f.l4.destination_port, tcp_id)
-            if k not in self.cache:
+            e = self.cache.get(k)
+            if e is not None:  # Get hit: touched (expiry extended, moved to the LRU front)
+                e.expires = self.clock + TTL_NS
+                self.cache.move_to_end(k)
+            else:
+                if len(self.cache) >= self.limit:  # Set at capacity: the LRU back goes, uncounted
+                    self.cache.popitem(last=False)
+                    self.capacity_evictions += 1
                 self.cache[k] = _Entry(nanos, bool(flags is not None and flags.SYN), self.clock + TTL_NS)
                 self.peak_live = max(self.peak_live, len(self.cache))
         elif f.trace_observation_point == O.OBS_FROM_NETWORK:

@@ -72,7 +72,8 @@ class LatencyState(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("latency_buckets", C.c_uint64 * 11), ("latency_count", C.c_uint64),
                 ("latency_sum", C.c_int64), ("handshake_buckets", C.c_uint64 * 11),
                 ("handshake_count", C.c_uint64), ("handshake_sum", C.c_int64), ("no_response", C.c_uint64),
-                ("pending", C.c_uint64), ("peak_pending", C.c_uint64)]
+                ("pending", C.c_uint64), ("peak_pending", C.c_uint64), ("peak_live", C.c_uint64),
+                ("capacity_evictions", C.c_uint64), ("capacity_batches", C.c_uint64), ("limit", C.c_uint64)]
 
 
 class Stats(C.Structure):

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <cstring>
 #include <thread>
+#include <deque>
 #include <unordered_map>
 #include <vector>
 
@@ -420,20 +421,37 @@ void Engine::hubble(const HubbleArgs &a) {
   });
 }
 
-// The TTL join of gpuagg_latency.hip in record order.  Per key: insert on a request
-// unless live, observe + delete on the first reply, expire (no_response) when an event's
-// clock passes the entry's expiry; at the batch end entries past the end clock expire and
-// the rest carry over.  The clock of a row is the running maximum of the record times.
+// The TTL join of gpuagg_latency.hip in record order, as the ttlcache runs it: before each
+// latency event the items whose expiry the clock has passed are evicted (no_response);
+// a request inserts unless its key is live, in which case the Get hit touches it
+// (expiry = clock + TTL, front of the LRU list); a Set with `limit` live items first
+// evicts the least recently touched one (uncounted); a reply observes and deletes.  At
+// the batch end items past the end clock expire and the rest carry over in LRU order.
+// The clock of a row is the running maximum of the record times.
 void Engine::latency(const LatArgs &a, uint32_t enabled) {
   unsigned long long *st = a.state;
   struct E {
-    uint64_t expires;
+    uint64_t expires, seq;
     uint32_t nanos;
     bool syn;
   };
   std::unordered_map<Key, E, KeyHash> live;
-  for (const auto &c : carry_) live[Key{c.k0, c.k1, 0}] = E{c.clock, c.nanos, ((c.bits >> 2) & 1u) != 0};
+  std::deque<std::pair<uint64_t, Key>> lru;  // (touch seq, key), stale once the key is touched again
+  const uint64_t limit = a.limit ? a.limit : kLatLimit;
+  for (const auto &c : carry_) {  // carried in LRU order
+    live[Key{c.k0, c.k1, 0}] = E{c.clock, c.seq, c.nanos, ((c.bits >> 2) & 1u) != 0};
+    lru.emplace_back(c.seq, Key{c.k0, c.k1, 0});
+  }
   carry_.clear();
+  // the least recently touched live item (stale records dropped), or live.end()
+  auto front = [&]() {
+    while (!lru.empty()) {
+      auto it = live.find(lru.front().second);
+      if (it != live.end() && it->second.seq == lru.front().first) return it;
+      lru.pop_front();
+    }
+    return live.end();
+  };
   auto is_api = [&](uint32_t ip) {
     for (uint32_t i = 0; i < a.n_api; ++i)
       if (a.api[i] == ip) return true;
@@ -441,6 +459,7 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
   };
   auto bucket = [](int64_t v) -> uint32_t { return v <= 0 ? 0u : v >= 5 ? 10u : (uint32_t)(2 * v); };
   uint64_t clk = st[kLatClock];
+  uint64_t seq = st[kLatSeqBase], peak = live.size();
   for (size_t i = 0; i < a.n; ++i) {
     clk = std::max<uint64_t>(clk, a.time_ns[i]);
     const uint32_t m = a.meta[i];
@@ -448,6 +467,12 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
     const uint32_t obs = m >> 30;
     const uint32_t role = obs == 3u ? 1u : obs == 2u ? 2u : 0u;
     if (!role || !(is_api(a.src[i]) || is_api(a.dst[i]))) continue;
+    const uint64_t my_seq = seq++;
+    for (auto f = front(); f != live.end() && clk > f->second.expires; f = front()) {
+      live.erase(f);  // evicted by the cleaner before this record
+      lru.pop_front();
+      if (enabled & 4u) st[kLatNoResponse] += 1;
+    }
     const uint32_t s = a.src[i], d = a.dst[i], p = a.ports[i], sp = p & 0xFFFFu, dp = p >> 16;
     const uint64_t id = a.tcp_id[i];
     const uint64_t k0 = role == 1u ? ((uint64_t)s | ((uint64_t)d << 32)) : ((uint64_t)d | ((uint64_t)s << 32));
@@ -457,14 +482,22 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
     const bool has_flags = verdict == kVerdictForwarded || verdict == kVerdictRetrans;
     const bool syn = has_flags && (flags & 2u), ack = has_flags && (flags & 16u);
     const uint32_t nanos = (uint32_t)(a.time_ns[i] % 1000000000ULL);
-    auto it = live.find(Key{k0, k1, 0});
-    if (it != live.end() && clk > it->second.expires) {  // evicted by the cleaner before this record
-      live.erase(it);
-      it = live.end();
-      if (enabled & 4u) st[kLatNoResponse] += 1;
-    }
+    const Key key{k0, k1, 0};
+    auto it = live.find(key);
     if (role == 1u) {
-      if (it == live.end()) live[Key{k0, k1, 0}] = E{clk + kLatTtlNs, nanos, syn};
+      if (it != live.end()) {  // Get hit: touched
+        it->second.expires = clk + kLatTtlNs;
+        it->second.seq = my_seq;
+      } else {
+        if (live.size() >= limit) {  // Set at capacity: the LRU back goes, uncounted
+          live.erase(front());
+          lru.pop_front();
+          st[kLatCapEvictions] += 1;
+        }
+        live[key] = E{clk + kLatTtlNs, my_seq, nanos, syn};
+        peak = std::max<uint64_t>(peak, live.size());
+      }
+      lru.emplace_back(my_seq, key);
     } else if (it != live.end()) {
       const int64_t dd = (int64_t)nanos - (int64_t)it->second.nanos, ad = dd < 0 ? -dd : dd;
       const int64_t lat = (dd < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
@@ -482,16 +515,20 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
       live.erase(it);
     }
   }
-  for (const auto &kv : live) {
-    if (clk > kv.second.expires) {
+  for (auto f = front(); f != live.end(); f = front()) {  // batch end, LRU order
+    if (clk > f->second.expires) {
       if (enabled & 4u) st[kLatNoResponse] += 1;
     } else {
-      carry_.push_back(LatEvent{kv.first.k0, kv.first.k1, kv.second.expires, kv.second.nanos,
-                                3u | (kv.second.syn ? 4u : 0u)});
+      carry_.push_back(LatEvent{f->first.k0, f->first.k1, f->second.expires, f->second.seq, f->second.nanos,
+                                3u | (f->second.syn ? 4u : 0u)});
     }
+    live.erase(f);
+    lru.pop_front();
   }
+  st[kLatSeqBase] = seq;
   st[kLatClock] = clk;
   st[kLatPending] = carry_.size();
+  st[kLatPeakLive] = std::max<uint64_t>(st[kLatPeakLive], peak);
 }
 
 void Engine::latency_reset() { carry_.clear(); }

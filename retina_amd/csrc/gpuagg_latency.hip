@@ -20,6 +20,14 @@
 //   5. lat_walk_kernel    one lane per key runs the TTL-cache state machine over its
 //                         events and books histogram buckets / no_response with atomics;
 //                         live entries carry over to the next batch.
+// The ttlcache (jellydator/ttlcache v3.3.0) also touches a key on every Get hit (a repeated
+// request keeps its entry alive: expiry = now + TTL, front of the LRU list) and holds at
+// most LIMIT = 100000 entries: a Set at capacity evicts the least recently touched one,
+// without counting it.  The capacity couples the keys, so before step 5 a first walk
+// (kPass 0) books every entry's life as +1 / -1 at event positions, a scan gives the live
+// count before each event and its maximum; while it stays within the limit (the normal
+// case) the keys are independent and step 5 is exact, else step 5 stands down and
+// lat_serial_kernel replays the batch in event order with an LRU queue (exact, slow, rare).
 // Latency traffic is a small share of a node's records; the filter pass (1, 3) streams
 // 36 B per record (src, dst, meta, ports, tcp_id, time_ns).
 #include <cstring>  // rocprim's texture iterator uses memset
@@ -150,6 +158,8 @@ __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
   const size_t lo = min((size_t)u * a.chunk, a.n), hi = min(lo + a.chunk, a.n);  // (chunks round up)
   uint64_t base = a.blk_base[u];
   unsigned long long clk = a.blk_clk[u];
+  // events are numbered across batches: position e of this batch (carried entries first)
+  const uint64_t seq0 = a.state[kLatSeqBase] - a.state[kLatPending];
   for (size_t r = lo; r < hi; r += 64) {
     const size_t i = r + lane;
     const bool in = i < hi;
@@ -177,7 +187,7 @@ __global__ __launch_bounds__(kLatThreads) void lat_emit_kernel(LatArgs a) {
       const bool has_flags = verdict == kVerdictForwarded || verdict == kVerdictRetrans;
       const uint32_t bits = role | ((has_flags && (flags & 2u)) ? 4u : 0u) | ((has_flags && (flags & 16u)) ? 8u : 0u);
       const uint64_t e = base + rank;
-      a.ev[e] = LatEvent{k0, k1, c, (uint32_t)((uint64_t)a.time_ns[i] % 1000000000ULL), bits};
+      a.ev[e] = LatEvent{k0, k1, c, seq0 + e, (uint32_t)((uint64_t)a.time_ns[i] % 1000000000ULL), bits};
       a.hash_in[e] = lat_hash(k0, k1);
       a.idx_in[e] = (uint32_t)e;
     }
@@ -202,8 +212,15 @@ __device__ __forceinline__ uint32_t lat_bucket(int64_t v) {
   return v >= 5 ? 10u : (uint32_t)(2 * v);
 }
 
+// kPass 0: each entry's life as event positions (delta[first] += 1, delta[gone] -= 1; no
+// other effect) for the capacity check.  kPass 1: the join's effects -- histograms,
+// no_response, the carry-out -- unless the capacity bound (lat_serial_kernel's batch).
+// An entry leaves at the reply that deletes it, or just before the first record event
+// whose clock passes its expiry (the cleaner evicts it then).
+template <int kPass>
 __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32_t enabled) {
   const uint64_t n = a.state[kLatEvents];
+  if (kPass == 1 && *a.max_live > (int64_t)a.limit) return;
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const unsigned long long h = a.hash_out[i];
@@ -211,7 +228,22 @@ __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32
   uint64_t j = i + 1;
   while (j < n && a.hash_out[j] == h) ++j;
   const unsigned long long clk_end = a.state[kLatClockEnd];
+  const uint64_t pend = a.state[kLatPending];
   unsigned long long *st = a.state;
+  // first record event (positions >= pend, clocks non-decreasing) whose clock passes `exp`
+  auto gone_at = [&](unsigned long long exp) {
+    uint64_t lo = pend, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (a.ev[mid].clock > exp) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  auto life = [&](uint64_t first, uint64_t gone) {  // kPass 0
+    atomicAdd(&a.delta[first], 1);
+    atomicAdd(&a.delta[gone], -1);
+  };
   // one pass per distinct exact key of the segment (a 64-bit hash collision is the only
   // way a segment holds two); events of a key in record order (stable sort)
   for (uint64_t p = i; p < j; ++p) {
@@ -224,9 +256,11 @@ __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32
     if (seen) continue;
     bool live = false, syn = false;
     unsigned long long expires = 0;
+    uint64_t first = 0, touch = 0;
     uint32_t nanos = 0;
     for (uint64_t q = p; q < j; ++q) {
-      const LatEvent e = a.ev[a.idx_out[q]];
+      const uint64_t pos = a.idx_out[q];
+      const LatEvent e = a.ev[pos];
       if (e.k0 != ep.k0 || e.k1 != ep.k1) continue;
       const uint32_t role = e.bits & 3u;
       if (role == kRoleCarry) {  // pending from an earlier batch: first in order
@@ -234,50 +268,195 @@ __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32
         expires = e.clock;
         nanos = e.nanos;
         syn = (e.bits >> 2) & 1u;
+        first = pos;
+        touch = e.seq;
         continue;
       }
       if (live && e.clock > expires) {  // the cleaner evicted it before this record
         live = false;
-        if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
+        if (kPass == 0) life(first, gone_at(expires));
+        else if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
       }
       if (role == kRoleReq) {
-        if (!live) {
+        if (!live) {  // Set
           live = true;
-          expires = e.clock + kLatTtlNs;
           nanos = e.nanos;
           syn = (e.bits >> 2) & 1u;
+          first = pos;
         }
+        expires = e.clock + kLatTtlNs;  // Set, or the Get hit's touch
+        touch = e.seq;
       } else if (live) {  // reply: latency of the first reply, then Delete
-        const int64_t d = (int64_t)e.nanos - (int64_t)nanos;
-        const int64_t ad = d < 0 ? -d : d;
-        const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
-        const uint32_t bk = lat_bucket(lat);
-        if (enabled & 1u) {
-          atomicAdd(&st[kLatHist + bk], 1ULL);
-          atomicAdd(&st[kLatHist + 11], 1ULL);
-          atomicAdd(&st[kLatHist + 12], (unsigned long long)lat);
-        }
-        if ((enabled & 2u) && syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
-          atomicAdd(&st[kLatHandshake + bk], 1ULL);
-          atomicAdd(&st[kLatHandshake + 11], 1ULL);
-          atomicAdd(&st[kLatHandshake + 12], (unsigned long long)lat);
+        if (kPass == 0) {
+          life(first, pos);
+        } else {
+          const int64_t d = (int64_t)e.nanos - (int64_t)nanos;
+          const int64_t ad = d < 0 ? -d : d;
+          const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
+          const uint32_t bk = lat_bucket(lat);
+          if (enabled & 1u) {
+            atomicAdd(&st[kLatHist + bk], 1ULL);
+            atomicAdd(&st[kLatHist + 11], 1ULL);
+            atomicAdd(&st[kLatHist + 12], (unsigned long long)lat);
+          }
+          if ((enabled & 2u) && syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
+            atomicAdd(&st[kLatHandshake + bk], 1ULL);
+            atomicAdd(&st[kLatHandshake + 11], 1ULL);
+            atomicAdd(&st[kLatHandshake + 12], (unsigned long long)lat);
+          }
         }
         live = false;
       }
     }
     if (!live) continue;
     if (clk_end > expires) {
-      if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
+      if (kPass == 0) life(first, gone_at(expires));
+      else if (enabled & 4u) atomicAdd(&st[kLatNoResponse], 1ULL);
+    } else if (kPass == 0) {
+      atomicAdd(&a.delta[first], 1);
     } else {
       const unsigned long long o = atomicAdd(&st[kLatCarryOut], 1ULL);
-      a.carry_out[o] = LatEvent{ep.k0, ep.k1, expires, nanos, kRoleCarry | (syn ? 4u : 0u)};
+      a.carry_out[o] = LatEvent{ep.k0, ep.k1, expires, touch, nanos, kRoleCarry | (syn ? 4u : 0u)};
     }
   }
 }
 
-__global__ void lat_finish_kernel(unsigned long long *st) {
+// The batch in event order when the capacity binds: the ttlcache itself, single-threaded
+// (every event depends on the live set the earlier ones left).  Items live in a pool, a
+// linear-probing table maps keys to them, and a queue of touches in order is the LRU
+// list (a record is stale once its item is touched again or freed): its front valid item
+// is the least recently touched, which is also the first to expire.
+__global__ __launch_bounds__(1024) void lat_serial_kernel(LatArgs a, uint32_t enabled) {
+  if (*a.max_live <= (int64_t)a.limit) return;
+  for (uint32_t k = threadIdx.x; k <= a.table_mask; k += blockDim.x) a.table[k] = 0u;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  unsigned long long *st = a.state;
+  const uint64_t n = st[kLatEvents], pend = st[kLatPending];
+  const uint32_t mask = a.table_mask;
+  uint32_t top = 0, nfree = 0;  // pool: never-used prefix, free stack
+  uint64_t qh = 0, qt = 0, live = 0;
+  auto home = [&](uint64_t k0, uint64_t k1) { return (uint32_t)lat_hash(k0, k1) & mask; };
+  auto find = [&](uint64_t k0, uint64_t k1) -> int64_t {  // table slot, or -1
+    for (uint32_t s = home(k0, k1);; s = (s + 1) & mask) {
+      const uint32_t v = a.table[s];
+      if (!v) return -1;
+      const LatEntry &x = a.pool[v - 1];
+      if (x.k0 == k0 && x.k1 == k1) return s;
+    }
+  };
+  auto erase = [&](uint32_t s) {  // backward-shift deletion, frees the item
+    const uint32_t idx = a.table[s] - 1;
+    a.pool[idx].seq = ~0ULL;
+    a.free_idx[nfree++] = idx;
+    for (uint32_t t = (s + 1) & mask;; t = (t + 1) & mask) {
+      const uint32_t v = a.table[t];
+      if (!v) break;
+      const uint32_t hm = home(a.pool[v - 1].k0, a.pool[v - 1].k1);
+      // the item at t may move to s unless its home lies cyclically in (s, t]
+      const bool stay = s <= t ? (hm > s && hm <= t) : (hm > s || hm <= t);
+      if (!stay) {
+        a.table[s] = v;
+        s = t;
+      }
+    }
+    a.table[s] = 0u;
+    --live;
+  };
+  auto insert = [&](const LatEntry &x) {
+    const uint32_t idx = nfree ? a.free_idx[--nfree] : top++;
+    a.pool[idx] = x;
+    uint32_t s = home(x.k0, x.k1);
+    while (a.table[s]) s = (s + 1) & mask;
+    a.table[s] = idx + 1;
+    a.queue[qt++] = LatTouch{x.seq, idx, 0u};
+    ++live;
+  };
+  // the front valid item (skipping stale records), or ~0
+  auto front = [&]() -> uint32_t {
+    while (qh < qt) {
+      const LatTouch r = a.queue[qh];
+      if (a.pool[r.idx].seq == r.seq) return r.idx;
+      ++qh;
+    }
+    return ~0u;
+  };
+  for (uint64_t k = 0; k < pend; ++k) {  // carried items, least recently touched first
+    const LatEvent c = a.ev[a.carry_order[k]];
+    insert(LatEntry{c.k0, c.k1, c.clock, c.seq, c.nanos, (c.bits >> 2) & 1u});
+  }
+  for (uint64_t pos = pend; pos < n; ++pos) {
+    const LatEvent e = a.ev[pos];
+    for (uint32_t f = front(); f != ~0u && e.clock > a.pool[f].expires; f = front()) {
+      erase((uint32_t)find(a.pool[f].k0, a.pool[f].k1));  // expired before this record
+      ++qh;
+      if (enabled & 4u) st[kLatNoResponse] += 1;
+    }
+    const int64_t s = find(e.k0, e.k1);
+    if ((e.bits & 3u) == kRoleReq) {
+      if (s >= 0) {  // Get hit: touched
+        const uint32_t idx = a.table[s] - 1;
+        a.pool[idx].expires = e.clock + kLatTtlNs;
+        a.pool[idx].seq = e.seq;
+        a.queue[qt++] = LatTouch{e.seq, idx, 0u};
+        continue;
+      }
+      if (live >= a.limit) {  // Set at capacity: the LRU back goes, uncounted
+        const uint32_t f = front();
+        erase((uint32_t)find(a.pool[f].k0, a.pool[f].k1));
+        ++qh;
+        st[kLatCapEvictions] += 1;
+      }
+      insert(LatEntry{e.k0, e.k1, e.clock + kLatTtlNs, e.seq, e.nanos, (e.bits >> 2) & 1u});
+    } else if (s >= 0) {  // reply: latency, then Delete
+      const LatEntry x = a.pool[a.table[s] - 1];
+      const int64_t d = (int64_t)e.nanos - (int64_t)x.nanos;
+      const int64_t ad = d < 0 ? -d : d;
+      const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
+      const uint32_t bk = lat_bucket(lat);
+      if (enabled & 1u) {
+        st[kLatHist + bk] += 1;
+        st[kLatHist + 11] += 1;
+        st[kLatHist + 12] += (unsigned long long)lat;
+      }
+      if ((enabled & 2u) && x.syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
+        st[kLatHandshake + bk] += 1;
+        st[kLatHandshake + 11] += 1;
+        st[kLatHandshake + 12] += (unsigned long long)lat;
+      }
+      erase((uint32_t)s);
+    }
+  }
+  // batch end: expired items count, the rest carry over in LRU order
+  const unsigned long long clk_end = st[kLatClockEnd];
+  uint64_t out = 0;
+  for (uint32_t f = front(); f != ~0u; f = front()) {
+    const LatEntry x = a.pool[f];
+    if (clk_end > x.expires) {
+      if (enabled & 4u) st[kLatNoResponse] += 1;
+    } else {
+      a.carry_out[out++] = LatEvent{x.k0, x.k1, x.expires, x.seq, x.nanos, kRoleCarry | (x.syn ? 4u : 0u)};
+    }
+    a.pool[f].seq = ~0ULL;
+    ++qh;
+  }
+  st[kLatCarryOut] = out;
+  st[kLatCapBatches] += 1;
+}
+
+__global__ void lat_finish_kernel(unsigned long long *st, const int32_t *max_live, uint64_t limit) {
+  st[kLatSeqBase] += st[kLatEvents] - st[kLatPending];
   st[kLatClock] = st[kLatClockEnd];
   st[kLatPending] = st[kLatCarryOut];
+  const unsigned long long peak = max_live ? (unsigned long long)min((int64_t)*max_live, (int64_t)limit) : 0ULL;
+  st[kLatPeakLive] = max(st[kLatPeakLive], max(peak, st[kLatPending]));
+}
+
+__global__ void lat_order_init_kernel(const LatEvent *carry, size_t n, unsigned long long *keys, uint32_t *vals) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    keys[e] = carry[e].seq;
+    vals[e] = (uint32_t)e;
+  }
 }
 
 // ---- host side ----------------------------------------------------------------------
@@ -290,10 +469,31 @@ hipError_t launch_latency_front(const LatArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Temporary storage for the pass's rocprim calls over n events: the hash sort, the
+// carried entries' LRU sort, the live-count scan and its maximum (one buffer, the largest).
 hipError_t latency_sort_bytes(size_t n, size_t *bytes) {
-  return rocprim::radix_sort_pairs(nullptr, *bytes, (const unsigned long long *)nullptr,
-                                   (unsigned long long *)nullptr, (const uint32_t *)nullptr,
-                                   (uint32_t *)nullptr, n, 0, 64, (hipStream_t)0);
+  size_t a = 0, b = 0, c = 0;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, a, (const unsigned long long *)nullptr,
+                                           (unsigned long long *)nullptr, (const uint32_t *)nullptr,
+                                           (uint32_t *)nullptr, n, 0, 64, (hipStream_t)0);
+  if (e != hipSuccess) return e;
+  if ((e = rocprim::inclusive_scan(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, n + 1,
+                                   rocprim::plus<int32_t>(), (hipStream_t)0)) != hipSuccess)
+    return e;
+  if ((e = rocprim::reduce(nullptr, c, (const int32_t *)nullptr, (int32_t *)nullptr, (int32_t)0, n + 1,
+                           rocprim::maximum<int32_t>(), (hipStream_t)0)) != hipSuccess)
+    return e;
+  *bytes = std::max(a, std::max(b, c));
+  return hipSuccess;
+}
+
+hipError_t latency_carry_order(const LatEvent *carry, size_t n, unsigned long long *keys, uint32_t *vals,
+                               void *tmp, size_t tmp_bytes, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(lat_order_init_kernel, dim3((uint32_t)std::min<size_t>(1024, (n + 255) / 256)), dim3(256),
+                     0, st, carry, n, keys, vals);
+  size_t tb = tmp_bytes;
+  return rocprim::radix_sort_pairs(tmp, tb, keys, keys + n, vals, vals + n, n, 0, 64, st);
 }
 
 hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
@@ -304,10 +504,24 @@ hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, siz
     if ((e = rocprim::radix_sort_pairs(tmp, tb, a.hash_in, a.hash_out, a.idx_in, a.idx_out, n_events, 0, 64,
                                        st)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(lat_walk_kernel, dim3((uint32_t)((n_events + kLatThreads - 1) / kLatThreads)),
-                       dim3(kLatThreads), 0, st, a, enabled);
+    const dim3 grid((uint32_t)((n_events + kLatThreads - 1) / kLatThreads));
+    // capacity check: entry lives as +1 / -1 at event positions, the live count before
+    // each event (prefix sums) and its maximum
+    if ((e = hipMemsetAsync(a.delta, 0, (n_events + 1) * sizeof(int32_t), st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lat_walk_kernel<0>, grid, dim3(kLatThreads), 0, st, a, enabled);
+    tb = tmp_bytes;
+    if ((e = rocprim::inclusive_scan(tmp, tb, a.delta, a.live, n_events + 1, rocprim::plus<int32_t>(), st)) !=
+        hipSuccess)
+      return e;
+    tb = tmp_bytes;
+    if ((e = rocprim::reduce(tmp, tb, a.live, a.max_live, (int32_t)0, n_events + 1, rocprim::maximum<int32_t>(),
+                             st)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(lat_walk_kernel<1>, grid, dim3(kLatThreads), 0, st, a, enabled);
+    hipLaunchKernelGGL(lat_serial_kernel, dim3(1), dim3(1024), 0, st, a, enabled);
   }
-  hipLaunchKernelGGL(lat_finish_kernel, dim3(1), dim3(1), 0, st, a.state);
+  hipLaunchKernelGGL(lat_finish_kernel, dim3(1), dim3(1), 0, st, a.state, n_events ? a.max_live : nullptr,
+                     a.limit);
   return hipGetLastError();
 }
 

@@ -134,18 +134,38 @@ hipError_t launch_hubble(const HubbleArgs &a, uint32_t n_cu, hipStream_t st);
 struct LatEvent {
   uint64_t k0, k1;   // request-oriented key: src | dst << 32, sport | dport << 16 | id << 32
   uint64_t clock;    // record clock (carried entry: its expiry)
+  uint64_t seq;      // event number across batches (carried entry: its last touch) -- the
+                     // ttlcache's LRU order, needed when the capacity binds
   uint32_t nanos;    // Time.Nanos
   uint32_t bits;     // role 1 request / 2 reply / 3 carried | SYN << 2 | ACK << 3
 };
+// One live request of the sequential (capacity-bound) pass: the ttlcache item.
+struct LatEntry {
+  uint64_t k0, k1;
+  uint64_t expires;
+  uint64_t seq;      // last touch (~0: free)
+  uint32_t nanos;
+  uint32_t syn;
+};
+struct LatTouch {  // LRU / expiry queue record (stale once its entry is touched again or freed)
+  uint64_t seq;
+  uint32_t idx;
+  uint32_t pad;
+};
+constexpr uint64_t kLatLimit = 100000;  // ttlcache.WithCapacity(LIMIT), latency.go:35,120-121
 constexpr uint32_t kLatMaxApi = 64;
 constexpr uint32_t kLatMaxUnits = 1u << 16;  // front-end units (one wave's contiguous rows each)
 constexpr uint64_t kLatTtlNs = 500000000ULL;  // latency.go:34
 // state words (u64): clock, pending carried entries, scratch, histograms, no_response
 enum : uint32_t {
   kLatClock = 0, kLatPending = 1, kLatCarryOut = 2, kLatClockEnd = 3, kLatEvents = 4,
+  kLatSeqBase = 5,     // events numbered so far (LatEvent.seq of this batch's first event)
+  kLatPeakLive = 6,    // most live requests at any event (the batch's max of the live count)
+  kLatCapBatches = 7,  // batches the capacity bound (run by the sequential pass)
   kLatHist = 8,        // 11 buckets (le 0, 0.5 .. 4.5, +Inf), count, sum (i64)
   kLatHandshake = 24,  // same layout
   kLatNoResponse = 40,
+  kLatCapEvictions = 41,  // requests evicted by the capacity (EvictionReasonCapacityReached)
   kLatStateWords = 48
 };
 struct LatArgs {
@@ -166,9 +186,22 @@ struct LatArgs {
   uint32_t *idx_in, *idx_out;
   const LatEvent *carry_in;
   LatEvent *carry_out;
+  // capacity (ttlcache.WithCapacity): live-count check and the sequential pass
+  uint64_t limit;
+  int32_t *delta, *live;            // [n_events + 1]: +1 / -1 per entry life, its prefix sums
+  int32_t *max_live;                // max of live[] (device scalar)
+  const uint32_t *carry_order;      // carried entries' positions in LRU (seq) order
+  LatEntry *pool;                   // [limit] ttlcache items
+  uint32_t *table;                  // [table_mask + 1] pool index + 1 (0: empty), linear probing
+  uint32_t table_mask;
+  uint32_t *free_idx;               // [limit] free-list stack
+  LatTouch *queue;                  // [n_events] touches in LRU order
 };
 hipError_t launch_latency_front(const LatArgs &a, hipStream_t st);
 hipError_t latency_sort_bytes(size_t n, size_t *bytes);
+// The carried entries' LRU order (by last touch): keys / values [2][n] each.
+hipError_t latency_carry_order(const LatEvent *carry, size_t n, unsigned long long *keys, uint32_t *vals,
+                               void *tmp, size_t tmp_bytes, hipStream_t st);
 hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
                                uint32_t enabled, hipStream_t st);
 

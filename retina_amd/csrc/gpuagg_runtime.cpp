@@ -224,6 +224,17 @@ struct gpuagg_ctx {
   uint64_t lat_carry_bound = 0;  // >= entries currently carried
   void *d_lat_tmp = nullptr;
   size_t lat_tmp_alloc = 0;
+  // capacity (ttlcache LIMIT): live-count check buffers and the sequential pass's ttlcache
+  int32_t *d_lat_delta = nullptr;   // [2][lat_ev_alloc + 1]: entry lives, live counts
+  int32_t *d_lat_max_live = nullptr;
+  LatEntry *d_lat_pool = nullptr;   // [limit]
+  uint32_t *d_lat_table = nullptr;  // [lat_table_mask + 1]
+  uint32_t lat_table_mask = 0;
+  uint32_t *d_lat_free = nullptr;   // [limit]
+  LatTouch *d_lat_queue = nullptr;  // [lat_ev_alloc]
+  unsigned long long *d_lat_okeys = nullptr;  // carried entries' LRU sort: [2][lat_carry_alloc]
+  uint32_t *d_lat_ovals = nullptr;
+  size_t lat_order_alloc = 0;
   uint64_t *h_lat_n = nullptr;   // pinned: state words [kLatPending, kLatEvents] of the batch
   uint64_t lat_peak_pending = 0; // most requests carried into a batch since the reconcile
   int64_t time_offset = 0;       // ktime.MonotonicOffset added to decoded record times
@@ -1001,6 +1012,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.api = c->d_api;
     a.n_api = (uint32_t)c->api_ips.size();
     a.state = c->d_lat;
+    a.limit = c->cfg.latency_limit ? c->cfg.latency_limit : kLatLimit;
     c->lat_peak_pending = std::max<uint64_t>(c->lat_peak_pending, c->d_lat[kLatPending]);
     c->cpu->latency(a, c->lat_enabled);
     return GPUAGG_OK;
@@ -1044,12 +1056,33 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     dev_free(c, c->d_lat_ev);
     dev_free(c, c->d_lat_hash);
     dev_free(c, c->d_lat_idx);
+    dev_free(c, c->d_lat_delta);
+    dev_free(c, c->d_lat_queue);
     c->lat_ev_alloc = 0;
     if ((rc = dev_alloc(c, &c->d_lat_ev, cap)) || (rc = dev_alloc(c, &c->d_lat_hash, 2 * cap)) ||
-        (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)))
+        (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)) || (rc = dev_alloc(c, &c->d_lat_delta, 2 * (cap + 1))) ||
+        (rc = dev_alloc(c, &c->d_lat_queue, cap)))
       return rc;
     c->lat_ev_alloc = cap;
   }
+  // the sequential pass's ttlcache: `limit` items, a table at most half full
+  a.limit = c->cfg.latency_limit ? c->cfg.latency_limit : kLatLimit;
+  if (!c->d_lat_pool) {
+    uint32_t tsize = 1024;
+    while (tsize < 2 * a.limit) tsize <<= 1;
+    if ((rc = dev_alloc(c, &c->d_lat_pool, a.limit)) || (rc = dev_alloc(c, &c->d_lat_table, tsize)) ||
+        (rc = dev_alloc(c, &c->d_lat_free, a.limit)) || (rc = dev_alloc(c, &c->d_lat_max_live, 1)))
+      return rc;
+    c->lat_table_mask = tsize - 1;
+  }
+  a.delta = c->d_lat_delta;
+  a.live = c->d_lat_delta + c->lat_ev_alloc + 1;
+  a.max_live = c->d_lat_max_live;
+  a.pool = c->d_lat_pool;
+  a.table = c->d_lat_table;
+  a.table_mask = c->lat_table_mask;
+  a.free_idx = c->d_lat_free;
+  a.queue = c->d_lat_queue;
   a.ev = c->d_lat_ev;
   a.hash_in = c->d_lat_hash;
   a.hash_out = c->d_lat_hash + c->lat_ev_alloc;
@@ -1085,6 +1118,21 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     c->lat_tmp_alloc = 0;
     HIPCHK(c, hipMalloc(&c->d_lat_tmp, tb));
     c->lat_tmp_alloc = tb;
+  }
+  // the carried entries' LRU order (by last touch), read by the sequential pass if the
+  // capacity binds; they sit at event positions [0, pending)
+  const uint64_t pend = c->h_lat_n[0];
+  if (pend) {
+    if (pend > c->lat_order_alloc) {
+      dev_free(c, c->d_lat_okeys);
+      dev_free(c, c->d_lat_ovals);
+      c->lat_order_alloc = 0;
+      if ((rc = dev_alloc(c, &c->d_lat_okeys, 2 * pend)) || (rc = dev_alloc(c, &c->d_lat_ovals, 2 * pend))) return rc;
+      c->lat_order_alloc = pend;
+    }
+    HIPCHK(c, latency_carry_order(a.ev, pend, c->d_lat_okeys, c->d_lat_ovals, c->d_lat_tmp, c->lat_tmp_alloc,
+                                  c->stream));
+    a.carry_order = c->d_lat_ovals + pend;
   }
   HIPCHK(c, launch_latency_back(a, ne, c->d_lat_tmp, c->lat_tmp_alloc, c->lat_enabled, c->stream));
   c->lat_carry_cur ^= 1;
@@ -1518,6 +1566,7 @@ int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out) {
   if (cfg->cms_depth && (cfg->cms_width_log2 < 4 || cfg->cms_width_log2 > 28 || cfg->cms_depth > 16))
     return GPUAGG_EINVAL;
   if (cfg->hll_precision && (cfg->hll_precision < 4 || cfg->hll_precision > 18)) return GPUAGG_EINVAL;
+  if (cfg->latency_limit > (1u << 26)) return GPUAGG_EINVAL;
   if (cfg->flags & GPUAGG_FLAG_CPU_BACKEND) {
     // host threads instead of a device: the node's CPU share (GPUAGG_CPU_THREADS, else the
     // hardware threads, at most 64)
@@ -1603,6 +1652,14 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c, c->d_lat_ev);
   dev_free(c, c->d_lat_hash);
   dev_free(c, c->d_lat_idx);
+  dev_free(c, c->d_lat_delta);
+  dev_free(c, c->d_lat_queue);
+  dev_free(c, c->d_lat_max_live);
+  dev_free(c, c->d_lat_pool);
+  dev_free(c, c->d_lat_table);
+  dev_free(c, c->d_lat_free);
+  dev_free(c, c->d_lat_okeys);
+  dev_free(c, c->d_lat_ovals);
   dev_free(c, c->d_lat_carry[0]);
   dev_free(c, c->d_lat_carry[1]);
   if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
@@ -3360,6 +3417,10 @@ int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
   out->no_response = w[kLatNoResponse];
   out->pending = w[kLatPending];
   out->peak_pending = std::max<uint64_t>(c->lat_peak_pending, w[kLatPending]);
+  out->peak_live = w[kLatPeakLive];
+  out->capacity_evictions = w[kLatCapEvictions];
+  out->capacity_batches = w[kLatCapBatches];
+  out->limit = c->cfg.latency_limit ? c->cfg.latency_limit : kLatLimit;
   return GPUAGG_OK;
 }
 

@@ -289,7 +289,9 @@ class GpuAgg:
                 "latency_count": st.latency_count, "latency_sum": st.latency_sum,
                 "handshake_buckets": list(st.handshake_buckets), "handshake_count": st.handshake_count,
                 "handshake_sum": st.handshake_sum, "no_response": st.no_response, "pending": st.pending,
-                "peak_pending": st.peak_pending}
+                "peak_pending": st.peak_pending, "peak_live": st.peak_live,
+                "capacity_evictions": st.capacity_evictions, "capacity_batches": st.capacity_batches,
+                "limit": st.limit}
 
     # -- enriched-flow emission, standard mode (enrich_kernel) --------------------------
     def enrich_device(self, cols: "_abi.Columns", n: int, src_slot, dst_slot) -> None:

@@ -428,3 +428,47 @@ def gen_latency_records(n_conn: int, pods: Pods, api_ips: Sequence[int], seed: i
     tcp_id = np.array([r[7] for r in rows], u)
     meta = pack_meta(np.full(n, 6, u), np.full(n, 1, u), np.where(obs == 3, 2, 1), 0, flags, obs=obs)
     return Records(src, dst, np.full(n, 100, u), meta, ports, np.zeros(n, u), [], tcp_id, time_ns)
+
+
+def gen_latency_burst(n_req: int, api_ips: Sequence[int], seed: int = 0, spacing_ns: int = 1000,
+                      reply_frac: float = 0.5, touch_frac: float = 0.05, background: int = 0) -> Records:
+    """A burst of node -> apiserver requests outstanding at once (the ttlcache capacity,
+    latency.go:35,120-121): n_req TO_NETWORK requests with distinct keys `spacing_ns`
+    apart, a `reply_frac` share answered 0.2-300 ms later (early requests of a burst past
+    the capacity were evicted, so their replies find nothing), and a `touch_frac` share
+    repeated 400 ms later (same TSval: the Get hit touches the entry) and answered 650 ms
+    after the first packet -- alive only through the touch.  Time-ordered records."""
+    rng = np.random.Generator(np.random.PCG64(seed + 9100))
+    u = np.uint32
+    apis = np.asarray(api_ips, u)
+    t0 = 1_700_000_000_000_000_000 + int(rng.integers(0, 10**9))
+    ACK, PSH, SYN = 16, 8, 2
+    rows = []
+    node = np.array([ip_le(10, 241, i >> 8, i & 255) for i in range(1, 65)], u)
+    for i in range(n_req):
+        t = t0 + i * spacing_ns
+        src, dst = int(node[i % len(node)]), int(apis[i % len(apis)])
+        sport, ts = 1024 + (i * 7919) % 60000, 1 + i
+        fl = SYN if i % 3 == 0 else ACK | PSH
+        rows.append((t, src, dst, sport, 443, 3, fl, ts))
+        x = rng.random()
+        if x < touch_frac:
+            rows.append((t + 400_000_000, src, dst, sport, 443, 3, fl, ts))
+            rows.append((t + 650_000_000, dst, src, 443, sport, 2, SYN | ACK if fl == SYN else ACK, ts))
+        elif x < touch_frac + reply_frac:
+            rows.append((t + int(rng.integers(200_000, 300_000_000)), dst, src, 443, sport, 2,
+                         SYN | ACK if fl == SYN else ACK, ts))
+    tmax = max(r[0] for r in rows)
+    for _ in range(background):
+        rows.append((int(rng.integers(t0, tmax)), int(node[0]), int(node[1]), 5000, 80, 3, ACK, 0))
+    rows.sort(key=lambda r: r[0])
+    n = len(rows)
+    time_ns = np.array([r[0] for r in rows], np.uint64)
+    src = np.array([r[1] for r in rows], u)
+    dst = np.array([r[2] for r in rows], u)
+    ports = np.array([r[3] | (r[4] << 16) for r in rows], u)
+    obs = np.array([r[5] for r in rows], u)
+    flags = np.array([r[6] for r in rows], u)
+    tcp_id = np.array([r[7] for r in rows], u)
+    meta = pack_meta(np.full(n, 6, u), np.full(n, 1, u), np.where(obs == 3, 2, 1), 0, flags, obs=obs)
+    return Records(src, dst, np.full(n, 100, u), meta, ports, np.zeros(n, u), [], tcp_id, time_ns)

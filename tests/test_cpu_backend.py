@@ -181,3 +181,39 @@ def test_merge_and_enrich():
     for i in range(1000):
         obj = cache.get_obj_by_ip(O.int2ip(int(recs.src_ip[i])))
         assert (s[i] >= 0) == isinstance(obj, O.RetinaEndpoint)
+
+
+@pytest.mark.parametrize("limit,chunks", [(300, 1), (300, 4), (100_000, 1)])
+def test_latency_capacity_and_touch(limit, chunks):
+    """The ttlcache's capacity (latency.go LIMIT, here also a small gpuagg_config
+    latency_limit) and its touch on a Get hit, on the CPU backend against the oracle:
+    a burst keeps more requests live than the limit (the least recently touched are
+    evicted, uncounted), repeated requests are kept alive by the touch; across batches
+    the carried entries keep their LRU order."""
+    from .latency_helpers import as_state, oracle_latency
+    api = [W.ip_le(10, 255, 0, 1), W.ip_le(10, 255, 0, 2)]
+    sp = [{"metric_name": "node_apiserver_latency"}, {"metric_name": "node_apiserver_handshake_latency"},
+          {"metric_name": "node_apiserver_no_response"}]
+    n_req = 1_200 if limit < 1000 else 130_000
+    recs = W.gen_latency_burst(n_req, api, seed=limit + chunks, spacing_ns=100_000 if limit < 1000 else 1_000,
+                               background=500)
+    m = oracle_latency(recs, api, limit=limit)
+    want = as_state(m, capacity=True)
+    assert want["capacity_evictions"] > 0 and want["peak_live"] == limit
+    pods = W.make_pods(20, seed=3)
+    g = make_engine(pods, sp, False, flags=CPU, latency_limit=0 if limit == 100_000 else limit)
+    try:
+        g.set_apiserver_ips(api)
+        n = len(recs.src_ip)
+        hb = g.alloc_batch(n)
+        bounds = np.linspace(0, n, chunks + 1).astype(int)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            hb.fill(recs, int(a), int(b - a))
+            g.submit(hb, int(b - a))
+        st = g.latency_state()
+    finally:
+        g.close()
+    assert {k: st[k] for k in want} == want
+    assert st["limit"] == limit
+    # the touch: without it the late replies (650 ms after their first request) find nothing
+    assert want["latency_buckets"][10] > 0

@@ -182,3 +182,54 @@ def test_apiserver_and_ipcache_before_endpoints(gpu_device):
     pos = {ip: i for i, ip in enumerate(ips)}
     exp = np.array([1000 + pos[int(s)] if int(s) in pos else 2 for s in recs.src_ip], np.uint32)
     assert np.array_equal(sid, exp)
+
+
+@pytest.mark.parametrize("limit,chunks", [(300, 1), (300, 5), (100_000, 1), (100_000, 3)],
+                         ids=["small-1", "small-5", "LIMIT-1", "LIMIT-3"])
+def test_capacity_and_touch_match_oracle(gpu_device, limit, chunks):
+    """The ttlcache capacity (latency.go LIMIT = 100000, and a small latency_limit) and
+    its touch on a Get hit: a burst keeps more requests live than the limit, so the
+    batches where the capacity binds run the sequential pass (least recently touched
+    evicted, uncounted) and the others the parallel walk; exact against the oracle across
+    batches (carried entries keep their LRU order)."""
+    from retina_amd import GpuAgg
+    from .latency_helpers import as_state
+    n_req = 1_200 if limit < 1000 else 130_000
+    recs = W.gen_latency_burst(n_req, API, seed=limit + chunks, spacing_ns=100_000 if limit < 1000 else 1_000,
+                               background=2_000)
+    m = oracle_latency(recs, API, limit=limit)
+    want = as_state(m, capacity=True)
+    assert want["capacity_evictions"] > 0 and want["peak_live"] == limit
+    pods = W.make_pods(50, seed=3)
+    g = make_engine(pods, SPEC, False, gpu_device, latency_limit=0 if limit == 100_000 else limit)
+    try:
+        g.set_apiserver_ips(API)
+        ts = _dev(recs, gpu_device)
+        n = len(recs.src_ip)
+        bounds = np.linspace(0, n, chunks + 1).astype(int)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            g.submit_device(GpuAgg.device_columns(*[x[a:] for x in ts]), int(b - a))
+        st = g.latency_state()
+    finally:
+        g.close()
+    assert {k: st[k] for k in want} == want
+    assert st["limit"] == limit and st["capacity_batches"] >= 1
+    assert want["latency_buckets"][10] > 0  # replies kept alive by the touch
+
+
+def test_touch_without_capacity(gpu_device):
+    """Below the capacity (the parallel walk): repeated requests touch their entry, so a
+    reply 650 ms after the first packet is observed, as the oracle's ttlcache does."""
+    from retina_amd import GpuAgg
+    recs = W.gen_latency_burst(3_000, API, seed=5, spacing_ns=50_000, touch_frac=0.2, background=1_000)
+    want = as_state(oracle_latency(recs, API), capacity=True)
+    assert want["capacity_evictions"] == 0 and want["latency_buckets"][10] > 0
+    pods = W.make_pods(50, seed=3)
+    g = _engine(pods, gpu_device)
+    try:
+        g.submit_device(GpuAgg.device_columns(*_dev(recs, gpu_device)), len(recs.src_ip))
+        st = g.latency_state()
+    finally:
+        g.close()
+    assert {k: st[k] for k in want} == want
+    assert st["capacity_batches"] == 0
