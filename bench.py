@@ -193,6 +193,47 @@ def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
             "note": "pinned host batches through gpuagg_submit (PCIe H2D included; not `value`)"}
 
 
+def host_fed_raw_rate(g, pods, seed: int, batches: int = 16, batch: int = GO_BATCH):
+    """The Go plugin's raw path (gpuagg_linux.go Start -> submitRaw): raw 72-byte
+    packetparser samples (conntrack.c:34-49) handed to the library feed in 2^16-sample
+    pieces (gpuagg_raw_feed_put: shard by the 5-tuple, copy into the device's pinned
+    staging, submit each full 2^20-record staging -- H2D DMA, on-GPU decode, aggregation),
+    then a flush and sync.  Also the host-side sharding rate over 8 devices
+    (gpuagg_shard_raw), the per-sample cost the plugin pays before any copy."""
+    from retina_amd import RawFeed, _abi
+    from retina_amd import workloads as W
+    raw = W.gen_raw_packets(batch, pods, seed=seed)  # one Go batch of samples, resubmitted
+    piece = 1 << 16
+    feed = RawFeed([g], _abi.RAW_PACKET, capacity=batch)
+    try:
+        for a in range(0, batch, piece):  # warm-up: staging and device buffers
+            feed.put(raw[a * 72:(a + piece) * 72])
+        feed.flush()
+        g.sync()
+        t0 = time.perf_counter()
+        for _ in range(batches):
+            for a in range(0, batch, piece):
+                feed.put(raw[a * 72:(a + piece) * 72])
+        feed.flush()
+        g.sync()
+        dt = time.perf_counter() - t0
+    finally:
+        feed.close()
+    shards = np.zeros(batch, np.uint32)
+    t1 = time.perf_counter()
+    for _ in range(4):
+        rc = g.lib.gpuagg_shard_raw(_abi.RAW_PACKET, raw.ctypes.data_as(C.c_void_p), batch, 8,
+                                    shards.ctypes.data_as(_abi.u32p))
+        if rc != 0:
+            raise RuntimeError("gpuagg_shard_raw: %d" % rc)
+    shard_rate = 4 * batch / (time.perf_counter() - t1)
+    return {"value": batches * batch / dt, "unit": "records/s", "batch_records": batch, "batches": batches,
+            "piece_records": piece, "record_bytes": 72, "shard_rate_8_devices": shard_rate,
+            "note": "raw packetparser samples through gpuagg_raw_feed_put (pinned staging, H2D DMA, on-GPU "
+                    "decode + aggregation) -- the Go plugin's real raw path; PCIe included, not `value`; "
+                    "shard_rate_8_devices = gpuagg_shard_raw samples/s on one host thread"}
+
+
 def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, launches: int = 100,
                         batch: int = GO_BATCH):
     """Device-resident launches of the Go plugin's batch size (GO_BATCH records each): the
@@ -409,6 +450,7 @@ def main():
         result["production"] = production_geometry(g, cols, n, bpr, stats["kernel_ms"] / max(1, stats["kernel_launches"]))
     if rank == 0 and world == 1 and not args.no_host_fed:
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
+        result["host_fed_raw"] = host_fed_raw_rate(g, pods, cfg["seed"] + 17)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         go_s, tu_s = (400_000, 4_000_000) if args.config == "c5" else (args.cpu_sample // 8, args.cpu_sample)
         result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s,

@@ -145,6 +145,9 @@ struct gpuagg_result {
   // families rendered outside `series` (the latency histograms / no_response counter):
   // name -> exposition text block
   std::map<std::string, std::string> extra_text;
+  // gpuagg_result_render_text's output, rendered once (callers size, then fill)
+  mutable std::string text;
+  mutable bool text_done = false;
 };
 
 struct gpuagg_ctx {
@@ -2758,6 +2761,39 @@ namespace {
 // decimal digits d1.d2..dn x 10^x that round-trip, in %e form (exponent of at least two
 // digits) when x < -4 or x >= 6 -- Go's fmtG uses precision 6 for that choice when the
 // digits are the shortest (strconv/ftoa.go) -- else in %f form.
+std::string go_float_g(double v);
+
+// go_float_g of an exact integer count: below 2^53 every integer is a double of its own
+// and a decimal with fewer significant digits is another integer, so the shortest
+// round-trip digits are the integer's, trailing zeros dropped (no probing).
+void go_float_u64_into(std::string &out, uint64_t v) {
+  if (v > (1ULL << 53)) {
+    out += go_float_g((double)v);
+    return;
+  }
+  char d[24];
+  int n = 0;
+  do {
+    d[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  const int x = n - 1;  // decimal exponent; digits most significant first: d[n-1] .. d[0]
+  if (x < 6) {          // Go 'g', shortest: %e only from exponent 6 (ftoa.go eprec = 6)
+    for (int k = n - 1; k >= 0; --k) out += d[k];
+    return;
+  }
+  int lo = 0;
+  while (lo < n - 1 && d[lo] == '0') ++lo;  // trailing zeros
+  out += d[n - 1];
+  if (n - 1 > lo) {
+    out += '.';
+    for (int k = n - 2; k >= lo; --k) out += d[k];
+  }
+  char e[8];
+  snprintf(e, sizeof e, "e+%02d", x);
+  out += e;
+}
+
 std::string go_float_g(double v) {
   if (v == 0) return "0";
   char buf[64];
@@ -2845,16 +2881,25 @@ void escape_into(std::string &out, const std::string &s, bool quote) {  // expfm
 
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
   if (!r || !len) return GPUAGG_EINVAL;
+  if (r->text_done) {
+    *len = r->text.size();
+    if (!buf) return GPUAGG_OK;
+    if (cap < r->text.size() + 1) return GPUAGG_ECAPACITY;
+    memcpy(buf, r->text.c_str(), r->text.size() + 1);
+    return GPUAGG_OK;
+  }
   // family name -> series indices; label pairs sorted by name (client_golang keeps a
   // metric's label pairs sorted), series sorted by those values (MetricSorter)
   std::map<std::string, std::vector<size_t>> fam;
   for (size_t i = 0; i < r->series.size(); ++i) fam[r->series[i].metric].push_back(i);
-  std::vector<std::vector<std::pair<std::string, std::string>>> pairs(r->series.size());
+  // (no string copies: pointers into the series)
+  std::vector<std::vector<std::pair<const std::string *, const std::string *>>> pairs(r->series.size());
   for (size_t i = 0; i < r->series.size(); ++i) {
     const Series &se = r->series[i];
-    for (size_t k = 0; k < se.names.size(); ++k) pairs[i].emplace_back(se.names[k], se.values[k]);
+    pairs[i].reserve(se.names.size());
+    for (size_t k = 0; k < se.names.size(); ++k) pairs[i].emplace_back(&se.names[k], &se.values[k]);
     std::stable_sort(pairs[i].begin(), pairs[i].end(),
-                     [](const auto &a, const auto &b) { return a.first < b.first; });
+                     [](const auto &a, const auto &b) { return *a.first < *b.first; });
   }
   std::map<std::string, std::string> blocks = r->extra_text;  // family name -> text
   for (auto &kv : fam) {
@@ -2862,8 +2907,10 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
     auto &idx = kv.second;
     std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
       const auto &pa = pairs[a], &pb = pairs[b];
-      for (size_t k = 0; k < pa.size() && k < pb.size(); ++k)
-        if (pa[k].second != pb[k].second) return pa[k].second < pb[k].second;
+      for (size_t k = 0; k < pa.size() && k < pb.size(); ++k) {
+        const int c = pa[k].second->compare(*pb[k].second);
+        if (c) return c < 0;
+      }
       return false;
     });
     const Series &first = r->series[idx[0]];
@@ -2876,19 +2923,25 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
         out += '{';
         for (size_t k = 0; k < pairs[i].size(); ++k) {
           if (k) out += ',';
-          out += pairs[i][k].first + "=\"";
-          escape_into(out, pairs[i][k].second, true);
+          out += *pairs[i][k].first;
+          out += "=\"";
+          escape_into(out, *pairs[i][k].second, true);
           out += '"';
         }
         out += '}';
       }
       out += ' ';
-      out += go_float_g((double)r->series[i].value);
+      go_float_u64_into(out, r->series[i].value);
       out += '\n';
     }
   }
-  std::string out;
+  std::string &out = r->text;
+  out.clear();
+  size_t total = 0;
+  for (auto &kv : blocks) total += kv.second.size();
+  out.reserve(total);
   for (auto &kv : blocks) out += kv.second;  // families sorted by name (expfmt)
+  r->text_done = true;
   *len = out.size();
   if (!buf) return GPUAGG_OK;
   if (cap < out.size() + 1) return GPUAGG_ECAPACITY;

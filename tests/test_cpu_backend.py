@@ -217,3 +217,48 @@ def test_latency_capacity_and_touch(limit, chunks):
     assert st["limit"] == limit
     # the touch: without it the late replies (650 ms after their first request) find nothing
     assert want["latency_buckets"][10] > 0
+
+
+def test_exposition_text_cpu_backend():
+    """gpuagg_result_render_text on the CPU backend equals the oracle's exposition, with
+    values on both sides of Go's 'g' notation switch (1e6: byte sums of jumbo packets,
+    trailing zeros, 2^53 and beyond) and a label value that needs escaping; the text is
+    rendered once and the sized second call returns the same bytes."""
+    import ctypes as C
+    from oracle import exposition as X
+    from oracle import oracle as O
+    pods = W.make_pods(200, seed=91)
+    recs = W.gen_records(20_000, pods, seed=92, drop_frac=0.1, retrans_frac=0.05, udp_frac=0.1)
+    pods.endpoints[7] = W.Endpoint('ns"q', 'pod\\x\nq', pods.endpoints[7].ips, pods.endpoints[7].owner_refs)
+    recs.src_ip[:500] = pods.endpoints[7].ips[0]
+    sizes = [1, 999_999, 1_000_000, 1_230_000, 4_000_000_000, 9_007_199_254_740_992 // 4096, 123_456_789]
+    for k, b in enumerate(sizes):  # a few big packets: forward_bytes well past 1e6 (and 2^53)
+        recs.bytes[1000 + 64 * k:1000 + 64 * k + 64] = min(b, 0xFFFFFFFF)
+    sp = spec(["forward_count", "forward_bytes", "drop_count", "drop_bytes"], ["namespace", "podname"])
+    g = make_engine(pods, sp, False, flags=CPU)
+    try:
+        for _ in range(3):
+            g.submit_numpy(recs)
+        r = C.c_void_p()
+        assert g.lib.gpuagg_snapshot(g.h, C.byref(r)) == 0
+        try:
+            n = C.c_size_t()
+            assert g.lib.gpuagg_result_render_text(r, None, 0, C.byref(n)) == 0
+            buf = C.create_string_buffer(n.value + 1)
+            assert g.lib.gpuagg_result_render_text(r, buf, n.value + 1, C.byref(n)) == 0
+            text = buf.value.decode()
+            small = C.create_string_buffer(8)
+            assert g.lib.gpuagg_result_render_text(r, small, 8, C.byref(n)) != 0  # too small: refused
+        finally:
+            g.lib.gpuagg_result_free(r)
+    finally:
+        g.close()
+    from .helpers import oracle_cache
+    m = O.Module(remote_context=False)
+    m.reconcile(R.spec_from_json(sp))
+    for _ in range(3):
+        R.replay(R.Batch(recs.src_ip, recs.dst_ip, recs.bytes, recs.meta, recs.ports, recs.dns_id),
+                 oracle_cache(pods), m)
+    want = X.render(m.series())
+    assert text == want
+    assert "e+" in text and 'pod\\\\x\\nq' in text
