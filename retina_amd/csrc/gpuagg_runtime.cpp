@@ -105,11 +105,22 @@ struct Group {
   uint64_t dense_base, nkeys;
 };
 
-struct Series {
-  std::string metric;
-  std::vector<std::string> names, values;
+// One Prometheus series of a snapshot: its family (the registered metric object), its
+// label values (NUL-terminated, in the family's label order, in one of the result's
+// arenas) and its value.
+struct SeriesRec {
+  uint32_t fam;
+  uint32_t arena;
+  uint64_t off;
   uint64_t value;
-  const char *type, *help;  // Prometheus family (static strings)
+};
+
+struct ResultFamily {
+  std::string metric;
+  std::vector<std::string> names;
+  std::vector<const char *> name_ptrs;
+  std::vector<uint32_t> by_name;  // label positions in name order (client_golang sorts pairs)
+  const char *type = "", *help = "";
 };
 
 // A metric family's Prometheus type and Help text, as the reference's Init creates its
@@ -139,8 +150,11 @@ struct OptCopy {
 }  // namespace
 
 struct gpuagg_result {
-  std::vector<Series> series;
-  std::vector<std::vector<const char *>> name_ptrs, value_ptrs;
+  std::vector<ResultFamily> fam;  // one per registered metric object
+  std::vector<SeriesRec> series;
+  std::vector<std::vector<char>> arenas;
+  std::vector<const char *> value_ptrs;  // series i's label values: [voff[i], voff[i + 1])
+  std::vector<uint64_t> voff;
   uint64_t dropped = 0;
   // families rendered outside `series` (the latency histograms / no_response counter):
   // name -> exposition text block
@@ -2617,6 +2631,339 @@ namespace {
 void render_latency(const gpuagg_latency_state &ls, std::map<std::string, std::string> &blocks);
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- snapshot rendering (the AdvancedRegistry's vectors at scrape time) ------------------
+// Every counter is first reduced to a key of label-determining integer ids -- equal ids
+// exactly when the rendered label strings are equal: IPs and ports are their own ids,
+// pod attributes and DNS payloads are canonicalised by their strings -- so equal tuples are
+// summed in hash maps on integers (partitioned over host threads) and each distinct series
+// is rendered to strings once, into per-partition arenas.
+struct LKey {
+  uint32_t w[8];  // view, prefix (direction / reason / flag / DNS payload), src ip / attrs / port, dst ...
+  bool operator==(const LKey &o) const { return memcmp(w, o.w, sizeof w) == 0; }
+};
+struct LKeyHash {
+  size_t operator()(const LKey &k) const {
+    uint64_t h = 0x8BADF00DULL;
+    for (int i = 0; i < 8; i += 2) h = fmix64(h ^ ((uint64_t)k.w[i] | ((uint64_t)k.w[i + 1] << 32)));
+    return (size_t)h;
+  }
+};
+struct LItem {
+  LKey k;
+  uint64_t cnt, byt;
+};
+
+// Canonical ids of the slot attributes a side's options render (namespace / pod /
+// workload; the service label is constant): csa[slot1] (slot1 0 or past the table:
+// "unknown"), and a representative slot1 per id.
+struct SlotCanon {
+  std::vector<uint32_t> id, rep;
+};
+
+void append_str(std::vector<char> &a, const char *s, size_t n) {
+  a.insert(a.end(), s, s + n);
+  a.push_back('\0');
+}
+void append_str(std::vector<char> &a, const std::string &s) { append_str(a, s.data(), s.size()); }
+
+// ctx_values (getByDirectionValues, types.go:418-505) into an arena.
+void ctx_values_into(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, uint32_t port17,
+                     std::vector<char> &out) {
+  const SlotAttr *a = (slot1 && slot1 - 1 < c->slots.size()) ? &c->slots[slot1 - 1] : nullptr;
+  static const std::string unk = "unknown";
+  if (opts & OPT_IP) {
+    char b[20];
+    const int n = snprintf(b, sizeof b, "%u.%u.%u.%u", ip & 255u, (ip >> 8) & 255u, (ip >> 16) & 255u, ip >> 24);
+    append_str(out, b, (size_t)n);
+  }
+  if (opts & OPT_NS) append_str(out, a ? a->ns : unk);
+  if (opts & OPT_POD) append_str(out, a ? a->pod : unk);
+  if (opts & OPT_WL) {
+    append_str(out, a && a->has_owner ? a->wk_kind : unk);
+    append_str(out, a && a->has_owner ? a->wk_name : unk);
+  }
+  if (opts & OPT_SVC) append_str(out, unk);
+  if (opts & OPT_PORT) {
+    if (port17 & 0x10000u) {
+      char b[8];
+      const int n = snprintf(b, sizeof b, "%u", port17 & 0xFFFFu);
+      append_str(out, b, (size_t)n);
+    } else {
+      append_str(out, unk);
+    }
+  }
+}
+
+int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vector<uint64_t> &db,
+                  const std::vector<uint64_t> &ent, size_t nent, gpuagg_result *r) {
+  const bool local = !c->remote;
+  const size_t ns_len = strlen("networkobservability_");
+  r->fam.resize(c->inst.size());
+  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
+    ResultFamily &f = r->fam[ii];
+    const Instance &in = c->inst[ii];
+    const FamilyInfo fi = family_info(in.vec_name.substr(ns_len));
+    f.metric = in.vec_name;
+    f.names = in.label_names;
+    f.type = fi.type;
+    f.help = fi.help;
+  }
+  for (auto &f : r->fam) {  // (pointers taken once the vector is final)
+    for (auto &n : f.names) f.name_ptrs.push_back(n.c_str());
+    f.by_name.resize(f.names.size());
+    for (uint32_t k = 0; k < f.by_name.size(); ++k) f.by_name[k] = k;
+    std::stable_sort(f.by_name.begin(), f.by_name.end(),
+                     [&](uint32_t a, uint32_t b) { return f.names[a] < f.names[b]; });
+  }
+  // views: (group, src labels, dst labels) of the active instances
+  struct View {
+    int group;
+    bool src, dst;
+    std::vector<uint32_t> insts;
+  };
+  std::vector<View> views;
+  std::vector<std::vector<uint32_t>> group_views(c->groups.size());
+  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
+    const Instance &in = c->inst[ii];
+    if (!in.active || in.group < 0) continue;
+    const bool s = local || in.has_src, d = !local && in.has_dst;
+    uint32_t v = 0;
+    while (v < views.size() && !(views[v].group == in.group && views[v].src == s && views[v].dst == d)) ++v;
+    if (v == views.size()) {
+      views.push_back(View{in.group, s, d, {}});
+      group_views[in.group].push_back(v);
+    }
+    views[v].insts.push_back((uint32_t)ii);
+  }
+  if (views.empty()) return GPUAGG_OK;
+  // canonical slot attributes per option mask
+  std::map<uint8_t, SlotCanon> canon;
+  auto slot_canon = [&](uint8_t opts) -> const SlotCanon & {
+    const uint8_t m = opts & (OPT_NS | OPT_POD | OPT_WL);
+    auto it = canon.find(m);
+    if (it != canon.end()) return it->second;
+    SlotCanon &sc = canon[m];
+    std::unordered_map<std::string, uint32_t> ids;
+    std::vector<char> buf;
+    sc.id.resize(c->slots.size() + 1);
+    for (uint32_t s1 = 0; s1 <= c->slots.size(); ++s1) {
+      buf.clear();
+      ctx_values_into(c, m, 0, s1, 0, buf);
+      auto ins = ids.emplace(std::string(buf.begin(), buf.end()), (uint32_t)sc.rep.size());
+      if (ins.second) sc.rep.push_back(s1);
+      sc.id[s1] = ins.first->second;
+    }
+    return sc;
+  };
+  for (const View &v : views) {
+    slot_canon(c->groups[v.group].src_opts);
+    slot_canon(c->groups[v.group].dst_opts);
+  }
+  auto cid = [&](const SlotCanon &sc, uint32_t slot1) { return sc.id[slot1 < sc.id.size() ? slot1 : 0]; };
+  // canonical DNS payloads: request series (qtypes, query), response series (rcode name,
+  // qtypes, query, ips, answers)
+  std::vector<uint32_t> dns_req, dns_resp, dns_req_rep, dns_resp_rep;
+  bool any_dns = false;
+  for (const View &v : views)
+    any_dns |= c->groups[v.group].family == FAM_DNS_REQ || c->groups[v.group].family == FAM_DNS_RESP;
+  if (any_dns) {
+    std::unordered_map<std::string, uint32_t> rq, rs;
+    dns_req.resize(c->dns.size());
+    dns_resp.resize(c->dns.size());
+    for (size_t k = 0; k < c->dns.size(); ++k) {
+      const DnsAttr &a = c->dns[k];
+      const std::string q = a.qtypes + '\0' + a.query;
+      auto i1 = rq.emplace(q, (uint32_t)dns_req_rep.size());
+      if (i1.second) dns_req_rep.push_back((uint32_t)k);
+      dns_req[k] = i1.first->second;
+      const std::string full = std::string(a.rcode < 6 ? kRcodeNames[a.rcode] : "") + '\0' + q + '\0' + a.ips + '\0' +
+                               std::to_string(a.nresp);
+      auto i2 = rs.emplace(full, (uint32_t)dns_resp_rep.size());
+      if (i2.second) dns_resp_rep.push_back((uint32_t)k);
+      dns_resp[k] = i2.first->second;
+    }
+  }
+  // items: one per (counter, view), partitioned by key hash
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t work = nent + (size_t)c->dense_len;
+  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, work / 65536 + 1}));
+  std::vector<std::vector<std::vector<LItem>>> parts(T, std::vector<std::vector<LItem>>(T));
+  std::vector<int> err(T, GPUAGG_OK);
+  auto run = [&](auto &&fn) {  // fn(t) on T threads
+    if (T == 1) {
+      fn(0u);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t) th.emplace_back(fn, t);
+    for (auto &x : th) x.join();
+  };
+  auto put = [&](unsigned t, const LKey &k, uint64_t cn, uint64_t by) {
+    parts[t][LKeyHash()(k) % T].push_back(LItem{k, cn, by});
+  };
+  run([&](unsigned t) {
+    // sparse entries [t * nent / T, (t + 1) * nent / T)
+    const size_t e0 = nent * t / T, e1 = nent * (t + 1) / T;
+    for (size_t e = e0; e < e1; ++e) {
+      const uint64_t *w = &ent[e * kSparseEntryWords];
+      const uint32_t grp = key_group(w[0]);
+      if (grp >= group_views.size()) continue;
+      const Group &g = c->groups[grp];
+      const uint32_t sub = key_sub(w[0]);
+      const uint32_t hi = sub >> 3, tdir = (sub >> 1) & 3, side = sub & 1;
+      const uint32_t dirv = local ? side : tdir;
+      uint32_t pre = 0;
+      switch (g.family) {
+        case FAM_FWD:
+        case FAM_RETRANS: pre = dirv; break;
+        case FAM_DROP: pre = (hi << 4) | dirv; break;
+        case FAM_TCPFLAGS: pre = hi; break;
+        case FAM_DNS_REQ:
+        case FAM_DNS_RESP: {
+          const uint32_t id = key_dns(w[2]);
+          if (id >= c->dns.size()) {
+            err[t] = GPUAGG_EINVAL;
+            return;
+          }
+          pre = g.family == FAM_DNS_REQ ? dns_req[id] : dns_resp[id];
+          break;
+        }
+      }
+      for (uint32_t vi : group_views[grp]) {
+        const View &v = views[vi];
+        LKey k{};
+        k.w[0] = vi;
+        k.w[1] = pre;
+        if (v.src) {
+          k.w[2] = (g.src_opts & OPT_IP) ? key_s_ip(w[0]) : 0u;
+          k.w[3] = cid(canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL)), key_s_slot1(w[0]));
+          k.w[4] = (g.src_opts & OPT_PORT) ? key_s_port17(w[1]) : 0u;
+        }
+        if (v.dst) {
+          k.w[5] = (g.dst_opts & OPT_IP) ? key_d_ip(w[2]) : 0u;
+          k.w[6] = cid(canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL)), key_d_slot1(w[1]));
+          k.w[7] = (g.dst_opts & OPT_PORT) ? key_d_port17(w[1]) : 0u;
+        }
+        put(t, k, w[3], w[4]);
+      }
+    }
+    // dense bins: group by group, keys split over the threads
+    for (size_t gi = 0; gi < c->groups.size(); ++gi) {
+      const Group &g = c->groups[gi];
+      if (g.sparse || group_views[gi].empty()) continue;
+      const SlotCanon &sc = canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
+      const uint64_t k0 = g.nkeys * t / T, k1 = g.nkeys * (t + 1) / T;
+      for (uint64_t key = k0; key < k1; ++key)
+        for (uint32_t side = 0; side < 2; ++side)
+          for (uint32_t sub = 0; sub < g.nsub; ++sub) {
+            const uint64_t idx = g.dense_base + (key * 2 + side) * g.nsub + sub;
+            if (!dc[idx]) continue;  // (a bytes series exists whenever its count does)
+            const uint32_t pre = g.family == FAM_DROP ? (sub << 4) | side : g.family == FAM_TCPFLAGS ? sub : side;
+            for (uint32_t vi : group_views[gi]) {
+              LKey k{};
+              k.w[0] = vi;
+              k.w[1] = pre;
+              k.w[3] = cid(sc, g.key_mode ? (uint32_t)key + 1 : 0u);
+              put(t, k, dc[idx], db[idx]);
+            }
+          }
+    }
+  });
+  for (int e : err)
+    if (e) return fail(c, e, "snapshot: a group-by key names a dns_id that was not interned");
+  // per partition: sum equal keys, then render each distinct key's series into the
+  // partition's arena
+  std::vector<std::vector<SeriesRec>> out(T);
+  r->arenas.resize(T);
+  run([&](unsigned p) {
+    size_t total = 0;
+    for (unsigned t = 0; t < T; ++t) total += parts[t][p].size();
+    std::unordered_map<LKey, std::pair<uint64_t, uint64_t>, LKeyHash> m;
+    m.reserve(total);
+    for (unsigned t = 0; t < T; ++t) {
+      for (const LItem &it : parts[t][p]) {
+        auto &a = m[it.k];
+        a.first += it.cnt;
+        a.second += it.byt;
+      }
+      std::vector<LItem>().swap(parts[t][p]);
+    }
+    std::vector<char> &ar = r->arenas[p];
+    for (const auto &kv : m) {
+      const LKey &k = kv.first;
+      const View &v = views[k.w[0]];
+      const Group &g = c->groups[v.group];
+      for (uint32_t ii : v.insts) {
+        const Instance &in = c->inst[ii];
+        out[p].push_back(SeriesRec{ii, p, ar.size(), in.vk == VK_BYTES ? kv.second.second : kv.second.first});
+        const uint32_t pre = k.w[1];
+        auto dir = [&](uint32_t d) {
+          if (local) append_str(ar, d == 0 ? "ingress" : "egress", d == 0 ? 7 : 6);
+          else append_str(ar, traffic_direction_name(d));
+        };
+        switch (g.family) {
+          case FAM_FWD:
+          case FAM_RETRANS: dir(pre); break;
+          case FAM_DROP:
+            append_str(ar, drop_reason_name(pre >> 4));
+            dir(pre & 15u);
+            break;
+          case FAM_TCPFLAGS: append_str(ar, kFlagNames[pre]); break;
+          case FAM_DNS_REQ:
+          case FAM_DNS_RESP: {
+            const DnsAttr &a = c->dns[g.family == FAM_DNS_REQ ? dns_req_rep[pre] : dns_resp_rep[pre]];
+            if (g.family == FAM_DNS_RESP) append_str(ar, a.rcode < 6 ? kRcodeNames[a.rcode] : "");
+            append_str(ar, a.qtypes);
+            append_str(ar, a.query);
+            if (g.family == FAM_DNS_RESP) {
+              append_str(ar, a.ips);
+              append_str(ar, std::to_string(a.nresp));
+            }
+            break;
+          }
+        }
+        if (v.src) {
+          const SlotCanon &sc = canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
+          ctx_values_into(c, g.src_opts, k.w[2], sc.rep[k.w[3]], k.w[4], ar);
+        }
+        if (v.dst) {
+          const SlotCanon &sc = canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL));
+          ctx_values_into(c, g.dst_opts, k.w[5], sc.rep[k.w[6]], k.w[7], ar);
+        }
+      }
+    }
+  });
+  size_t ns = 0;
+  for (auto &o : out) ns += o.size();
+  r->series.reserve(ns);
+  for (auto &o : out) r->series.insert(r->series.end(), o.begin(), o.end());
+  // label value pointers (the arenas are final now)
+  r->voff.resize(ns + 1);
+  uint64_t nv = 0;
+  for (size_t i = 0; i < ns; ++i) {
+    r->voff[i] = nv;
+    nv += r->fam[r->series[i].fam].names.size();
+  }
+  r->voff[ns] = nv;
+  r->value_ptrs.resize(nv);
+  for (size_t i = 0; i < ns; ++i) {
+    const char *q = r->arenas[r->series[i].arena].data() + r->series[i].off;
+    for (uint64_t k = r->voff[i]; k < r->voff[i + 1]; ++k) {
+      r->value_ptrs[k] = q;
+      q += strlen(q) + 1;
+    }
+  }
+  return GPUAGG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
   if (!c || !out) return GPUAGG_EINVAL;
   *out = nullptr;
@@ -2648,84 +2995,11 @@ int gpuagg_snapshot(gpuagg_ctx *c, gpuagg_result **out) {
     c->stats.sparse_entries = nent;
   }
 
-  // render: key -> label tuple, summing equal tuples
-  std::vector<std::map<std::vector<std::string>, uint64_t>> acc(c->inst.size());
-  std::vector<std::string> vals;
-  const bool local = !c->remote;
-  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
-    const Instance &in = c->inst[ii];
-    if (!in.active || in.group < 0) continue;
-    const Group &g = c->groups[in.group];
-    auto &dst = acc[ii];
-    if (!g.sparse) {
-      for (uint64_t key = 0; key < g.nkeys; ++key)
-        for (uint32_t side = 0; side < 2; ++side)
-          for (uint32_t sub = 0; sub < g.nsub; ++sub) {
-            const uint64_t idx = g.dense_base + (key * 2 + side) * g.nsub + sub;
-            if (!dc[idx]) continue;
-            vals.clear();
-            if (g.family == FAM_DROP) vals.push_back(drop_reason_name(sub));
-            if (g.family == FAM_TCPFLAGS) vals.push_back(kFlagNames[sub]);
-            if (g.family != FAM_TCPFLAGS) vals.push_back(side == 0 ? "ingress" : "egress");
-            ctx_values(c, g.src_opts, 0, g.key_mode ? (uint32_t)key + 1 : 0, 0, vals);
-            dst[vals] += in.vk == VK_BYTES ? db[idx] : dc[idx];
-          }
-      continue;
-    }
-    for (size_t e = 0; e < nent; ++e) {
-      const uint64_t *w = &ent[e * kSparseEntryWords];
-      if ((int)key_group(w[0]) != in.group) continue;
-      const uint32_t sub = key_sub(w[0]);
-      vals.clear();
-      const uint32_t hi = sub >> 3, tdir = (sub >> 1) & 3, side = sub & 1;
-      switch (g.family) {
-        case FAM_FWD:
-        case FAM_RETRANS:
-          vals.push_back(local ? (side == 0 ? "ingress" : "egress") : traffic_direction_name(tdir));
-          break;
-        case FAM_DROP:
-          vals.push_back(drop_reason_name(hi));
-          vals.push_back(local ? (side == 0 ? "ingress" : "egress") : traffic_direction_name(tdir));
-          break;
-        case FAM_TCPFLAGS: vals.push_back(kFlagNames[hi]); break;
-        case FAM_DNS_REQ:
-        case FAM_DNS_RESP: {
-          const uint32_t id = key_dns(w[2]);
-          if (id >= c->dns.size()) return fail(c, GPUAGG_EINVAL, "dns_id %u was not interned", id);
-          const DnsAttr &a = c->dns[id];
-          if (g.family == FAM_DNS_RESP) vals.push_back(a.rcode < 6 ? kRcodeNames[a.rcode] : "");
-          vals.push_back(a.qtypes);
-          vals.push_back(a.query);
-          if (g.family == FAM_DNS_RESP) {
-            vals.push_back(a.ips);
-            vals.push_back(std::to_string(a.nresp));
-          }
-          break;
-        }
-      }
-      if (local) {
-        ctx_values(c, g.src_opts, key_s_ip(w[0]), key_s_slot1(w[0]), key_s_port17(w[1]), vals);
-      } else {
-        if (in.has_src) ctx_values(c, g.src_opts, key_s_ip(w[0]), key_s_slot1(w[0]), key_s_port17(w[1]), vals);
-        if (in.has_dst) ctx_values(c, g.dst_opts, key_d_ip(w[2]), key_d_slot1(w[1]), key_d_port17(w[1]), vals);
-      }
-      dst[vals] += in.vk == VK_BYTES ? w[4] : w[3];
-    }
-  }
-
   auto *r = new gpuagg_result();
   r->dropped = c->stats.sparse_dropped;
-  const size_t ns_len = strlen("networkobservability_");
-  for (size_t ii = 0; ii < c->inst.size(); ++ii) {
-    const FamilyInfo fi = family_info(c->inst[ii].vec_name.substr(ns_len));
-    for (auto &kv : acc[ii])
-      r->series.push_back(Series{c->inst[ii].vec_name, c->inst[ii].label_names, kv.first, kv.second, fi.type, fi.help});
-  }
-  r->name_ptrs.resize(r->series.size());
-  r->value_ptrs.resize(r->series.size());
-  for (size_t i = 0; i < r->series.size(); ++i) {
-    for (auto &s : r->series[i].names) r->name_ptrs[i].push_back(s.c_str());
-    for (auto &s : r->series[i].values) r->value_ptrs[i].push_back(s.c_str());
+  if ((rc = render_series(c, dc, db, ent, nent, r))) {
+    gpuagg_result_free(r);
+    return rc;
   }
   if (c->cms_len || c->hll_len) {
     if ((rc = gpuagg_sketch_refresh(c))) {
@@ -2749,8 +3023,8 @@ size_t gpuagg_result_count(const gpuagg_result *r) { return r ? r->series.size()
 
 int gpuagg_result_family(const gpuagg_result *r, size_t i, const char **type, const char **help) {
   if (!r || i >= r->series.size()) return GPUAGG_EINVAL;
-  if (type) *type = r->series[i].type;
-  if (help) *help = r->series[i].help;
+  if (type) *type = r->fam[r->series[i].fam].type;
+  if (help) *help = r->fam[r->series[i].fam].help;
   return GPUAGG_OK;
 }
 
@@ -2869,14 +3143,16 @@ void render_latency(const gpuagg_latency_state &ls, std::map<std::string, std::s
   }
 }
 
-void escape_into(std::string &out, const std::string &s, bool quote) {  // expfmt escaping
-  for (char ch : s) {
+void escape_cstr(std::string &out, const char *s, bool quote) {  // expfmt escaping
+  for (; *s; ++s) {
+    const char ch = *s;
     if (ch == '\\') out += "\\\\";
     else if (ch == '\n') out += "\\n";
     else if (quote && ch == '"') out += "\\\"";
     else out += ch;
   }
 }
+void escape_into(std::string &out, const std::string &s, bool quote) { escape_cstr(out, s.c_str(), quote); }
 }  // namespace
 
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
@@ -2888,52 +3164,69 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
     memcpy(buf, r->text.c_str(), r->text.size() + 1);
     return GPUAGG_OK;
   }
-  // family name -> series indices; label pairs sorted by name (client_golang keeps a
-  // metric's label pairs sorted), series sorted by those values (MetricSorter)
+  // families by name; within one, series sorted by their label values taken in label
+  // name order (client_golang keeps a metric's pairs sorted by name; MetricSorter) --
+  // sorted in parallel chunks, merged, then rendered in parallel chunks
   std::map<std::string, std::vector<size_t>> fam;
-  for (size_t i = 0; i < r->series.size(); ++i) fam[r->series[i].metric].push_back(i);
-  // (no string copies: pointers into the series)
-  std::vector<std::vector<std::pair<const std::string *, const std::string *>>> pairs(r->series.size());
-  for (size_t i = 0; i < r->series.size(); ++i) {
-    const Series &se = r->series[i];
-    pairs[i].reserve(se.names.size());
-    for (size_t k = 0; k < se.names.size(); ++k) pairs[i].emplace_back(&se.names[k], &se.values[k]);
-    std::stable_sort(pairs[i].begin(), pairs[i].end(),
-                     [](const auto &a, const auto &b) { return *a.first < *b.first; });
-  }
+  for (size_t i = 0; i < r->series.size(); ++i) fam[r->fam[r->series[i].fam].metric].push_back(i);
   std::map<std::string, std::string> blocks = r->extra_text;  // family name -> text
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   for (auto &kv : fam) {
-    std::string &out = blocks[kv.first];
     auto &idx = kv.second;
-    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
-      const auto &pa = pairs[a], &pb = pairs[b];
-      for (size_t k = 0; k < pa.size() && k < pb.size(); ++k) {
-        const int c = pa[k].second->compare(*pb[k].second);
+    const ResultFamily &F = r->fam[r->series[idx[0]].fam];
+    const size_t nl = F.names.size();
+    auto less = [&](size_t a, size_t b) {
+      const char *const *va = r->value_ptrs.data() + r->voff[a], *const *vb = r->value_ptrs.data() + r->voff[b];
+      for (size_t k = 0; k < nl; ++k) {
+        const int c = strcmp(va[F.by_name[k]], vb[F.by_name[k]]);
         if (c) return c < 0;
       }
       return false;
-    });
-    const Series &first = r->series[idx[0]];
-    out += "# HELP " + kv.first + " ";
-    escape_into(out, first.help, false);
-    out += "\n# TYPE " + kv.first + " " + first.type + "\n";
-    for (size_t i : idx) {
-      out += kv.first;
-      if (!pairs[i].empty()) {
-        out += '{';
-        for (size_t k = 0; k < pairs[i].size(); ++k) {
-          if (k) out += ',';
-          out += *pairs[i][k].first;
-          out += "=\"";
-          escape_into(out, *pairs[i][k].second, true);
-          out += '"';
-        }
-        out += '}';
+    };
+    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 32768 + 1}));
+    std::vector<size_t> cut(T + 1);
+    for (unsigned t = 0; t <= T; ++t) cut[t] = idx.size() * t / T;
+    auto par = [&](unsigned n, auto &&fn) {
+      if (n == 1) {
+        fn(0u);
+        return;
       }
-      out += ' ';
-      go_float_u64_into(out, r->series[i].value);
-      out += '\n';
-    }
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < n; ++t) th.emplace_back(fn, t);
+      for (auto &x : th) x.join();
+    };
+    par(T, [&](unsigned t) { std::sort(idx.begin() + cut[t], idx.begin() + cut[t + 1], less); });
+    for (size_t w = 1; w < T; w *= 2)  // pairwise merges of sorted runs
+      for (size_t a = 0; a + w < T; a += 2 * w)
+        std::inplace_merge(idx.begin() + cut[a], idx.begin() + cut[a + w], idx.begin() + cut[std::min<size_t>(a + 2 * w, T)], less);
+    std::vector<std::string> chunk(T);
+    par(T, [&](unsigned t) {
+      std::string &o = chunk[t];
+      for (size_t q = cut[t]; q < cut[t + 1]; ++q) {
+        const size_t i = idx[q];
+        o += F.metric;
+        const char *const *v = r->value_ptrs.data() + r->voff[i];
+        if (nl) {
+          o += '{';
+          for (size_t k = 0; k < nl; ++k) {
+            if (k) o += ',';
+            o += F.names[F.by_name[k]];
+            o += "=\"";
+            escape_cstr(o, v[F.by_name[k]], true);
+            o += '"';
+          }
+          o += '}';
+        }
+        o += ' ';
+        go_float_u64_into(o, r->series[i].value);
+        o += '\n';
+      }
+    });
+    std::string &out = blocks[kv.first];
+    out += "# HELP " + kv.first + " ";
+    escape_cstr(out, F.help, false);
+    out += "\n# TYPE " + kv.first + " " + F.type + "\n";
+    for (auto &ch : chunk) out += ch;
   }
   std::string &out = r->text;
   out.clear();
@@ -2952,11 +3245,12 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
 int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, uint32_t *n_labels,
                          const char *const **names, const char *const **values, uint64_t *value) {
   if (!r || i >= r->series.size()) return GPUAGG_EINVAL;
-  const Series &s = r->series[i];
-  if (metric) *metric = s.metric.c_str();
-  if (n_labels) *n_labels = (uint32_t)s.names.size();
-  if (names) *names = r->name_ptrs[i].data();
-  if (values) *values = r->value_ptrs[i].data();
+  const SeriesRec &s = r->series[i];
+  const ResultFamily &f = r->fam[s.fam];
+  if (metric) *metric = f.metric.c_str();
+  if (n_labels) *n_labels = (uint32_t)f.names.size();
+  if (names) *names = f.name_ptrs.data();
+  if (values) *values = r->value_ptrs.data() + r->voff[i];
   if (value) *value = s.value;
   return GPUAGG_OK;
 }

@@ -163,7 +163,9 @@ def test_deferred_sketch_folds_exact(gpu_device, flags):
 
     def check(tag):
         assert np.array_equal(g.cms_array(), want_c), tag
-        assert np.array_equal(g.hll_array()[:len(more.endpoints)], want_h), tag
+        h = g.hll_array()  # rows of the slots in use (grown with them)
+        n = min(len(h), len(want_h))
+        assert np.array_equal(h[:n], want_h[:n]) and not want_h[n:].any(), tag
 
     total = 0
     try:
