@@ -3144,6 +3144,11 @@ void render_latency(const gpuagg_latency_state &ls, std::map<std::string, std::s
 }
 
 void escape_cstr(std::string &out, const char *s, bool quote) {  // expfmt escaping
+  const size_t n = strlen(s);
+  if (!memchr(s, '\\', n) && !memchr(s, '\n', n) && !(quote && memchr(s, '"', n))) {
+    out.append(s, n);  // nothing to escape (the usual case)
+    return;
+  }
   for (; *s; ++s) {
     const char ch = *s;
     if (ch == '\\') out += "\\\\";
@@ -3167,8 +3172,11 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
   // families by name; within one, series sorted by their label values taken in label
   // name order (client_golang keeps a metric's pairs sorted by name; MetricSorter) --
   // sorted in parallel chunks, merged, then rendered in parallel chunks
+  std::vector<std::vector<size_t>> by_fam(r->fam.size());
+  for (size_t i = 0; i < r->series.size(); ++i) by_fam[r->series[i].fam].push_back(i);
   std::map<std::string, std::vector<size_t>> fam;
-  for (size_t i = 0; i < r->series.size(); ++i) fam[r->fam[r->series[i].fam].metric].push_back(i);
+  for (size_t f = 0; f < by_fam.size(); ++f)
+    if (!by_fam[f].empty()) fam[r->fam[f].metric] = std::move(by_fam[f]);
   std::map<std::string, std::string> blocks = r->extra_text;  // family name -> text
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   for (auto &kv : fam) {
@@ -3183,7 +3191,7 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
       }
       return false;
     };
-    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 32768 + 1}));
+    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 8192 + 1}));
     std::vector<size_t> cut(T + 1);
     for (unsigned t = 0; t <= T; ++t) cut[t] = idx.size() * t / T;
     auto par = [&](unsigned n, auto &&fn) {
@@ -3202,6 +3210,7 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
     std::vector<std::string> chunk(T);
     par(T, [&](unsigned t) {
       std::string &o = chunk[t];
+      o.reserve((cut[t + 1] - cut[t]) * (F.metric.size() + 24 * (nl + 1)));
       for (size_t q = cut[t]; q < cut[t + 1]; ++q) {
         const size_t i = idx[q];
         o += F.metric;
