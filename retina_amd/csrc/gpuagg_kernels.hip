@@ -152,6 +152,7 @@ struct KArgs {
   uint32_t ipl_dr[kIprMaxPfx];             // dense radix descriptors (kIp 2)
   uint32_t *stage_a;  // tier-1 staged flush: [gridDim.x][stage_a_stride] u32, or null
   uint32_t stage_a_stride;
+  uint32_t stage_accum;  // tier-1: bins start from this workgroup's staged copy (deferred reduce)
   // compact group-by keys bucketed per table segment (generic kernel), or null
   unsigned long long *sp_lists;
   uint32_t *sp_counts;
@@ -1083,6 +1084,12 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
   __syncthreads();
   auto insert = [&](unsigned long long key) {
     const uint32_t h = compact_home(s, key);
+    // the key already in its home slot (a key is published whole by its claiming CAS):
+    // one read, then the no-return add
+    if (__hip_atomic_load(&seg[2 * h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == key) {
+      atomicAdd(&seg[2 * h + 1], 1ULL);
+      return;
+    }
     for (uint32_t probe = 0; probe <= smask; ++probe) {
       const uint32_t i = (h + probe) & smask;
       const unsigned long long cur = atomicCAS(&seg[2 * i], 0ULL, key);
@@ -1175,6 +1182,18 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   }
   __syncthreads();
   auto insert = [&](uint32_t h, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {  // h: home slot
+    {  // the key already sits published in its home slot (the common case under skew): one
+       // round trip of reads (K2 first: published after K1, LDS returns in order), then
+       // no-return adds -- no CAS, no dependent chain
+      const unsigned long long p2 = __hip_atomic_load(&K2[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned long long p0 = __hip_atomic_load(&K0[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned long long p1 = K1[h];
+      if (p2 == x2 && p0 == x0 && p1 == x1) {
+        __hip_atomic_fetch_add(&CN[h], (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (b) __hip_atomic_fetch_add(&BY[h], (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+      }
+    }
     for (uint32_t probe = 0; probe < N; ++probe) {
       const uint32_t i = (h + probe) & smask;
       const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
@@ -1702,7 +1721,12 @@ __global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a) {
   uint32_t *bins = (uint32_t *)(smem + a.ipl_bytes);
   const uint32_t L4 = a.lds_bins;
   fill_lds_u4((uint4 *)smem, (const uint4 *)a.ipl, a.ipl_bytes / 16);
-  for (uint32_t i = threadIdx.x; i < L4 + 64; i += blockDim.x) bins[i] = 0u;
+  if (a.stage_accum) {  // deferred reduce: continue from this workgroup's staged copy
+    const uint32_t *mine = a.stage_a + (size_t)blockIdx.x * a.stage_a_stride;
+    for (uint32_t i = threadIdx.x; i < L4 + 64; i += blockDim.x) bins[i] = i < L4 ? mine[i] : 0u;
+  } else {
+    for (uint32_t i = threadIdx.x; i < L4 + 64; i += blockDim.x) bins[i] = 0u;
+  }
   for (uint32_t w = threadIdx.x; w < kMaxSpillWindows; w += blockDim.x)
     bins[L4 + 64 + w] = a.spill && w < a.nwin ? spill_ctr0(a, w) : 0u;
   __syncthreads();
@@ -3025,6 +3049,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   }
   k.stage_a = a.stage_a;
   k.stage_a_stride = a.stage_a_stride;
+  k.stage_accum = a.stage_a && a.stage_accum ? 1u : 0u;
   k.sp_lists = (unsigned long long *)a.sp_lists;
   k.sp_counts = a.sp_counts;
   k.sp_nwin = a.sp_lists ? a.sp_nwin : 0u;
@@ -3118,6 +3143,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
       LaunchArgs r = a;
       r.spill = nullptr;
       r.stage_b = nullptr;
+      if (a.stage_defer) r.stage_a = nullptr;
       if (!a.fold_cond) r.sp_lists = nullptr;
       return launch_folds(r, st);
     }
@@ -3194,10 +3220,11 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   if (e != hipSuccess) return e;
   if (between && (e = hipEventRecord(between, st)) != hipSuccess) return e;
   if (a.defer_folds) {  // lists folded later (launch_folds), or when the device says so;
-    // the tier-1 copies now
+    // the tier-1 copies now, unless they accumulate too (stage_defer)
     LaunchArgs r = a;
     r.spill = nullptr;
     r.stage_b = nullptr;
+    if (a.stage_defer) r.stage_a = nullptr;
     if (!a.fold_cond) r.sp_lists = nullptr;
     return launch_folds(r, st);
   }

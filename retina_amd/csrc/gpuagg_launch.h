@@ -76,6 +76,11 @@ struct LaunchArgs {
   // launch_folds (the tier-1 copies are still summed per launch)
   bool accum;
   bool defer_folds;
+  // small deferred launches also keep the tier-1 copies: stage_defer = the copies are
+  // summed by the deferred fold (not per launch); stage_accum = this launch's LDS bins
+  // start from its workgroup's staged copy (the copies accumulate across launches)
+  bool stage_defer;
+  bool stage_accum;
   // wide-key lists folded when the device says so: the aggregation kernel records the
   // fullest list in fold_flag[fold_parity] and the per-launch fold skips itself while that
   // is below half the capacity (fold_cond); fold_pending folds unconditionally

@@ -594,7 +594,8 @@ int fold_pending(gpuagg_ctx *c) {
   if (!c->pend.active) return GPUAGG_OK;
   c->pend.active = false;
   LaunchArgs f = c->pend.a;
-  f.stage_a = nullptr;  // summed per launch
+  if (!f.stage_defer) f.stage_a = nullptr;  // summed per launch, unless the copies accumulate
+  f.stage_accum = false;
   f.defer_folds = false;
   f.fold_cond = false;  // unconditional (the flags are left to the launches)
   std::array<hipEvent_t, 2> ev{};
@@ -1354,6 +1355,10 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.stage_a = nullptr;
     if (a.tier1 && a.lds_bins) {  // per-workgroup copies of the LDS bins, summed after
       a.stage_a_stride = (a.lds_bins + 3u) & ~3u;
+      // accumulating copies are summed before their buffer can be reallocated
+      if (c->pend.active && c->pend.a.stage_defer && (size_t)a.blocks * a.stage_a_stride > c->stage_a_alloc &&
+          (rc = fold_pending(c)))
+        return rc;
       if ((rc = ensure_buf(c, &c->d_stage_a, &c->stage_a_alloc, (size_t)a.blocks * a.stage_a_stride)))
         return rc;
       a.stage_a = c->d_stage_a;
@@ -1471,6 +1476,12 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     a.accum = accum;
     a.defer_folds = defer && (a.spill || a.sp_lists);
+    // small spill-only launches keep the tier-1 copies too: each workgroup continues from
+    // its staged copy and the copies are summed once, by the deferred fold -- the per-launch
+    // stage_reduce_kernel (reading blocks x the LDS bins) was most of such a launch's cost
+    a.stage_defer = a.defer_folds && small_spill && !sp_lists && a.stage_a != nullptr;
+    a.stage_accum = a.stage_defer && accum && c->pend.a.stage_defer && c->pend.a.stage_a == a.stage_a &&
+                    c->pend.a.stage_a_stride == a.stage_a_stride;
     a.fold_cond = false;
     a.fold_flag = nullptr;
     if (fold_cond && a.sp_lists) {

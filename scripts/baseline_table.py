@@ -32,10 +32,33 @@ def rows(path):
         r["achieved"], r["kernel_ms"], 100 * r["frac"],
         100 * r["step_bytes_per_record"] * d["config"]["records_per_gpu"] / (d["ms_per_step"] * 1e-3) / 8e12,
         traffic))
+    pr = d.get("production")
+    if pr:
+        out.append("| %s | HIP, device-resident 2^20-record launches (Go batch) | 1 GPU | %.3g | — | %.1f %% kernel | — |" % (
+            LABEL[cfg], pr["records_per_s"], 100 * pr["kernel_frac"]))
     hf = d.get("host_fed")
     if hf:
         out.append("| %s | HIP, host-fed 2^20-record pinned batches (PCIe H2D incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
             LABEL[cfg], hf["value"]))
+    hr = d.get("host_fed_raw")
+    if hr:
+        out.append("| %s | HIP, raw 72-B samples via gpuagg_raw_feed_put (PCIe incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
+            LABEL[cfg], hr["value"]))
+    return out
+
+
+def scrape_rows(paths):
+    """Scrape cost per config: gpuagg_snapshot + gpuagg_result_render_text on the bench's state."""
+    out = ["| Config | series | text MB | snapshot ms | render ms | % of a 15 s scrape epoch |",
+           "|---|---|---|---|---|---|"]
+    for path in paths:
+        d = json.load(open(path))
+        sc = d.get("scrape")
+        if not sc:
+            continue
+        cfg = path.rsplit("_bench_", 1)[-1].replace(".json", "")
+        out.append("| %s | %d | %.1f | %.1f | %.1f | %.2f %% |" % (
+            LABEL[cfg], sc["series"], sc["text_bytes"] / 1e6, sc["snapshot_ms"], sc["render_ms"], 100 * sc["epoch_frac"]))
     return out
 
 
@@ -44,3 +67,5 @@ if __name__ == "__main__":
     print("|---|---|---|---|---|---|---|")
     for p in sys.argv[1:]:
         print("\n".join(rows(p)))
+    print()
+    print("\n".join(scrape_rows(sys.argv[1:])))
