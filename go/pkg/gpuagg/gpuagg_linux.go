@@ -110,6 +110,8 @@ type gpuAgg struct {
 	devs     []*device
 	rawBuf   map[int][]byte                // per kind: back-to-back raw records awaiting submit
 	feeds    map[int]*C.gpuagg_raw_feed    // per kind: shard + scatter into pinned per-device staging
+	recFeed  *C.gpuagg_raw_feed            // decoded records: shard + transpose into pinned SoA batches
+	recBuf   []Record                      // single Write()s awaiting the record feed
 	spec     *api.MetricsSpec
 	vecs     map[string]*prometheus.GaugeVec
 	ctrs     map[string]*prometheus.CounterVec
@@ -377,6 +379,18 @@ func (g *gpuAgg) Init() error {
 		}
 		g.feeds[kind] = f
 	}
+	// decoded records (Write / WriteBatch) go through a GPUAGG_RECORD feed: one cgo call per
+	// slice shards them and transposes them into each device's pinned SoA batch in C (the
+	// Record layout is struct gpuagg_record's)
+	if unsafe.Sizeof(Record{}) != C.sizeof_gpuagg_record {
+		g.destroyLocked()
+		return fmt.Errorf("gpuagg: Record is %d bytes, gpuagg_record %d", unsafe.Sizeof(Record{}), C.sizeof_gpuagg_record)
+	}
+	if err := check(ctxs[0], C.gpuagg_raw_feed_create(&ctxs[0], C.size_t(len(ctxs)), C.GPUAGG_RECORD,
+		batchCapacity, &g.recFeed), "gpuagg_raw_feed_create(records)"); err != nil {
+		g.destroyLocked()
+		return err
+	}
 	g.stopping = false
 	g.spec = nil
 	g.apiIPs = map[string]uint32{}
@@ -629,6 +643,25 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		}
 		return nil
 	}
+	// putRecords hands a slice of decoded records to the record feed (the enriched-flow
+	// path keeps the per-record batches: emitLocked rebuilds flows from them)
+	putRecords := func(rs []Record, flush bool) error {
+		g.mu.Lock()
+		defer g.mu.Unlock()
+		if err := g.commitLocked(); err != nil {
+			return err
+		}
+		if len(rs) > 0 {
+			if err := check(devs[0].ctx, C.gpuagg_raw_feed_put(g.recFeed, unsafe.Pointer(&rs[0]), C.size_t(len(rs))),
+				"gpuagg_raw_feed_put(records)"); err != nil {
+				return err
+			}
+		}
+		if flush {
+			return check(devs[0].ctx, C.gpuagg_raw_feed_flush(g.recFeed), "gpuagg_raw_feed_flush(records)")
+		}
+		return nil
+	}
 	submitAll := func() error {
 		var err error
 		for _, d := range devs {
@@ -636,6 +669,10 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 				err = e
 			}
 		}
+		if e := putRecords(g.recBuf, true); e != nil && err == nil {
+			err = e
+		}
+		g.recBuf = g.recBuf[:0]
 		for kind := range rawSize {
 			if e := submitRaw(kind, true); e != nil && err == nil {
 				err = e
@@ -662,10 +699,26 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		case <-ctx.Done():
 			return submitAll()
 		case r := <-g.records:
-			put(&r)
+			if g.external != nil {
+				put(&r)
+				break
+			}
+			g.recBuf = append(g.recBuf, r)
+			if len(g.recBuf) >= rawPiece {
+				if err := putRecords(g.recBuf, false); err != nil {
+					g.l.Error("record submit failed", zap.Error(err))
+				}
+				g.recBuf = g.recBuf[:0]
+			}
 		case rs := <-g.batches:
-			for i := range rs {
-				put(&rs[i])
+			if g.external != nil {
+				for i := range rs {
+					put(&rs[i])
+				}
+				break
+			}
+			if err := putRecords(rs, false); err != nil {
+				g.l.Error("record submit failed", zap.Error(err))
 			}
 		case s := <-g.raw:
 			g.rawBuf[s.kind] = append(g.rawBuf[s.kind], s.b...)
@@ -813,6 +866,10 @@ func (g *gpuAgg) destroyLocked() {
 	for kind, f := range g.feeds {
 		C.gpuagg_raw_feed_destroy(f) // before the contexts: it frees their pinned staging
 		delete(g.feeds, kind)
+	}
+	if g.recFeed != nil {
+		C.gpuagg_raw_feed_destroy(g.recFeed)
+		g.recFeed = nil
 	}
 	for _, d := range g.devs {
 		C.gpuagg_destroy(d.ctx) // frees the pinned batch too

@@ -274,6 +274,15 @@ int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uin
 int gpuagg_shard_columns(const uint32_t *src_ip, const uint32_t *dst_ip, const uint32_t *ports,
                          const uint32_t *meta, size_t n, uint32_t n_shards, uint32_t *shard_out);
 
+/* Decoded records back to back (the Go plugin's Record, gpuagg_linux.go): the feed kind
+ * GPUAGG_RECORD takes arrays of these, shards them by gpuagg_shard_columns' function and
+ * transposes them into each context's pinned SoA batch (gpuagg_submit when full). */
+#define GPUAGG_RECORD 3
+typedef struct gpuagg_record {
+  uint32_t src_ip, dst_ip, bytes, meta, ports, dns_id, tcp_id, pad_;
+  uint64_t time_ns;
+} gpuagg_record;
+
 /* Node-wide raw ingestion (the Go plugin's raw path, gpuagg_linux.go Start/submitRaw):
  * one call shards a buffer of back-to-back raw samples over the node's contexts (one per
  * device; the gpuagg_shard_raw function) and copies each sample into its context's
@@ -285,6 +294,7 @@ int gpuagg_shard_columns(const uint32_t *src_ip, const uint32_t *dst_ip, const u
  * staging (the plugin's flushInterval tick and Stop); _submitted reports the records
  * handed to each context.  Not thread-safe: one feed per reader goroutine. */
 typedef struct gpuagg_raw_feed gpuagg_raw_feed;
+/* kind: GPUAGG_RAW_PACKET / GPUAGG_RAW_DROP (perf samples) or GPUAGG_RECORD (gpuagg_record) */
 int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
                            gpuagg_raw_feed **out);
 int gpuagg_raw_feed_put(gpuagg_raw_feed *feed, const void *raw, size_t n);

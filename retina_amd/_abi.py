@@ -87,7 +87,8 @@ class Stats(C.Structure):
 
 
 RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
-RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32}
+RECORD = 3  # GPUAGG_RECORD: decoded records, struct gpuagg_record (40 bytes)
+RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32, RECORD: 40}
 
 
 KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel", 4: "cpu"}

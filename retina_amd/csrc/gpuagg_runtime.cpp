@@ -3857,6 +3857,7 @@ struct gpuagg_raw_feed {
   int kind = 0;
   size_t rec = 0, cap = 0;         // bytes per record, records per device staging
   std::vector<uint8_t *> buf;      // pinned (CPU backend: host) staging, one per context
+  std::vector<gpuagg_batch *> bat; // GPUAGG_RECORD: each context's pinned SoA batch
   std::vector<size_t> fill;        // records staged per context
   std::vector<uint32_t> shard;     // scratch: the device of each record of one piece
   std::vector<uint64_t> submitted; // records handed to each context so far
@@ -3865,9 +3866,10 @@ struct gpuagg_raw_feed {
 namespace {
 int feed_submit(gpuagg_raw_feed *f, size_t d) {
   if (!f->fill[d]) return GPUAGG_OK;
-  // gpuagg_submit_raw returns once the H2D copy (a DMA: the staging is pinned) is done,
+  // gpuagg_submit(_raw) returns once the H2D copy (a DMA: the staging is pinned) is done,
   // so the staging is refilled while the device decodes and aggregates it
-  const int rc = gpuagg_submit_raw(f->ctxs[d], f->kind, f->buf[d], f->fill[d]);
+  const int rc = f->kind == GPUAGG_RECORD ? gpuagg_submit(f->ctxs[d], f->bat[d], f->fill[d])
+                                          : gpuagg_submit_raw(f->ctxs[d], f->kind, f->buf[d], f->fill[d]);
   if (rc == GPUAGG_OK) f->submitted[d] += f->fill[d];
   f->fill[d] = 0;
   return rc;
@@ -3876,7 +3878,21 @@ int feed_submit(gpuagg_raw_feed *f, size_t d) {
 void feed_free(gpuagg_raw_feed *f) {
   for (size_t d = 0; d < f->buf.size(); ++d)
     if (f->buf[d]) x_host_free(f->ctxs[d], f->buf[d]);
+  for (size_t d = 0; d < f->bat.size(); ++d)
+    if (f->bat[d]) gpuagg_free_batch(f->ctxs[d], f->bat[d]);
   delete f;
+}
+
+// One decoded record into position i of a SoA batch.
+inline void put_record(gpuagg_batch *b, size_t i, const gpuagg_record &r) {
+  b->cols.src_ip[i] = r.src_ip;
+  b->cols.dst_ip[i] = r.dst_ip;
+  b->cols.bytes[i] = r.bytes;
+  b->cols.meta[i] = r.meta;
+  b->cols.ports[i] = r.ports;
+  b->cols.dns_id[i] = r.dns_id;
+  b->cols.tcp_id[i] = r.tcp_id;
+  b->cols.time_ns[i] = r.time_ns;
 }
 }  // namespace
 
@@ -3884,20 +3900,29 @@ extern "C" {
 
 int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
                            gpuagg_raw_feed **out) {
-  if (!ctxs || !n_ctx || !out || !capacity || (kind != kRawPacket && kind != kRawDrop)) return GPUAGG_EINVAL;
+  if (!ctxs || !n_ctx || !out || !capacity || (kind != kRawPacket && kind != kRawDrop && kind != GPUAGG_RECORD))
+    return GPUAGG_EINVAL;
   *out = nullptr;
   for (size_t d = 0; d < n_ctx; ++d)
     if (!ctxs[d]) return GPUAGG_EINVAL;
   auto *f = new gpuagg_raw_feed();
   f->ctxs.assign(ctxs, ctxs + n_ctx);
   f->kind = kind;
-  f->rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
+  f->rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : kind == kRawDrop ? GPUAGG_RAW_DROP_SIZE : sizeof(gpuagg_record);
   f->cap = capacity;
   f->buf.assign(n_ctx, nullptr);
+  f->bat.assign(n_ctx, nullptr);
   f->fill.assign(n_ctx, 0);
   f->submitted.assign(n_ctx, 0);
   for (size_t d = 0; d < n_ctx; ++d) {
     gpuagg_ctx *c = ctxs[d];
+    if (kind == GPUAGG_RECORD) {  // the context's own pinned SoA batch (gpuagg_submit)
+      if (int rc = gpuagg_alloc_batch(c, capacity, &f->bat[d])) {
+        feed_free(f);
+        return rc;
+      }
+      continue;
+    }
     if (bind(c) || x_host_alloc(c, (void **)&f->buf[d], capacity * f->rec) != hipSuccess) {
       fail(c, GPUAGG_ENOMEM, "raw feed staging (%zu records)", capacity);
       feed_free(f);
@@ -3919,6 +3944,16 @@ int gpuagg_raw_feed_put(gpuagg_raw_feed *f, const void *raw, size_t n) {
   const uint8_t *p = (const uint8_t *)raw;
   const size_t nd = f->ctxs.size(), rec = f->rec;
   int err = GPUAGG_OK;
+  if (f->kind == GPUAGG_RECORD) {  // decoded records: shard and transpose into the SoA batches
+    const gpuagg_record *r = (const gpuagg_record *)raw;
+    for (size_t i = 0; i < n; ++i) {
+      const size_t d = nd == 1 ? 0 : shard_one(r[i].src_ip, r[i].dst_ip, r[i].ports, r[i].meta, (uint32_t)nd);
+      put_record(f->bat[d], f->fill[d], r[i]);
+      if (++f->fill[d] == f->cap)
+        if (int rc = feed_submit(f, d)) err = err ? err : rc;
+    }
+    return err;
+  }
   if (nd == 1) {  // one device: straight into its staging
     while (n) {
       const size_t m = std::min(n, f->cap - f->fill[0]);

@@ -468,10 +468,30 @@ class GpuAgg:
         self._check(self.lib.gpuagg_set_timing(self.h, 1 if enabled else 0))
 
 
+# struct gpuagg_record (include/gpuagg.h): the Go plugin's Record, back to back
+RECORD_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("bytes", "<u4"), ("meta", "<u4"),
+                         ("ports", "<u4"), ("dns_id", "<u4"), ("tcp_id", "<u4"), ("pad_", "<u4"),
+                         ("time_ns", "<u8")])
+
+
+def records_aos(recs) -> np.ndarray:
+    """W.Records (SoA) -> gpuagg_record array (AoS), as the Go plugin holds them."""
+    n = len(recs.src_ip)
+    a = np.zeros(n, RECORD_DTYPE)
+    for k in ("src_ip", "dst_ip", "bytes", "meta", "ports", "dns_id"):
+        a[k] = getattr(recs, k)
+    if getattr(recs, "tcp_id", None) is not None:
+        a["tcp_id"] = recs.tcp_id
+    if getattr(recs, "time_ns", None) is not None:
+        a["time_ns"] = recs.time_ns
+    return a
+
+
 class RawFeed:
-    """Node-wide raw ingestion over one context per device (gpuagg_raw_feed_*): samples are
-    sharded by the 5-tuple (gpuagg_shard_raw's function) and copied into each context's
-    pinned staging in the library; full stagings are submitted as they fill."""
+    """Node-wide ingestion over one context per device (gpuagg_raw_feed_*): raw perf samples
+    (kind RAW_PACKET / RAW_DROP) or decoded gpuagg_record arrays (RECORD) are sharded by the
+    5-tuple (gpuagg_shard_raw's / gpuagg_shard_columns' function) and copied into each
+    context's pinned staging in the library; full stagings are submitted as they fill."""
 
     def __init__(self, engines, kind: int, capacity: int = 1 << 20):
         self.engines = list(engines)

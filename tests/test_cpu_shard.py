@@ -112,3 +112,37 @@ def test_raw_feed_rejects_bad_args(lib):
     assert lib.gpuagg_raw_feed_create(arr, 1, _abi.RAW_PACKET, 16, C.byref(h)) == _abi.EINVAL
     assert lib.gpuagg_raw_feed_put(None, None, 0) == _abi.EINVAL
     assert lib.gpuagg_raw_feed_flush(None) == _abi.EINVAL
+
+
+@pytest.mark.parametrize("world,cap", [(1, 7_000), (3, 2_048)])
+def test_record_feed_scatter(lib, world, cap):
+    """GPUAGG_RECORD feed (the Go plugin's WriteBatch slices of Record): AoS records sharded
+    by gpuagg_shard_columns' function and transposed into each context's pinned SoA batch;
+    every context's series equal the oracle over its shard."""
+    from retina_amd import RawFeed, _abi
+    from retina_amd.engine import records_aos
+    from .helpers import diff_series, make_engine, oracle_series
+    pods = W.make_pods(300, seed=31)
+    sp = [{"metric_name": m, "source_labels": ["namespace", "podname"]}
+          for m in ("forward_count", "forward_bytes", "drop_count", "drop_bytes")]
+    recs = W.gen_records(20_000, pods, seed=32, drop_frac=0.2, udp_frac=0.1)
+    aos = records_aos(recs)
+    shard = dist.shard_of(recs.src_ip, recs.dst_ip, recs.ports, recs.meta, world)
+    engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(world)]
+    feed = RawFeed(engines, _abi.RECORD, capacity=cap)
+    try:
+        for a in range(0, len(aos), 3_000):
+            feed.put(aos[a:a + 3_000])
+        feed.flush()
+        assert feed.submitted() == [int((shard == d).sum()) for d in range(world)]
+        for d, g in enumerate(engines):
+            m = shard == d
+            part = W.Records(recs.src_ip[m], recs.dst_ip[m], recs.bytes[m], recs.meta[m], recs.ports[m],
+                             recs.dns_id[m])
+            want = oracle_series(part, pods, sp, False)
+            got = g.snapshot()
+            assert got == want, diff_series(got, want)
+    finally:
+        feed.close()
+        for g in engines:
+            g.close()
