@@ -2775,6 +2775,13 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     slot_canon(c->groups[v.group].dst_opts);
   }
   auto cid = [&](const SlotCanon &sc, uint32_t slot1) { return sc.id[slot1 < sc.id.size() ? slot1 : 0]; };
+  // each viewed group's canonical tables, looked up once
+  std::vector<const SlotCanon *> src_canon(c->groups.size(), nullptr), dst_canon(c->groups.size(), nullptr);
+  for (const View &v : views) {
+    const Group &g = c->groups[v.group];
+    src_canon[v.group] = &canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
+    dst_canon[v.group] = &canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL));
+  }
   // canonical DNS payloads: request series (qtypes, query), response series (rcode name,
   // qtypes, query, ips, answers)
   std::vector<uint32_t> dns_req, dns_resp, dns_req_rep, dns_resp_rep;
@@ -2851,12 +2858,12 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
         k.w[1] = pre;
         if (v.src) {
           k.w[2] = (g.src_opts & OPT_IP) ? key_s_ip(w[0]) : 0u;
-          k.w[3] = cid(canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL)), key_s_slot1(w[0]));
+          k.w[3] = cid(*src_canon[grp], key_s_slot1(w[0]));
           k.w[4] = (g.src_opts & OPT_PORT) ? key_s_port17(w[1]) : 0u;
         }
         if (v.dst) {
           k.w[5] = (g.dst_opts & OPT_IP) ? key_d_ip(w[2]) : 0u;
-          k.w[6] = cid(canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL)), key_d_slot1(w[1]));
+          k.w[6] = cid(*dst_canon[grp], key_d_slot1(w[1]));
           k.w[7] = (g.dst_opts & OPT_PORT) ? key_d_port17(w[1]) : 0u;
         }
         put(t, k, w[3], w[4]);
@@ -2866,7 +2873,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     for (size_t gi = 0; gi < c->groups.size(); ++gi) {
       const Group &g = c->groups[gi];
       if (g.sparse || group_views[gi].empty()) continue;
-      const SlotCanon &sc = canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
+      const SlotCanon &sc = *src_canon[gi];
       const uint64_t k0 = g.nkeys * t / T, k1 = g.nkeys * (t + 1) / T;
       for (uint64_t key = k0; key < k1; ++key)
         for (uint32_t side = 0; side < 2; ++side)
@@ -2937,14 +2944,8 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
             break;
           }
         }
-        if (v.src) {
-          const SlotCanon &sc = canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
-          ctx_values_into(c, g.src_opts, k.w[2], sc.rep[k.w[3]], k.w[4], ar);
-        }
-        if (v.dst) {
-          const SlotCanon &sc = canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL));
-          ctx_values_into(c, g.dst_opts, k.w[5], sc.rep[k.w[6]], k.w[7], ar);
-        }
+        if (v.src) ctx_values_into(c, g.src_opts, k.w[2], src_canon[v.group]->rep[k.w[3]], k.w[4], ar);
+        if (v.dst) ctx_values_into(c, g.dst_opts, k.w[5], dst_canon[v.group]->rep[k.w[6]], k.w[7], ar);
       }
     }
   });
