@@ -13,6 +13,8 @@ OUT="$R/gpurun_out"
 mkdir -p "$OUT"
 { rocminfo | grep -m2 -E "Name: +gfx|Marketing Name: +AMD Instinct"; nproc; lscpu | grep "Model name"; } > "$OUT/${TAG}_info.txt" 2>&1
 export TMPDIR=/tmp
+# generated workloads are cached across this session's bench / prof / pmc runs (bench.py)
+export BENCH_CACHE=/tmp/benchcache_$TAG
 for s in $STEPS; do
   name=${s%%:*}
   arg=""
