@@ -382,9 +382,9 @@ func (g *gpuAgg) Init() error {
 	// decoded records (Write / WriteBatch) go through a GPUAGG_RECORD feed: one cgo call per
 	// slice shards them and transposes them into each device's pinned SoA batch in C (the
 	// Record layout is struct gpuagg_record's)
-	if unsafe.Sizeof(Record{}) != C.sizeof_gpuagg_record {
+	if unsafe.Sizeof(Record{}) != uintptr(C.sizeof_gpuagg_record) {
 		g.destroyLocked()
-		return fmt.Errorf("gpuagg: Record is %d bytes, gpuagg_record %d", unsafe.Sizeof(Record{}), C.sizeof_gpuagg_record)
+		return fmt.Errorf("gpuagg: Record is %d bytes, gpuagg_record %d", unsafe.Sizeof(Record{}), int(C.sizeof_gpuagg_record))
 	}
 	if err := check(ctxs[0], C.gpuagg_raw_feed_create(&ctxs[0], C.size_t(len(ctxs)), C.GPUAGG_RECORD,
 		batchCapacity, &g.recFeed), "gpuagg_raw_feed_create(records)"); err != nil {
