@@ -115,6 +115,14 @@ struct SeriesRec {
   uint64_t value;
 };
 
+// Canonical ids of the slot attributes a side's options render (namespace / pod /
+// workload; the service label is constant): id[slot1] (slot1 0 or past the table:
+// "unknown") and a representative slot1 per id; rebuilt when the slots change.
+struct SlotCanon {
+  std::vector<uint32_t> id, rep;
+  uint64_t version = ~0ull;
+};
+
 struct ResultFamily {
   std::string metric;
   std::vector<std::string> names;
@@ -203,6 +211,13 @@ struct gpuagg_ctx {
   std::unordered_map<uint32_t, std::string> ip_to_svc, ip_to_node;
   std::unordered_map<std::string, uint32_t> dns_ids;
   std::vector<DnsAttr> dns;
+  // label-canonical DNS payloads, kept at intern time: request series render (qtypes,
+  // query), response series (rcode name, qtypes, query, ips, answers)
+  std::unordered_map<std::string, uint32_t> dns_req_canon, dns_resp_canon;
+  std::vector<uint32_t> dns_req_id, dns_resp_id, dns_req_rep, dns_resp_rep;
+  // canonical slot attributes per option mask (snapshot), valid for slots_version
+  std::map<uint8_t, SlotCanon> slot_canon;
+  uint64_t slots_version = 0;
 
   // IP table
   uint64_t *d_ip = nullptr;
@@ -2012,6 +2027,7 @@ int gpuagg_slot_intern(gpuagg_ctx *c, const char *ns, const char *pod, const cha
     id = (int32_t)c->slots.size();
     c->slots.push_back(a);
   }
+  ++c->slots_version;
   c->slot_ids.emplace(key, id);
   *slot = id;
   return GPUAGG_OK;
@@ -2414,6 +2430,7 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
     a.in_use = false;
     c->free_slots.push_back((int32_t)s);
   }
+  ++c->slots_version;
   std::sort(c->free_slots.begin(), c->free_slots.end(), std::greater<int32_t>());  // lowest id first
   if (n_retired) *n_retired = dead.size();
   return GPUAGG_OK;
@@ -2433,6 +2450,15 @@ int gpuagg_dns_intern(gpuagg_ctx *c, uint32_t rcode, const char *qtypes, const c
   const uint32_t nid = (uint32_t)c->dns.size();
   c->dns.push_back(DnsAttr{rcode, nresp, qtypes, query, ips});
   c->dns_ids.emplace(std::move(key), nid);
+  const std::string q = std::string(qtypes) + '\0' + query;
+  auto i1 = c->dns_req_canon.emplace(q, (uint32_t)c->dns_req_rep.size());
+  if (i1.second) c->dns_req_rep.push_back(nid);
+  c->dns_req_id.push_back(i1.first->second);
+  const std::string full = std::string(rcode < 6 ? kRcodeNames[rcode] : "") + '\0' + q + '\0' + ips + '\0' +
+                           std::to_string(nresp);
+  auto i2 = c->dns_resp_canon.emplace(full, (uint32_t)c->dns_resp_rep.size());
+  if (i2.second) c->dns_resp_rep.push_back(nid);
+  c->dns_resp_id.push_back(i2.first->second);
   *id = nid;
   return GPUAGG_OK;
 }
@@ -2668,13 +2694,6 @@ struct LItem {
   uint64_t cnt, byt;
 };
 
-// Canonical ids of the slot attributes a side's options render (namespace / pod /
-// workload; the service label is constant): csa[slot1] (slot1 0 or past the table:
-// "unknown"), and a representative slot1 per id.
-struct SlotCanon {
-  std::vector<uint32_t> id, rep;
-};
-
 void append_str(std::vector<char> &a, const char *s, size_t n) {
   a.insert(a.end(), s, s + n);
   a.push_back('\0');
@@ -2751,23 +2770,29 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     views[v].insts.push_back((uint32_t)ii);
   }
   if (views.empty()) return GPUAGG_OK;
-  // canonical slot attributes per option mask
-  std::map<uint8_t, SlotCanon> canon;
+  // canonical slot attributes per option mask (cached until the slots change)
+  std::map<uint8_t, SlotCanon> &canon = c->slot_canon;
   auto slot_canon = [&](uint8_t opts) -> const SlotCanon & {
     const uint8_t m = opts & (OPT_NS | OPT_POD | OPT_WL);
-    auto it = canon.find(m);
-    if (it != canon.end()) return it->second;
     SlotCanon &sc = canon[m];
-    std::unordered_map<std::string, uint32_t> ids;
-    std::vector<char> buf;
-    sc.id.resize(c->slots.size() + 1);
-    for (uint32_t s1 = 0; s1 <= c->slots.size(); ++s1) {
-      buf.clear();
-      ctx_values_into(c, m, 0, s1, 0, buf);
-      auto ins = ids.emplace(std::string(buf.begin(), buf.end()), (uint32_t)sc.rep.size());
-      if (ins.second) sc.rep.push_back(s1);
-      sc.id[s1] = ins.first->second;
+    if (sc.version == c->slots_version) return sc;
+    sc.id.assign(c->slots.size() + 1, 0u);
+    sc.rep.clear();
+    if (!(m & (OPT_NS | OPT_POD | OPT_WL))) {  // nothing slot-derived: one id
+      sc.rep.push_back(0u);
+    } else {
+      std::unordered_map<std::string, uint32_t> ids;
+      ids.reserve(c->slots.size() + 1);
+      std::vector<char> buf;
+      for (uint32_t s1 = 0; s1 <= c->slots.size(); ++s1) {
+        buf.clear();
+        ctx_values_into(c, m, 0, s1, 0, buf);
+        auto ins = ids.emplace(std::string(buf.begin(), buf.end()), (uint32_t)sc.rep.size());
+        if (ins.second) sc.rep.push_back(s1);
+        sc.id[s1] = ins.first->second;
+      }
     }
+    sc.version = c->slots_version;
     return sc;
   };
   for (const View &v : views) {
@@ -2782,29 +2807,9 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     src_canon[v.group] = &canon.at(g.src_opts & (OPT_NS | OPT_POD | OPT_WL));
     dst_canon[v.group] = &canon.at(g.dst_opts & (OPT_NS | OPT_POD | OPT_WL));
   }
-  // canonical DNS payloads: request series (qtypes, query), response series (rcode name,
-  // qtypes, query, ips, answers)
-  std::vector<uint32_t> dns_req, dns_resp, dns_req_rep, dns_resp_rep;
-  bool any_dns = false;
-  for (const View &v : views)
-    any_dns |= c->groups[v.group].family == FAM_DNS_REQ || c->groups[v.group].family == FAM_DNS_RESP;
-  if (any_dns) {
-    std::unordered_map<std::string, uint32_t> rq, rs;
-    dns_req.resize(c->dns.size());
-    dns_resp.resize(c->dns.size());
-    for (size_t k = 0; k < c->dns.size(); ++k) {
-      const DnsAttr &a = c->dns[k];
-      const std::string q = a.qtypes + '\0' + a.query;
-      auto i1 = rq.emplace(q, (uint32_t)dns_req_rep.size());
-      if (i1.second) dns_req_rep.push_back((uint32_t)k);
-      dns_req[k] = i1.first->second;
-      const std::string full = std::string(a.rcode < 6 ? kRcodeNames[a.rcode] : "") + '\0' + q + '\0' + a.ips + '\0' +
-                               std::to_string(a.nresp);
-      auto i2 = rs.emplace(full, (uint32_t)dns_resp_rep.size());
-      if (i2.second) dns_resp_rep.push_back((uint32_t)k);
-      dns_resp[k] = i2.first->second;
-    }
-  }
+  // canonical DNS payloads (kept by gpuagg_dns_intern)
+  const std::vector<uint32_t> &dns_req = c->dns_req_id, &dns_resp = c->dns_resp_id;
+  const std::vector<uint32_t> &dns_req_rep = c->dns_req_rep, &dns_resp_rep = c->dns_resp_rep;
   // items: one per (counter, view), partitioned by key hash
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t work = nent + (size_t)c->dense_len;
@@ -2949,26 +2954,36 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
       }
     }
   });
-  size_t ns = 0;
-  for (auto &o : out) ns += o.size();
-  r->series.reserve(ns);
-  for (auto &o : out) r->series.insert(r->series.end(), o.begin(), o.end());
-  // label value pointers (the arenas are final now)
+  // concatenate the partitions and point at each series' label values (the arenas are
+  // final now), partition by partition on the same threads
+  std::vector<size_t> sbase(T + 1, 0);
+  std::vector<uint64_t> vbase(T + 1, 0);
+  for (unsigned p = 0; p < T; ++p) {
+    uint64_t nv = 0;
+    for (const SeriesRec &sr : out[p]) nv += r->fam[sr.fam].names.size();
+    sbase[p + 1] = sbase[p] + out[p].size();
+    vbase[p + 1] = vbase[p] + nv;
+  }
+  const size_t ns = sbase[T];
+  r->series.resize(ns);
   r->voff.resize(ns + 1);
-  uint64_t nv = 0;
-  for (size_t i = 0; i < ns; ++i) {
-    r->voff[i] = nv;
-    nv += r->fam[r->series[i].fam].names.size();
-  }
-  r->voff[ns] = nv;
-  r->value_ptrs.resize(nv);
-  for (size_t i = 0; i < ns; ++i) {
-    const char *q = r->arenas[r->series[i].arena].data() + r->series[i].off;
-    for (uint64_t k = r->voff[i]; k < r->voff[i + 1]; ++k) {
-      r->value_ptrs[k] = q;
-      q += strlen(q) + 1;
+  r->value_ptrs.resize(vbase[T]);
+  r->voff[ns] = vbase[T];
+  run([&](unsigned p) {
+    uint64_t k = vbase[p];
+    const char *ar = r->arenas[p].data();
+    for (size_t i = 0; i < out[p].size(); ++i) {
+      const SeriesRec &sr = out[p][i];
+      r->series[sbase[p] + i] = sr;
+      r->voff[sbase[p] + i] = k;
+      const char *q = ar + sr.off;
+      for (size_t j = 0, nn = r->fam[sr.fam].names.size(); j < nn; ++j) {
+        r->value_ptrs[k++] = q;
+        q += strlen(q) + 1;
+      }
     }
-  }
+    std::vector<SeriesRec>().swap(out[p]);
+  });
   return GPUAGG_OK;
 }
 
@@ -3170,96 +3185,280 @@ void escape_cstr(std::string &out, const char *s, bool quote) {  // expfmt escap
   }
 }
 void escape_into(std::string &out, const std::string &s, bool quote) { escape_cstr(out, s.c_str(), quote); }
+
+extern "C++" {
+// run fn(t) for t < n on n threads (inline when n == 1)
+template <class F>
+void run_par(unsigned n, F &&fn) {
+  if (n <= 1) {
+    fn(0u);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < n; ++t) th.emplace_back(fn, t);
+  for (auto &x : th) x.join();
+}
+
+// Sample sort on T threads: T-1 splitters from an even sample, each thread buckets its
+// slice, buckets are sorted independently and land in order.
+template <class E, class L>
+void par_sort(std::vector<E> &v, L less, unsigned T) {
+  const size_t n = v.size();
+  if (T <= 1 || n < 65536) {
+    std::sort(v.begin(), v.end(), less);
+    return;
+  }
+  const size_t ov = 64;
+  std::vector<E> smp;
+  smp.reserve((size_t)T * ov);
+  for (size_t i = 0; i < (size_t)T * ov; ++i) smp.push_back(v[i * n / ((size_t)T * ov)]);
+  std::sort(smp.begin(), smp.end(), less);
+  std::vector<E> sp;
+  for (unsigned j = 1; j < T; ++j) sp.push_back(smp[j * ov]);
+  std::vector<uint32_t> bk(n);
+  std::vector<size_t> cnt((size_t)T * T, 0);  // [thread][bucket]
+  run_par(T, [&](unsigned t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      const uint32_t b = (uint32_t)(std::upper_bound(sp.begin(), sp.end(), v[i], less) - sp.begin());
+      bk[i] = b;
+      ++cnt[(size_t)t * T + b];
+    }
+  });
+  std::vector<size_t> off((size_t)T * T), bstart(T + 1, 0);
+  size_t o = 0;
+  for (unsigned b = 0; b < T; ++b) {
+    bstart[b] = o;
+    for (unsigned t = 0; t < T; ++t) {
+      off[(size_t)t * T + b] = o;
+      o += cnt[(size_t)t * T + b];
+    }
+  }
+  bstart[T] = o;
+  std::vector<E> tmp(n);
+  run_par(T, [&](unsigned t) {
+    size_t *po = &off[(size_t)t * T];
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) tmp[po[bk[i]]++] = v[i];
+  });
+  run_par(T, [&](unsigned b) { std::sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1], less); });
+  v.swap(tmp);
+}
+}  // extern "C++"
+
+struct SvKey {
+  const char *p;
+  uint32_t n;
+  uint64_t h;
+  bool operator==(const SvKey &o) const { return n == o.n && memcmp(p, o.p, n) == 0; }
+};
+struct SvKeyHash {
+  size_t operator()(const SvKey &k) const { return (size_t)k.h; }
+};
+
+// Series of one family in exposition order (client_golang sorts a family's metrics by
+// their label values taken in label-name order; MetricSorter): every value is replaced by
+// its rank among the family's distinct values (string order), so the sort compares
+// integers -- one packed 128-bit key when the ranks fit, else rank rows.
+void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size_t> &idx, unsigned T) {
+  const size_t n = idx.size(), nl = F.names.size();
+  if (n < 2 || nl == 0) return;
+  const size_t ne = n * nl;
+  std::vector<uint64_t> hv(ne);
+  std::vector<uint32_t> ln(ne), rk(ne);
+  run_par(T, [&](unsigned t) {
+    for (size_t q = n * t / T; q < n * (t + 1) / T; ++q) {
+      const char *const *v = r->value_ptrs.data() + r->voff[idx[q]];
+      for (size_t k = 0; k < nl; ++k) {
+        const char *s = v[F.by_name[k]];
+        const size_t m = strlen(s);
+        ln[q * nl + k] = (uint32_t)m;
+        hv[q * nl + k] = std::hash<std::string_view>()(std::string_view(s, m));
+      }
+    }
+  });
+  auto val = [&](size_t e) { return r->value_ptrs[r->voff[idx[e / nl]] + F.by_name[e % nl]]; };
+  // distinct values, partitioned by hash over the threads: dist[t] owns h % T == t
+  std::vector<std::vector<SvKey>> dist(T);
+  run_par(T, [&](unsigned t) {
+    std::unordered_map<SvKey, uint32_t, SvKeyHash> m;
+    for (size_t e = 0; e < ne; ++e) {
+      if (hv[e] % T != t) continue;
+      const SvKey k{val(e), ln[e], hv[e]};
+      auto ins = m.emplace(k, (uint32_t)dist[t].size());
+      if (ins.second) dist[t].push_back(k);
+      rk[e] = ins.first->second;  // local id for now
+    }
+  });
+  std::vector<std::pair<SvKey, uint32_t>> all;  // (value, owner thread << 0 | local id)
+  std::vector<size_t> dbase(T + 1, 0);
+  for (unsigned t = 0; t < T; ++t) dbase[t + 1] = dbase[t] + dist[t].size();
+  all.reserve(dbase[T]);
+  for (unsigned t = 0; t < T; ++t)
+    for (size_t i = 0; i < dist[t].size(); ++i) all.push_back({dist[t][i], (uint32_t)(dbase[t] + i)});
+  par_sort(all, [](const std::pair<SvKey, uint32_t> &a, const std::pair<SvKey, uint32_t> &b) {
+    const int c = memcmp(a.first.p, b.first.p, std::min(a.first.n, b.first.n));
+    return c ? c < 0 : a.first.n < b.first.n;
+  }, T);
+  std::vector<uint32_t> rank(dbase[T]);
+  for (size_t i = 0; i < all.size(); ++i) rank[all[i].second] = (uint32_t)i;
+  run_par(T, [&](unsigned t) {
+    for (size_t e = ne * t / T; e < ne * (t + 1) / T; ++e) rk[e] = rank[dbase[hv[e] % T] + rk[e]];
+  });
+  unsigned bits = 1;
+  while (bits < 32 && (1ull << bits) < all.size()) ++bits;
+  const std::vector<size_t> old = idx;
+  if (nl * bits <= 128) {
+    using K = std::pair<unsigned __int128, uint32_t>;
+    std::vector<K> keys(n);
+    run_par(T, [&](unsigned t) {
+      for (size_t q = n * t / T; q < n * (t + 1) / T; ++q) {
+        unsigned __int128 x = 0;
+        for (size_t k = 0; k < nl; ++k) x = (x << bits) | rk[q * nl + k];
+        keys[q] = K{x, (uint32_t)q};
+      }
+    });
+    par_sort(keys, [](const K &a, const K &b) { return a.first < b.first; }, T);
+    for (size_t q = 0; q < n; ++q) idx[q] = old[keys[q].second];
+  } else {
+    std::vector<uint32_t> ord(n);
+    for (size_t q = 0; q < n; ++q) ord[q] = (uint32_t)q;
+    par_sort(ord, [&](uint32_t a, uint32_t b) {
+      const uint32_t *x = &rk[(size_t)a * nl], *y = &rk[(size_t)b * nl];
+      for (size_t k = 0; k < nl; ++k)
+        if (x[k] != y[k]) return x[k] < y[k];
+      return false;
+    }, T);
+    for (size_t q = 0; q < n; ++q) idx[q] = old[ord[q]];
+  }
+}
+
+// expfmt escaping of a label value into a raw buffer sized for the worst case (2x)
+inline char *escape_raw(char *o, const char *s) {
+  for (; *s; ++s) {
+    const char ch = *s;
+    if (ch == '\\' || ch == '"') {
+      *o++ = '\\';
+      *o++ = ch;
+    } else if (ch == '\n') {
+      *o++ = '\\';
+      *o++ = 'n';
+    } else {
+      *o++ = ch;
+    }
+  }
+  return o;
+}
+
+// gpuagg_result_render_text's text, built once per result: families sorted by name
+// (expfmt), each family's series in client_golang's order, rendered in parallel chunks
+// and copied into place in parallel.
+void render_text(const gpuagg_result *r) {
+  std::vector<std::vector<size_t>> by_fam(r->fam.size());
+  for (size_t i = 0; i < r->series.size(); ++i) by_fam[r->series[i].fam].push_back(i);
+  std::map<std::string, size_t> fam;  // metric name -> family
+  for (size_t f = 0; f < by_fam.size(); ++f)
+    if (!by_fam[f].empty()) fam[r->fam[f].metric] = f;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  // pieces in output order: (pointer, size); text they point at lives in `store`
+  std::vector<std::pair<const char *, size_t>> piece;
+  std::vector<std::unique_ptr<std::string>> store;
+  std::map<std::string, int> names;  // every family name, extra blocks included
+  for (auto &kv : r->extra_text) names[kv.first] = 0;
+  for (auto &kv : fam) names[kv.first] = 0;
+  for (auto &nk : names) {
+    auto ex = r->extra_text.find(nk.first);
+    if (ex != r->extra_text.end()) piece.push_back({ex->second.data(), ex->second.size()});
+    auto fi = fam.find(nk.first);
+    if (fi == fam.end()) continue;
+    std::vector<size_t> &idx = by_fam[fi->second];
+    const ResultFamily &F = r->fam[fi->second];
+    const size_t nl = F.names.size();
+    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 8192 + 1}));
+    sort_family(r, F, idx, T);
+    // label prefixes: {name=" then ",name=" ; closed by "}
+    std::vector<std::string> lab(nl);
+    for (size_t k = 0; k < nl; ++k) lab[k] = (k ? "\"," : "{") + F.names[F.by_name[k]] + "=\"";
+    auto head = std::make_unique<std::string>("# HELP " + nk.first + " ");
+    escape_cstr(*head, F.help, false);
+    *head += "\n# TYPE " + nk.first + " " + F.type + "\n";
+    piece.push_back({head->data(), head->size()});
+    store.push_back(std::move(head));
+    std::vector<std::unique_ptr<std::string>> chunk(T);
+    for (auto &c : chunk) c = std::make_unique<std::string>();
+    run_par(T, [&](unsigned t) {
+      const size_t q0 = idx.size() * t / T, q1 = idx.size() * (t + 1) / T;
+      size_t bound = 0;
+      for (size_t q = q0; q < q1; ++q) {
+        const char *const *v = r->value_ptrs.data() + r->voff[idx[q]];
+        bound += F.metric.size() + 2 + 32;
+        for (size_t k = 0; k < nl; ++k) bound += lab[k].size() + 2 * strlen(v[F.by_name[k]]);
+      }
+      std::string &o = *chunk[t];
+      o.resize(bound);
+      char *w = &o[0];
+      for (size_t q = q0; q < q1; ++q) {
+        const size_t i = idx[q];
+        memcpy(w, F.metric.data(), F.metric.size());
+        w += F.metric.size();
+        const char *const *v = r->value_ptrs.data() + r->voff[i];
+        for (size_t k = 0; k < nl; ++k) {
+          memcpy(w, lab[k].data(), lab[k].size());
+          w += lab[k].size();
+          w = escape_raw(w, v[F.by_name[k]]);
+        }
+        if (nl) {
+          *w++ = '"';
+          *w++ = '}';
+        }
+        *w++ = ' ';
+        const uint64_t x = r->series[i].value;
+        if (x < 1000000) {  // plain integer digits (go_float_u64_into's short case)
+          char d[8];
+          int m = 0;
+          uint64_t y = x;
+          do {
+            d[m++] = (char)('0' + y % 10);
+            y /= 10;
+          } while (y);
+          while (m) *w++ = d[--m];
+        } else {
+          std::string f;
+          go_float_u64_into(f, x);
+          memcpy(w, f.data(), f.size());
+          w += f.size();
+        }
+        *w++ = '\n';
+      }
+      o.resize((size_t)(w - o.data()));
+    });
+    for (auto &c : chunk) {
+      piece.push_back({c->data(), c->size()});
+      store.push_back(std::move(c));
+    }
+  }
+  std::vector<size_t> at(piece.size() + 1, 0);
+  for (size_t i = 0; i < piece.size(); ++i) at[i + 1] = at[i] + piece[i].second;
+  std::string &out = r->text;
+  out.resize(at[piece.size()]);
+  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, out.size() / (1u << 22) + 1}));
+  run_par(T, [&](unsigned t) {  // byte range [t * N / T, (t + 1) * N / T) of the output
+    const size_t b0 = out.size() * t / T, b1 = out.size() * (t + 1) / T;
+    size_t i = std::upper_bound(at.begin(), at.end(), b0) - at.begin() - 1;
+    for (; i < piece.size() && at[i] < b1; ++i) {
+      const size_t s0 = std::max(b0, at[i]), s1 = std::min(b1, at[i + 1]);
+      if (s1 > s0) memcpy(&out[s0], piece[i].first + (s0 - at[i]), s1 - s0);
+    }
+  });
+  r->text_done = true;
+}
 }  // namespace
 
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
   if (!r || !len) return GPUAGG_EINVAL;
-  if (r->text_done) {
-    *len = r->text.size();
-    if (!buf) return GPUAGG_OK;
-    if (cap < r->text.size() + 1) return GPUAGG_ECAPACITY;
-    memcpy(buf, r->text.c_str(), r->text.size() + 1);
-    return GPUAGG_OK;
-  }
-  // families by name; within one, series sorted by their label values taken in label
-  // name order (client_golang keeps a metric's pairs sorted by name; MetricSorter) --
-  // sorted in parallel chunks, merged, then rendered in parallel chunks
-  std::vector<std::vector<size_t>> by_fam(r->fam.size());
-  for (size_t i = 0; i < r->series.size(); ++i) by_fam[r->series[i].fam].push_back(i);
-  std::map<std::string, std::vector<size_t>> fam;
-  for (size_t f = 0; f < by_fam.size(); ++f)
-    if (!by_fam[f].empty()) fam[r->fam[f].metric] = std::move(by_fam[f]);
-  std::map<std::string, std::string> blocks = r->extra_text;  // family name -> text
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  for (auto &kv : fam) {
-    auto &idx = kv.second;
-    const ResultFamily &F = r->fam[r->series[idx[0]].fam];
-    const size_t nl = F.names.size();
-    auto less = [&](size_t a, size_t b) {
-      const char *const *va = r->value_ptrs.data() + r->voff[a], *const *vb = r->value_ptrs.data() + r->voff[b];
-      for (size_t k = 0; k < nl; ++k) {
-        const int c = strcmp(va[F.by_name[k]], vb[F.by_name[k]]);
-        if (c) return c < 0;
-      }
-      return false;
-    };
-    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 8192 + 1}));
-    std::vector<size_t> cut(T + 1);
-    for (unsigned t = 0; t <= T; ++t) cut[t] = idx.size() * t / T;
-    auto par = [&](unsigned n, auto &&fn) {
-      if (n == 1) {
-        fn(0u);
-        return;
-      }
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < n; ++t) th.emplace_back(fn, t);
-      for (auto &x : th) x.join();
-    };
-    par(T, [&](unsigned t) { std::sort(idx.begin() + cut[t], idx.begin() + cut[t + 1], less); });
-    for (size_t w = 1; w < T; w *= 2)  // pairwise merges of sorted runs
-      for (size_t a = 0; a + w < T; a += 2 * w)
-        std::inplace_merge(idx.begin() + cut[a], idx.begin() + cut[a + w], idx.begin() + cut[std::min<size_t>(a + 2 * w, T)], less);
-    std::vector<std::string> chunk(T);
-    par(T, [&](unsigned t) {
-      std::string &o = chunk[t];
-      o.reserve((cut[t + 1] - cut[t]) * (F.metric.size() + 24 * (nl + 1)));
-      for (size_t q = cut[t]; q < cut[t + 1]; ++q) {
-        const size_t i = idx[q];
-        o += F.metric;
-        const char *const *v = r->value_ptrs.data() + r->voff[i];
-        if (nl) {
-          o += '{';
-          for (size_t k = 0; k < nl; ++k) {
-            if (k) o += ',';
-            o += F.names[F.by_name[k]];
-            o += "=\"";
-            escape_cstr(o, v[F.by_name[k]], true);
-            o += '"';
-          }
-          o += '}';
-        }
-        o += ' ';
-        go_float_u64_into(o, r->series[i].value);
-        o += '\n';
-      }
-    });
-    std::string &out = blocks[kv.first];
-    out += "# HELP " + kv.first + " ";
-    escape_cstr(out, F.help, false);
-    out += "\n# TYPE " + kv.first + " " + F.type + "\n";
-    for (auto &ch : chunk) out += ch;
-  }
-  std::string &out = r->text;
-  out.clear();
-  size_t total = 0;
-  for (auto &kv : blocks) total += kv.second.size();
-  out.reserve(total);
-  for (auto &kv : blocks) out += kv.second;  // families sorted by name (expfmt)
-  r->text_done = true;
-  *len = out.size();
+  if (!r->text_done) render_text(r);
+  *len = r->text.size();
   if (!buf) return GPUAGG_OK;
-  if (cap < out.size() + 1) return GPUAGG_ECAPACITY;
-  memcpy(buf, out.c_str(), out.size() + 1);
+  if (cap < r->text.size() + 1) return GPUAGG_ECAPACITY;
+  memcpy(buf, r->text.c_str(), r->text.size() + 1);
   return GPUAGG_OK;
 }
 

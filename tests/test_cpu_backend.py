@@ -262,3 +262,28 @@ def test_exposition_text_cpu_backend():
     want = X.render(m.series())
     assert text == want
     assert "e+" in text and 'pod\\\\x\\nq' in text
+
+
+@pytest.mark.parametrize("src,dst", [(["ip", "port"], None),  # few labels: one packed rank key
+                                     (["ip", "namespace", "podname", "workload", "service", "port"],
+                                      ["ip", "namespace", "podname", "workload", "service", "port"])],
+                         ids=["packed-key", "rank-rows"])
+def test_exposition_order_large_families(src, dst):
+    """Families past the parallel sort's threshold (65536 series) come out in
+    client_golang's order -- label values compared in label-name order -- whichever key
+    the sort uses: the ranks packed into one 128-bit key, or rank rows when too many
+    labels make them wider (oracle.exposition.render over the engine's own series)."""
+    from oracle import exposition as X
+    pods = W.make_pods(3000, seed=5)
+    recs = W.gen_records(400_000, pods, seed=6, flows=300_000, n_dst=50_000)
+    sp = spec(["forward_count", "forward_bytes"], src, dst)
+    g = make_engine(pods, sp, True, flags=CPU, sparse_capacity_log2=21)
+    try:
+        g.submit_numpy(recs)
+        text = g.snapshot_text()
+        series = g.snapshot()
+    finally:
+        g.close()
+    fam = sum(1 for k in series if k[0].endswith("forward_count"))
+    assert fam > 65536
+    assert text == X.render(series)
