@@ -113,6 +113,15 @@ struct SeriesRec {
   uint32_t arena;
   uint64_t off;
   uint64_t value;
+  uint64_t tok;  // its label values' sort tokens (render_series), in the same arena's token list
+};
+
+// One canonical id's labels at render time: its values' sort tokens and where its
+// pre-rendered values lie (one cache line per id for render_series' random lookups).
+struct LabelRec {
+  uint32_t tok[5];
+  uint32_t len;
+  uint64_t off;
 };
 
 // Canonical ids of the slot attributes a side's options render (namespace / pod /
@@ -120,6 +129,12 @@ struct SeriesRec {
 // "unknown") and a representative slot1 per id; rebuilt when the slots change.
 struct SlotCanon {
   std::vector<uint32_t> id, rep;
+  // per id: rank of its namespace / podname / workload kind / workload name string among
+  // the ids' (exposition sort tokens)
+  // rendered values (ctx_values_into of the mask, NUL-terminated) at blk[rec[id].off], tokens
+  // of namespace / podname / workload kind / workload name in rec[id].tok
+  std::vector<char> blk;
+  std::vector<LabelRec> rec;
   uint64_t version = ~0ull;
 };
 
@@ -161,6 +176,7 @@ struct gpuagg_result {
   std::vector<ResultFamily> fam;  // one per registered metric object
   std::vector<SeriesRec> series;
   std::vector<std::vector<char>> arenas;
+  std::vector<std::vector<uint32_t>> toks;  // per arena: label sort tokens (render_series)
   std::vector<const char *> value_ptrs;  // series i's label values: [voff[i], voff[i + 1])
   std::vector<uint64_t> voff;
   uint64_t dropped = 0;
@@ -168,7 +184,8 @@ struct gpuagg_result {
   // name -> exposition text block
   std::map<std::string, std::string> extra_text;
   // gpuagg_result_render_text's output, rendered once (callers size, then fill)
-  mutable std::string text;
+  mutable std::unique_ptr<char[]> text;  // text_len bytes + NUL
+  mutable size_t text_len = 0;
   mutable bool text_done = false;
 };
 
@@ -215,6 +232,13 @@ struct gpuagg_ctx {
   // query), response series (rcode name, qtypes, query, ips, answers)
   std::unordered_map<std::string, uint32_t> dns_req_canon, dns_resp_canon;
   std::vector<uint32_t> dns_req_id, dns_resp_id, dns_req_rep, dns_resp_rep;
+  // per canonical payload: sort tokens of request (qtypes, query) / response (rcode, qtypes,
+  // query, ips, answers) labels and its block below; rebuilt when the table has grown
+  std::vector<LabelRec> dns_req_rec, dns_resp_rec;
+  // the canonical payloads' label values, rendered at intern time (NUL-terminated, in
+  // label order): block of id i = [*_boff[i], *_boff[i + 1])
+  std::vector<char> dns_req_blk, dns_resp_blk;
+  std::vector<uint64_t> dns_req_boff{0}, dns_resp_boff{0};
   // canonical slot attributes per option mask (snapshot), valid for slots_version
   std::map<uint8_t, SlotCanon> slot_canon;
   uint64_t slots_version = 0;
@@ -2452,12 +2476,22 @@ int gpuagg_dns_intern(gpuagg_ctx *c, uint32_t rcode, const char *qtypes, const c
   c->dns_ids.emplace(std::move(key), nid);
   const std::string q = std::string(qtypes) + '\0' + query;
   auto i1 = c->dns_req_canon.emplace(q, (uint32_t)c->dns_req_rep.size());
-  if (i1.second) c->dns_req_rep.push_back(nid);
+  if (i1.second) {
+    c->dns_req_rep.push_back(nid);
+    c->dns_req_blk.insert(c->dns_req_blk.end(), q.begin(), q.end());
+    c->dns_req_blk.push_back('\0');
+    c->dns_req_boff.push_back(c->dns_req_blk.size());
+  }
   c->dns_req_id.push_back(i1.first->second);
   const std::string full = std::string(rcode < 6 ? kRcodeNames[rcode] : "") + '\0' + q + '\0' + ips + '\0' +
                            std::to_string(nresp);
   auto i2 = c->dns_resp_canon.emplace(full, (uint32_t)c->dns_resp_rep.size());
-  if (i2.second) c->dns_resp_rep.push_back(nid);
+  if (i2.second) {
+    c->dns_resp_rep.push_back(nid);
+    c->dns_resp_blk.insert(c->dns_resp_blk.end(), full.begin(), full.end());
+    c->dns_resp_blk.push_back('\0');
+    c->dns_resp_boff.push_back(c->dns_resp_blk.size());
+  }
   c->dns_resp_id.push_back(i2.first->second);
   *id = nid;
   return GPUAGG_OK;
@@ -2695,21 +2729,174 @@ struct LItem {
 };
 
 void append_str(std::vector<char> &a, const char *s, size_t n) {
-  a.insert(a.end(), s, s + n);
-  a.push_back('\0');
+  const size_t o = a.size();
+  a.resize(o + n + 1);
+  memcpy(a.data() + o, s, n);
+  a[o + n] = '\0';
 }
 void append_str(std::vector<char> &a, const std::string &s) { append_str(a, s.data(), s.size()); }
+
+// Exposition sort tokens: every label value is paired with an integer whose order is its
+// string's order (client_golang compares label values as strings) -- dense ranks with equal
+// strings tied -- so a family's series sort on integers without touching the strings.
+// run fn(t) for t < n on n threads (inline when n == 1)
+template <class F>
+void run_par(unsigned n, F &&fn) {
+  if (n <= 1) {
+    fn(0u);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < n; ++t) th.emplace_back(fn, t);
+  for (auto &x : th) x.join();
+}
+
+// Sample sort on T threads: T-1 splitters from an even sample, each thread buckets its
+// slice, buckets are sorted independently and land in order.
+template <class E, class L>
+void par_sort(std::vector<E> &v, L less, unsigned T) {
+  const size_t n = v.size();
+  if (T <= 1 || n < 65536) {
+    std::sort(v.begin(), v.end(), less);
+    return;
+  }
+  const size_t ov = 64;
+  std::vector<E> smp;
+  smp.reserve((size_t)T * ov);
+  for (size_t i = 0; i < (size_t)T * ov; ++i) smp.push_back(v[i * n / ((size_t)T * ov)]);
+  std::sort(smp.begin(), smp.end(), less);
+  std::vector<E> sp;
+  for (unsigned j = 1; j < T; ++j) sp.push_back(smp[j * ov]);
+  std::vector<uint32_t> bk(n);
+  std::vector<size_t> cnt((size_t)T * T, 0);  // [thread][bucket]
+  run_par(T, [&](unsigned t) {
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      const uint32_t b = (uint32_t)(std::upper_bound(sp.begin(), sp.end(), v[i], less) - sp.begin());
+      bk[i] = b;
+      ++cnt[(size_t)t * T + b];
+    }
+  });
+  std::vector<size_t> off((size_t)T * T), bstart(T + 1, 0);
+  size_t o = 0;
+  for (unsigned b = 0; b < T; ++b) {
+    bstart[b] = o;
+    for (unsigned t = 0; t < T; ++t) {
+      off[(size_t)t * T + b] = o;
+      o += cnt[(size_t)t * T + b];
+    }
+  }
+  bstart[T] = o;
+  std::vector<E> tmp(n);
+  run_par(T, [&](unsigned t) {
+    size_t *po = &off[(size_t)t * T];
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) tmp[po[bk[i]]++] = v[i];
+  });
+  run_par(T, [&](unsigned b) { std::sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1], less); });
+  v.swap(tmp);
+}
+
+std::vector<uint32_t> dense_ranks(const std::vector<std::string_view> &v) {
+  using P = std::pair<std::string_view, uint32_t>;
+  std::vector<P> ord(v.size());
+  for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = P{v[i], i};
+  const unsigned T = (unsigned)std::min<size_t>({(size_t)16, (size_t)std::max(1u, std::thread::hardware_concurrency()),
+                                                 v.size() / 16384 + 1});
+  par_sort(ord, [](const P &a, const P &b) { return a.first < b.first; }, T);
+  std::vector<uint32_t> rk(v.size());
+  uint32_t r = 0;
+  for (size_t i = 0; i < ord.size(); ++i) {
+    if (i && ord[i].first != ord[i - 1].first) ++r;
+    rk[ord[i].second] = r;
+  }
+  return rk;
+}
+
+// Fixed tables: an IPv4 label "a.b.c.d" orders as the tuple of its octets' decimal strings
+// (a '.' sorts below every digit, as the string's end does), so its token is the four
+// octet ranks; a port label is "unknown" (index 65536) or the port's decimal string.
+struct TokTables {
+  uint32_t octet[256];
+  std::vector<uint32_t> port;  // 65537
+  uint32_t dir_local[2], dir_remote[4], drop[16], flag[F_COUNT], rcode[7];
+  TokTables() {
+    std::vector<std::string> st;
+    auto ranks = [&](size_t n, auto &&name) {
+      st.clear();
+      for (size_t i = 0; i < n; ++i) st.push_back(name(i));
+      std::vector<std::string_view> sv(st.begin(), st.end());
+      return dense_ranks(sv);
+    };
+    auto o = ranks(256, [](size_t i) { return std::to_string(i); });
+    std::copy(o.begin(), o.end(), octet);
+    port = ranks(65537, [](size_t i) { return i < 65536 ? std::to_string(i) : std::string("unknown"); });
+    auto d = ranks(2, [](size_t i) { return std::string(i == 0 ? "ingress" : "egress"); });
+    std::copy(d.begin(), d.end(), dir_local);
+    d = ranks(4, [](size_t i) { return traffic_direction_name((uint32_t)i); });
+    std::copy(d.begin(), d.end(), dir_remote);
+    d = ranks(16, [](size_t i) { return drop_reason_name((uint32_t)i); });
+    std::copy(d.begin(), d.end(), drop);
+    d = ranks(F_COUNT, [](size_t i) { return std::string(kFlagNames[i]); });
+    std::copy(d.begin(), d.end(), flag);
+    d = ranks(7, [](size_t i) { return std::string(i < 6 ? kRcodeNames[i] : ""); });
+    std::copy(d.begin(), d.end(), rcode);
+  }
+  uint32_t ip(uint32_t v) const {
+    return octet[v & 255u] << 24 | octet[(v >> 8) & 255u] << 16 | octet[(v >> 16) & 255u] << 8 | octet[v >> 24];
+  }
+};
+const TokTables &tok_tables() {
+  static const TokTables t;
+  return t;
+}
+
+// ctx_values_into's tokens, value for value
+void ctx_tokens_into(const TokTables &tt, uint8_t opts, uint32_t ip, const SlotCanon &sc, uint32_t cid,
+                     uint32_t port17, std::vector<uint32_t> &out) {
+  if (opts & OPT_IP) out.push_back(tt.ip(ip));
+  const LabelRec &lr = sc.rec[cid];
+  if (opts & OPT_NS) out.push_back(lr.tok[0]);
+  if (opts & OPT_POD) out.push_back(lr.tok[1]);
+  if (opts & OPT_WL) {
+    out.push_back(lr.tok[2]);
+    out.push_back(lr.tok[3]);
+  }
+  if (opts & OPT_SVC) out.push_back(0u);
+  if (opts & OPT_PORT) out.push_back(tt.port[(port17 & 0x10000u) ? (port17 & 0xFFFFu) : 65536u]);
+}
+
+void append_ip(std::vector<char> &out, uint32_t ip) {  // "a.b.c.d", a = the low byte
+  char b[16];
+  size_t n = 0;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t o = (ip >> (8 * k)) & 255u;
+    if (k) b[n++] = '.';
+    if (o >= 100) b[n++] = (char)('0' + o / 100);
+    if (o >= 10) b[n++] = (char)('0' + o / 10 % 10);
+    b[n++] = (char)('0' + o % 10);
+  }
+  append_str(out, b, n);
+}
+void append_port(std::vector<char> &out, uint32_t port17) {  // decimal, or "unknown"
+  if (!(port17 & 0x10000u)) {
+    append_str(out, "unknown", 7);
+    return;
+  }
+  char d[8];
+  int n = 0;
+  uint32_t x = port17 & 0xFFFFu;
+  do {
+    d[7 - n++] = (char)('0' + x % 10);
+    x /= 10;
+  } while (x);
+  append_str(out, d + 8 - n, (size_t)n);
+}
 
 // ctx_values (getByDirectionValues, types.go:418-505) into an arena.
 void ctx_values_into(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t slot1, uint32_t port17,
                      std::vector<char> &out) {
   const SlotAttr *a = (slot1 && slot1 - 1 < c->slots.size()) ? &c->slots[slot1 - 1] : nullptr;
   static const std::string unk = "unknown";
-  if (opts & OPT_IP) {
-    char b[20];
-    const int n = snprintf(b, sizeof b, "%u.%u.%u.%u", ip & 255u, (ip >> 8) & 255u, (ip >> 16) & 255u, ip >> 24);
-    append_str(out, b, (size_t)n);
-  }
+  if (opts & OPT_IP) append_ip(out, ip);
   if (opts & OPT_NS) append_str(out, a ? a->ns : unk);
   if (opts & OPT_POD) append_str(out, a ? a->pod : unk);
   if (opts & OPT_WL) {
@@ -2717,15 +2904,19 @@ void ctx_values_into(const gpuagg_ctx *c, uint8_t opts, uint32_t ip, uint32_t sl
     append_str(out, a && a->has_owner ? a->wk_name : unk);
   }
   if (opts & OPT_SVC) append_str(out, unk);
-  if (opts & OPT_PORT) {
-    if (port17 & 0x10000u) {
-      char b[8];
-      const int n = snprintf(b, sizeof b, "%u", port17 & 0xFFFFu);
-      append_str(out, b, (size_t)n);
-    } else {
-      append_str(out, unk);
-    }
+  if (opts & OPT_PORT) append_port(out, port17);
+}
+
+// ctx_values_into with the slot attributes from the canonical id's pre-rendered block
+void ctx_values_fast(uint8_t opts, uint32_t ip, const SlotCanon &sc, uint32_t cid, uint32_t port17,
+                     std::vector<char> &out) {
+  if (opts & OPT_IP) append_ip(out, ip);
+  if (opts & (OPT_NS | OPT_POD | OPT_WL)) {
+    const LabelRec &lr = sc.rec[cid];
+    out.insert(out.end(), sc.blk.data() + lr.off, sc.blk.data() + lr.off + lr.len);
   }
+  if (opts & OPT_SVC) append_str(out, "unknown", 7);
+  if (opts & OPT_PORT) append_port(out, port17);
 }
 
 int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vector<uint64_t> &db,
@@ -2792,6 +2983,29 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
         sc.id[s1] = ins.first->second;
       }
     }
+    sc.blk.clear();
+    sc.rec.assign(sc.rep.size(), LabelRec{});
+    for (size_t i = 0; i < sc.rep.size(); ++i) {
+      sc.rec[i].off = sc.blk.size();
+      ctx_values_into(c, m, 0, sc.rep[i], 0, sc.blk);
+      sc.rec[i].len = (uint32_t)(sc.blk.size() - sc.rec[i].off);
+    }
+    static const std::string unk = "unknown";
+    for (int f = 0; f < 4; ++f) {
+      std::vector<std::string_view> sv(sc.rep.size());
+      for (size_t i = 0; i < sc.rep.size(); ++i) {
+        const uint32_t s1 = sc.rep[i];
+        const SlotAttr *a = (s1 && s1 - 1 < c->slots.size()) ? &c->slots[s1 - 1] : nullptr;
+        const std::string *x = &unk;
+        if (a && f == 0) x = &a->ns;
+        if (a && f == 1) x = &a->pod;
+        if (a && a->has_owner && f == 2) x = &a->wk_kind;
+        if (a && a->has_owner && f == 3) x = &a->wk_name;
+        sv[i] = *x;
+      }
+      const std::vector<uint32_t> rk = dense_ranks(sv);
+      for (size_t i = 0; i < sc.rep.size(); ++i) sc.rec[i].tok[f] = rk[i];
+    }
     sc.version = c->slots_version;
     return sc;
   };
@@ -2810,6 +3024,43 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   // canonical DNS payloads (kept by gpuagg_dns_intern)
   const std::vector<uint32_t> &dns_req = c->dns_req_id, &dns_resp = c->dns_resp_id;
   const std::vector<uint32_t> &dns_req_rep = c->dns_req_rep, &dns_resp_rep = c->dns_resp_rep;
+  const TokTables &tt = tok_tables();
+  bool any_dns = false;
+  for (const View &v : views)
+    any_dns |= c->groups[v.group].family == FAM_DNS_REQ || c->groups[v.group].family == FAM_DNS_RESP;
+  auto dns_recs = [&](std::vector<LabelRec> &rec, const std::vector<uint32_t> &reps,
+                      const std::vector<uint64_t> &boff, bool resp) {
+    if (rec.size() == reps.size()) return;  // (tokens are recomputed as the table grows)
+    const size_t n = reps.size();
+    rec.assign(n, LabelRec{});
+    for (size_t i = 0; i < n; ++i) {
+      rec[i].off = boff[i];
+      rec[i].len = (uint32_t)(boff[i + 1] - boff[i]);
+    }
+    std::vector<std::string_view> sv(n);
+    std::vector<std::string> nr;
+    auto field = [&](int f, auto &&get) {
+      for (size_t i = 0; i < n; ++i) sv[i] = get(c->dns[reps[i]], i);
+      const std::vector<uint32_t> rk = dense_ranks(sv);
+      for (size_t i = 0; i < n; ++i) rec[i].tok[f] = rk[i];
+    };
+    int f = 0;
+    if (resp)
+      for (size_t i = 0; i < n; ++i) rec[i].tok[f] = tt.rcode[std::min<uint32_t>(c->dns[reps[i]].rcode, 6u)];
+    f += resp;
+    field(f++, [](const DnsAttr &a, size_t) -> std::string_view { return a.qtypes; });
+    field(f++, [](const DnsAttr &a, size_t) -> std::string_view { return a.query; });
+    if (resp) {
+      field(f++, [](const DnsAttr &a, size_t) -> std::string_view { return a.ips; });
+      nr.resize(n);
+      for (size_t i = 0; i < n; ++i) nr[i] = std::to_string(c->dns[reps[i]].nresp);
+      field(f++, [&](const DnsAttr &, size_t i) -> std::string_view { return nr[i]; });
+    }
+  };
+  if (any_dns) {
+    dns_recs(c->dns_req_rec, dns_req_rep, c->dns_req_boff, false);
+    dns_recs(c->dns_resp_rec, dns_resp_rep, c->dns_resp_boff, true);
+  }
   // items: one per (counter, view), partitioned by key hash
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t work = nent + (size_t)c->dense_len;
@@ -2902,6 +3153,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   // partition's arena
   std::vector<std::vector<SeriesRec>> out(T);
   r->arenas.resize(T);
+  r->toks.resize(T);
   run([&](unsigned p) {
     size_t total = 0;
     for (unsigned t = 0; t < T; ++t) total += parts[t][p].size();
@@ -2915,42 +3167,63 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
       }
       std::vector<LItem>().swap(parts[t][p]);
     }
+    const size_t NM = m.size();
     std::vector<char> &ar = r->arenas[p];
+    std::vector<uint32_t> &tk = r->toks[p];
+    ar.reserve(m.size() * 48);
+    tk.reserve(m.size() * 4);
+    out[p].reserve(m.size() * 2);
     for (const auto &kv : m) {
       const LKey &k = kv.first;
       const View &v = views[k.w[0]];
       const Group &g = c->groups[v.group];
-      for (uint32_t ii : v.insts) {
-        const Instance &in = c->inst[ii];
-        out[p].push_back(SeriesRec{ii, p, ar.size(), in.vk == VK_BYTES ? kv.second.second : kv.second.first});
-        const uint32_t pre = k.w[1];
-        auto dir = [&](uint32_t d) {
-          if (local) append_str(ar, d == 0 ? "ingress" : "egress", d == 0 ? 7 : 6);
-          else append_str(ar, traffic_direction_name(d));
-        };
-        switch (g.family) {
-          case FAM_FWD:
-          case FAM_RETRANS: dir(pre); break;
-          case FAM_DROP:
-            append_str(ar, drop_reason_name(pre >> 4));
-            dir(pre & 15u);
-            break;
-          case FAM_TCPFLAGS: append_str(ar, kFlagNames[pre]); break;
-          case FAM_DNS_REQ:
-          case FAM_DNS_RESP: {
-            const DnsAttr &a = c->dns[g.family == FAM_DNS_REQ ? dns_req_rep[pre] : dns_resp_rep[pre]];
-            if (g.family == FAM_DNS_RESP) append_str(ar, a.rcode < 6 ? kRcodeNames[a.rcode] : "");
-            append_str(ar, a.qtypes);
-            append_str(ar, a.query);
-            if (g.family == FAM_DNS_RESP) {
-              append_str(ar, a.ips);
-              append_str(ar, std::to_string(a.nresp));
-            }
-            break;
-          }
+      // the view's instances (count / bytes objects) share the labels: rendered once
+      const uint64_t off = ar.size(), tok = tk.size();
+      for (uint32_t ii : v.insts)
+        out[p].push_back(SeriesRec{ii, p, off, c->inst[ii].vk == VK_BYTES ? kv.second.second : kv.second.first, tok});
+      const uint32_t pre = k.w[1];
+      auto dir = [&](uint32_t d) {
+        if (local) {
+          append_str(ar, d == 0 ? "ingress" : "egress", d == 0 ? 7 : 6);
+          tk.push_back(tt.dir_local[d & 1u]);
+        } else {
+          append_str(ar, traffic_direction_name(d));
+          tk.push_back(tt.dir_remote[d & 3u]);
         }
-        if (v.src) ctx_values_into(c, g.src_opts, k.w[2], src_canon[v.group]->rep[k.w[3]], k.w[4], ar);
-        if (v.dst) ctx_values_into(c, g.dst_opts, k.w[5], dst_canon[v.group]->rep[k.w[6]], k.w[7], ar);
+      };
+      switch (g.family) {
+        case FAM_FWD:
+        case FAM_RETRANS: dir(pre); break;
+        case FAM_DROP:
+          append_str(ar, drop_reason_name(pre >> 4));
+          tk.push_back(tt.drop[(pre >> 4) & 15u]);
+          dir(pre & 15u);
+          break;
+        case FAM_TCPFLAGS:
+          append_str(ar, kFlagNames[pre]);
+          tk.push_back(tt.flag[pre]);
+          break;
+        case FAM_DNS_REQ:
+        case FAM_DNS_RESP: {
+          if (g.family == FAM_DNS_REQ) {  // qtypes, query
+            const LabelRec &lr = c->dns_req_rec[pre];
+            ar.insert(ar.end(), c->dns_req_blk.data() + lr.off, c->dns_req_blk.data() + lr.off + lr.len);
+            tk.insert(tk.end(), lr.tok, lr.tok + 2);
+          } else {  // rcode, qtypes, query, ips, answers
+            const LabelRec &lr = c->dns_resp_rec[pre];
+            ar.insert(ar.end(), c->dns_resp_blk.data() + lr.off, c->dns_resp_blk.data() + lr.off + lr.len);
+            tk.insert(tk.end(), lr.tok, lr.tok + 5);
+          }
+          break;
+        }
+      }
+      if (v.src) {
+        ctx_values_fast(g.src_opts, k.w[2], *src_canon[v.group], k.w[3], k.w[4], ar);
+        ctx_tokens_into(tt, g.src_opts, k.w[2], *src_canon[v.group], k.w[3], k.w[4], tk);
+      }
+      if (v.dst) {
+        ctx_values_fast(g.dst_opts, k.w[5], *dst_canon[v.group], k.w[6], k.w[7], ar);
+        ctx_tokens_into(tt, g.dst_opts, k.w[5], *dst_canon[v.group], k.w[6], k.w[7], tk);
       }
     }
   });
@@ -3186,133 +3459,42 @@ void escape_cstr(std::string &out, const char *s, bool quote) {  // expfmt escap
 }
 void escape_into(std::string &out, const std::string &s, bool quote) { escape_cstr(out, s.c_str(), quote); }
 
-extern "C++" {
-// run fn(t) for t < n on n threads (inline when n == 1)
-template <class F>
-void run_par(unsigned n, F &&fn) {
-  if (n <= 1) {
-    fn(0u);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < n; ++t) th.emplace_back(fn, t);
-  for (auto &x : th) x.join();
-}
-
-// Sample sort on T threads: T-1 splitters from an even sample, each thread buckets its
-// slice, buckets are sorted independently and land in order.
-template <class E, class L>
-void par_sort(std::vector<E> &v, L less, unsigned T) {
-  const size_t n = v.size();
-  if (T <= 1 || n < 65536) {
-    std::sort(v.begin(), v.end(), less);
-    return;
-  }
-  const size_t ov = 64;
-  std::vector<E> smp;
-  smp.reserve((size_t)T * ov);
-  for (size_t i = 0; i < (size_t)T * ov; ++i) smp.push_back(v[i * n / ((size_t)T * ov)]);
-  std::sort(smp.begin(), smp.end(), less);
-  std::vector<E> sp;
-  for (unsigned j = 1; j < T; ++j) sp.push_back(smp[j * ov]);
-  std::vector<uint32_t> bk(n);
-  std::vector<size_t> cnt((size_t)T * T, 0);  // [thread][bucket]
-  run_par(T, [&](unsigned t) {
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
-      const uint32_t b = (uint32_t)(std::upper_bound(sp.begin(), sp.end(), v[i], less) - sp.begin());
-      bk[i] = b;
-      ++cnt[(size_t)t * T + b];
-    }
-  });
-  std::vector<size_t> off((size_t)T * T), bstart(T + 1, 0);
-  size_t o = 0;
-  for (unsigned b = 0; b < T; ++b) {
-    bstart[b] = o;
-    for (unsigned t = 0; t < T; ++t) {
-      off[(size_t)t * T + b] = o;
-      o += cnt[(size_t)t * T + b];
-    }
-  }
-  bstart[T] = o;
-  std::vector<E> tmp(n);
-  run_par(T, [&](unsigned t) {
-    size_t *po = &off[(size_t)t * T];
-    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) tmp[po[bk[i]]++] = v[i];
-  });
-  run_par(T, [&](unsigned b) { std::sort(tmp.begin() + bstart[b], tmp.begin() + bstart[b + 1], less); });
-  v.swap(tmp);
-}
-}  // extern "C++"
-
-struct SvKey {
-  const char *p;
-  uint32_t n;
-  uint64_t h;
-  bool operator==(const SvKey &o) const { return n == o.n && memcmp(p, o.p, n) == 0; }
-};
-struct SvKeyHash {
-  size_t operator()(const SvKey &k) const { return (size_t)k.h; }
-};
 
 // Series of one family in exposition order (client_golang sorts a family's metrics by
-// their label values taken in label-name order; MetricSorter): every value is replaced by
-// its rank among the family's distinct values (string order), so the sort compares
-// integers -- one packed 128-bit key when the ranks fit, else rank rows.
+// their label values taken in label-name order; MetricSorter), on the values' sort tokens
+// (render_series): packed into one 128-bit key when their widths fit, else as rows.
 void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size_t> &idx, unsigned T) {
   const size_t n = idx.size(), nl = F.names.size();
   if (n < 2 || nl == 0) return;
-  const size_t ne = n * nl;
-  std::vector<uint64_t> hv(ne);
-  std::vector<uint32_t> ln(ne), rk(ne);
+  std::vector<uint32_t> rk(n * nl);  // tokens in name order
+  std::vector<std::vector<uint32_t>> mx(T, std::vector<uint32_t>(nl, 0));
   run_par(T, [&](unsigned t) {
     for (size_t q = n * t / T; q < n * (t + 1) / T; ++q) {
-      const char *const *v = r->value_ptrs.data() + r->voff[idx[q]];
+      const SeriesRec &sr = r->series[idx[q]];
+      const uint32_t *tok = r->toks[sr.arena].data() + sr.tok;
       for (size_t k = 0; k < nl; ++k) {
-        const char *s = v[F.by_name[k]];
-        const size_t m = strlen(s);
-        ln[q * nl + k] = (uint32_t)m;
-        hv[q * nl + k] = std::hash<std::string_view>()(std::string_view(s, m));
+        const uint32_t x = tok[F.by_name[k]];
+        rk[q * nl + k] = x;
+        mx[t][k] = std::max(mx[t][k], x);
       }
     }
   });
-  auto val = [&](size_t e) { return r->value_ptrs[r->voff[idx[e / nl]] + F.by_name[e % nl]]; };
-  // distinct values, partitioned by hash over the threads: dist[t] owns h % T == t
-  std::vector<std::vector<SvKey>> dist(T);
-  run_par(T, [&](unsigned t) {
-    std::unordered_map<SvKey, uint32_t, SvKeyHash> m;
-    for (size_t e = 0; e < ne; ++e) {
-      if (hv[e] % T != t) continue;
-      const SvKey k{val(e), ln[e], hv[e]};
-      auto ins = m.emplace(k, (uint32_t)dist[t].size());
-      if (ins.second) dist[t].push_back(k);
-      rk[e] = ins.first->second;  // local id for now
-    }
-  });
-  std::vector<std::pair<SvKey, uint32_t>> all;  // (value, owner thread << 0 | local id)
-  std::vector<size_t> dbase(T + 1, 0);
-  for (unsigned t = 0; t < T; ++t) dbase[t + 1] = dbase[t] + dist[t].size();
-  all.reserve(dbase[T]);
-  for (unsigned t = 0; t < T; ++t)
-    for (size_t i = 0; i < dist[t].size(); ++i) all.push_back({dist[t][i], (uint32_t)(dbase[t] + i)});
-  par_sort(all, [](const std::pair<SvKey, uint32_t> &a, const std::pair<SvKey, uint32_t> &b) {
-    const int c = memcmp(a.first.p, b.first.p, std::min(a.first.n, b.first.n));
-    return c ? c < 0 : a.first.n < b.first.n;
-  }, T);
-  std::vector<uint32_t> rank(dbase[T]);
-  for (size_t i = 0; i < all.size(); ++i) rank[all[i].second] = (uint32_t)i;
-  run_par(T, [&](unsigned t) {
-    for (size_t e = ne * t / T; e < ne * (t + 1) / T; ++e) rk[e] = rank[dbase[hv[e] % T] + rk[e]];
-  });
-  unsigned bits = 1;
-  while (bits < 32 && (1ull << bits) < all.size()) ++bits;
+  std::vector<unsigned> bits(nl, 0);
+  unsigned tbits = 0;
+  for (size_t k = 0; k < nl; ++k) {
+    uint32_t m = 0;
+    for (unsigned t = 0; t < T; ++t) m = std::max(m, mx[t][k]);
+    while (bits[k] < 32 && (m >> bits[k])) ++bits[k];
+    tbits += bits[k];
+  }
   const std::vector<size_t> old = idx;
-  if (nl * bits <= 128) {
+  if (tbits <= 128) {
     using K = std::pair<unsigned __int128, uint32_t>;
     std::vector<K> keys(n);
     run_par(T, [&](unsigned t) {
       for (size_t q = n * t / T; q < n * (t + 1) / T; ++q) {
         unsigned __int128 x = 0;
-        for (size_t k = 0; k < nl; ++k) x = (x << bits) | rk[q * nl + k];
+        for (size_t k = 0; k < nl; ++k) x = (x << bits[k]) | rk[q * nl + k];
         keys[q] = K{x, (uint32_t)q};
       }
     });
@@ -3437,15 +3619,18 @@ void render_text(const gpuagg_result *r) {
   }
   std::vector<size_t> at(piece.size() + 1, 0);
   for (size_t i = 0; i < piece.size(); ++i) at[i + 1] = at[i] + piece[i].second;
-  std::string &out = r->text;
-  out.resize(at[piece.size()]);
-  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, out.size() / (1u << 22) + 1}));
+  const size_t N = at[piece.size()];
+  r->text.reset(new char[N + 1]);  // (not zeroed: every byte is copied below, page faults spread over the threads)
+  r->text_len = N;
+  char *out = r->text.get();
+  out[N] = '\0';
+  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, N / (1u << 22) + 1}));
   run_par(T, [&](unsigned t) {  // byte range [t * N / T, (t + 1) * N / T) of the output
-    const size_t b0 = out.size() * t / T, b1 = out.size() * (t + 1) / T;
+    const size_t b0 = N * t / T, b1 = N * (t + 1) / T;
     size_t i = std::upper_bound(at.begin(), at.end(), b0) - at.begin() - 1;
     for (; i < piece.size() && at[i] < b1; ++i) {
       const size_t s0 = std::max(b0, at[i]), s1 = std::min(b1, at[i + 1]);
-      if (s1 > s0) memcpy(&out[s0], piece[i].first + (s0 - at[i]), s1 - s0);
+      if (s1 > s0) memcpy(out + s0, piece[i].first + (s0 - at[i]), s1 - s0);
     }
   });
   r->text_done = true;
@@ -3455,10 +3640,10 @@ void render_text(const gpuagg_result *r) {
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
   if (!r || !len) return GPUAGG_EINVAL;
   if (!r->text_done) render_text(r);
-  *len = r->text.size();
+  *len = r->text_len;
   if (!buf) return GPUAGG_OK;
-  if (cap < r->text.size() + 1) return GPUAGG_ECAPACITY;
-  memcpy(buf, r->text.c_str(), r->text.size() + 1);
+  if (cap < r->text_len + 1) return GPUAGG_ECAPACITY;
+  memcpy(buf, r->text.get(), r->text_len + 1);
   return GPUAGG_OK;
 }
 

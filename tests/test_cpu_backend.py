@@ -15,7 +15,7 @@ from oracle import sketch as S
 from retina_amd import workloads as W
 
 from .helpers import diff_series, engine_series, make_engine, oracle_series
-from .test_gpu_parity import CASES, MIX, spec
+from .test_gpu_parity import CASES, DNS_ALL, MIX, TCP_ALL, spec
 
 CPU = 128  # GPUAGG_FLAG_CPU_BACKEND
 
@@ -287,3 +287,54 @@ def test_exposition_order_large_families(src, dst):
     fam = sum(1 for k in series if k[0].endswith("forward_count"))
     assert fam > 65536
     assert text == X.render(series)
+
+
+@pytest.mark.parametrize("cid,sp,remote,gen", CASES, ids=[c[0] for c in CASES])
+def test_exposition_order_every_case(cid, sp, remote, gen):
+    """The exposition text of every parity case (all families: directions, drop reasons,
+    flags, DNS payloads, workloads, ports and "unknown" values) is the oracle's rendering of
+    the same series: the sort tokens order each label exactly as its strings."""
+    from oracle import exposition as X
+    pods = W.make_pods(200, seed=23)
+    recs = W.gen_records(20_000, pods, seed=zlib.crc32(cid.encode()) & 0xFFFF, **gen)
+    g = make_engine(pods, sp, remote, recs=recs, flags=CPU)
+    try:
+        g.submit_numpy(recs)
+        text = g.snapshot_text()
+        series = g.snapshot()
+    finally:
+        g.close()
+    assert text == X.render(series)
+
+
+def test_exposition_order_across_growth_and_churn():
+    """The cached render tables (canonical slot attributes per slots version, DNS payload
+    tokens per table size) follow the engine between snapshots: new DNS payloads interned
+    and pods deleted, added and retired in between still render in the oracle's order."""
+    from oracle import exposition as X
+    pods = W.make_pods(200, seed=31)
+    sp = spec(TCP_ALL + DNS_ALL, ["namespace", "podname"])
+    a = W.gen_records(20_000, pods, seed=32, **MIX)
+    g = make_engine(pods, sp, False, recs=a, flags=CPU)
+    try:
+        g.submit_numpy(a)
+        assert g.snapshot_text() == X.render(g.snapshot())
+        more = W.make_pods(260, seed=33)
+        for ep in pods.endpoints[:60]:
+            g.cache_delete_endpoint(ep.namespace, ep.name)
+        for ep in more.endpoints[200:]:
+            g.cache_update_endpoint(ep)
+        g.cache_commit(1)
+        g.retire_slots()
+        b = W.gen_records(20_000, more, seed=34, **dict(MIX, n_queries=500))
+        ids = np.array([g.dns_intern(p.rcode, p.qtypes, p.query, p.ips, p.num_answers) for p in b.dns],
+                       np.uint32)
+        assert ids.max() >= len(a.dns)  # the table grew
+        has = b.dns_id < len(b.dns)
+        b.dns_id[has] = ids[b.dns_id[has]]
+        g.submit_numpy(b)
+        series = g.snapshot()
+        assert any(k[0].endswith("dns_request_count") for k in series)
+        assert g.snapshot_text() == X.render(series)
+    finally:
+        g.close()
