@@ -272,7 +272,7 @@ def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, 
     g.set_timing(False)
     k = st["kernel_launches"] or 1
     kms = st["kernel_ms"] / k
-    other = st["fold_ms"] / k + (st["sketch_ms"] / st["sketch_launches"] if st["sketch_launches"] else 0.0)
+    other = (st["fold_ms"] + st["sketch_ms"]) / k  # folds and the sketch pass, per aggregation launch
     at_full_rate = full_kernel_ms * n / n_total
     return {"batch_records": n, "launches": launches, "records_per_s": n / wall, "ms_per_launch": wall * 1e3,
             "kernel_ms": kms, "other_kernels_ms": other,
@@ -290,10 +290,13 @@ SCRAPE_EPOCH_S = 15.0
 def scrape_cost(g, reps: int = 3):
     """Host-side cost of one scrape on the state the timed region left: gpuagg_snapshot
     (device sync, table compaction and D2H, label rendering of every series) and
-    gpuagg_result_render_text (client_golang's text exposition), median of `reps`.  The
-    walk a Go publish does over the result is not included (it is the caller's)."""
-    snap, rend, nser, nbytes = [], [], 0, 0
-    for _ in range(reps):
+    gpuagg_result_render_text (client_golang's text exposition: rendered by the sizing call,
+    then copied into the caller's buffer), median of `reps` after a first, cold scrape
+    (whose snapshot also builds the canonical label tables, as a scrape does after pod churn
+    or new DNS payloads).  The walk a Go publish does over the result is not included."""
+    snap, rend, copy, nser, nbytes = [], [], [], 0, 0
+    out = None
+    for _ in range(reps + 1):
         r = C.c_void_p()
         t0 = time.perf_counter()
         rc = g.lib.gpuagg_snapshot(g.h, C.byref(r))
@@ -304,10 +307,13 @@ def scrape_cost(g, reps: int = 3):
             nser = int(g.lib.gpuagg_result_count(r))
             ln = C.c_size_t()
             t2 = time.perf_counter()
-            g.lib.gpuagg_result_render_text(r, None, 0, C.byref(ln))
-            buf = C.create_string_buffer(ln.value + 1)
-            rc = g.lib.gpuagg_result_render_text(r, buf, ln.value + 1, C.byref(ln))
+            rc = g.lib.gpuagg_result_render_text(r, None, 0, C.byref(ln))
             t3 = time.perf_counter()
+            if out is None or out.size < ln.value + 1:
+                out = np.empty(ln.value + 1, np.uint8)
+            t4 = time.perf_counter()
+            rc = rc or g.lib.gpuagg_result_render_text(r, out.ctypes.data_as(C.c_char_p), out.size, C.byref(ln))
+            t5 = time.perf_counter()
             if rc != 0:
                 raise RuntimeError("gpuagg_result_render_text: %d" % rc)
             nbytes = int(ln.value)
@@ -315,11 +321,15 @@ def scrape_cost(g, reps: int = 3):
             g.lib.gpuagg_result_free(r)
         snap.append((t1 - t0) * 1e3)
         rend.append((t3 - t2) * 1e3)
-    sm, rm = float(np.median(snap)), float(np.median(rend))
-    return {"series": nser, "text_bytes": nbytes, "snapshot_ms": sm, "render_ms": rm,
-            "epoch_frac": (sm + rm) / (SCRAPE_EPOCH_S * 1e3), "epoch_s": SCRAPE_EPOCH_S,
-            "note": "gpuagg_snapshot + gpuagg_result_render_text on the timed region's state, median of %d; "
-                    "host cost per scrape epoch, outside `value`" % reps}
+        copy.append((t5 - t4) * 1e3)
+    sm, rm, cm = (float(np.median(x[1:])) for x in (snap, rend, copy))
+    return {"series": nser, "text_bytes": nbytes, "snapshot_ms": sm, "render_ms": rm, "copy_ms": cm,
+            "cold_snapshot_ms": snap[0], "cold_render_ms": rend[0],
+            "epoch_frac": (sm + rm + cm) / (SCRAPE_EPOCH_S * 1e3),
+            "cold_epoch_frac": (snap[0] + rend[0] + copy[0]) / (SCRAPE_EPOCH_S * 1e3), "epoch_s": SCRAPE_EPOCH_S,
+            "note": "gpuagg_snapshot + gpuagg_result_render_text (render, then copy into the caller's buffer) on "
+                    "the timed region's state: median of %d warm scrapes, and the first (cold) one; host cost per "
+                    "scrape epoch, outside `value`" % reps}
 
 
 def main():

@@ -504,7 +504,8 @@ typedef struct gpuagg_stats {
 #define GPUAGG_KERNEL_CPU 4u           /* the CPU backend's host threads               */
 
 int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
-/* Enables HIP-event timing of the aggregation kernel on the ctx's stream. */
+/* Enables HIP-event timing of the aggregation kernel on the ctx's stream; disabling zeroes
+ * the timed counters (kernel / fold / sketch / decode ms and launches). */
 int gpuagg_set_timing(gpuagg_ctx *ctx, int enabled);
 /* Returns the ctx's HIP stream (hipStream_t) as an opaque pointer. */
 void *gpuagg_stream(gpuagg_ctx *ctx);

@@ -4187,10 +4187,14 @@ int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   if (c->cpu) c->host_timing = enabled != 0;  // host wall time of the launches (no HIP events)
   else c->timing = enabled != 0;
   c->tm_chain = false;
-  if (!enabled) {
+  if (!enabled) {  // the timed counters start again from zero
     c->stats.kernel_ms = 0;
     c->stats.fold_ms = 0;
     c->stats.kernel_launches = 0;
+    c->stats.sketch_ms = 0;
+    c->stats.sketch_launches = 0;
+    c->stats.decode_ms = 0;
+    c->stats.decode_launches = 0;
   }
   return GPUAGG_OK;
 }
