@@ -28,6 +28,7 @@
 #include <map>
 #include <set>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -114,6 +115,8 @@ struct SeriesRec {
   uint64_t off;
   uint64_t value;
   uint64_t tok;  // its label values' sort tokens (render_series), in the same arena's token list
+  uint32_t len;  // bytes of its label values in the arena (NULs included)
+  uint32_t esc;  // a value holds a byte the exposition escapes (\\ " newline)
 };
 
 // One canonical id's labels at render time: its values' sort tokens and where its
@@ -177,8 +180,11 @@ struct gpuagg_result {
   std::vector<SeriesRec> series;
   std::vector<std::vector<char>> arenas;
   std::vector<std::vector<uint32_t>> toks;  // per arena: label sort tokens (render_series)
-  std::vector<const char *> value_ptrs;  // series i's label values: [voff[i], voff[i + 1])
-  std::vector<uint64_t> voff;
+  // series i's label values: value_ptrs[voff[i] ...], built on the first gpuagg_result_series
+  // (the exposition text walks the arenas itself)
+  mutable std::vector<const char *> value_ptrs;
+  mutable std::vector<uint64_t> voff;
+  mutable std::once_flag ptrs_once;
   uint64_t dropped = 0;
   // families rendered outside `series` (the latency histograms / no_response counter):
   // name -> exposition text block
@@ -3179,8 +3185,6 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
       const Group &g = c->groups[v.group];
       // the view's instances (count / bytes objects) share the labels: rendered once
       const uint64_t off = ar.size(), tok = tk.size();
-      for (uint32_t ii : v.insts)
-        out[p].push_back(SeriesRec{ii, p, off, c->inst[ii].vk == VK_BYTES ? kv.second.second : kv.second.first, tok});
       const uint32_t pre = k.w[1];
       auto dir = [&](uint32_t d) {
         if (local) {
@@ -3225,36 +3229,20 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
         ctx_values_fast(g.dst_opts, k.w[5], *dst_canon[v.group], k.w[6], k.w[7], ar);
         ctx_tokens_into(tt, g.dst_opts, k.w[5], *dst_canon[v.group], k.w[6], k.w[7], tk);
       }
+      const uint32_t len = (uint32_t)(ar.size() - off);
+      const char *b = ar.data() + off;
+      const uint32_t esc = memchr(b, '\\', len) || memchr(b, '"', len) || memchr(b, '\n', len);
+      for (uint32_t ii : v.insts)
+        out[p].push_back(SeriesRec{ii, p, off, c->inst[ii].vk == VK_BYTES ? kv.second.second : kv.second.first, tok,
+                                   len, esc});
     }
   });
-  // concatenate the partitions and point at each series' label values (the arenas are
-  // final now), partition by partition on the same threads
+  // concatenate the partitions
   std::vector<size_t> sbase(T + 1, 0);
-  std::vector<uint64_t> vbase(T + 1, 0);
-  for (unsigned p = 0; p < T; ++p) {
-    uint64_t nv = 0;
-    for (const SeriesRec &sr : out[p]) nv += r->fam[sr.fam].names.size();
-    sbase[p + 1] = sbase[p] + out[p].size();
-    vbase[p + 1] = vbase[p] + nv;
-  }
-  const size_t ns = sbase[T];
-  r->series.resize(ns);
-  r->voff.resize(ns + 1);
-  r->value_ptrs.resize(vbase[T]);
-  r->voff[ns] = vbase[T];
+  for (unsigned p = 0; p < T; ++p) sbase[p + 1] = sbase[p] + out[p].size();
+  r->series.resize(sbase[T]);
   run([&](unsigned p) {
-    uint64_t k = vbase[p];
-    const char *ar = r->arenas[p].data();
-    for (size_t i = 0; i < out[p].size(); ++i) {
-      const SeriesRec &sr = out[p][i];
-      r->series[sbase[p] + i] = sr;
-      r->voff[sbase[p] + i] = k;
-      const char *q = ar + sr.off;
-      for (size_t j = 0, nn = r->fam[sr.fam].names.size(); j < nn; ++j) {
-        r->value_ptrs[k++] = q;
-        q += strlen(q) + 1;
-      }
-    }
+    std::copy(out[p].begin(), out[p].end(), r->series.begin() + sbase[p]);
     std::vector<SeriesRec>().swap(out[p]);
   });
   return GPUAGG_OK;
@@ -3530,9 +3518,61 @@ inline char *escape_raw(char *o, const char *s) {
   return o;
 }
 
+// Label values of a series, in label order, from its arena block (NUL-separated).
+inline void series_values(const gpuagg_result *r, const SeriesRec &sr, size_t nl, const char **v) {
+  const char *q = r->arenas[sr.arena].data() + sr.off;
+  for (size_t j = 0; j < nl; ++j) {
+    v[j] = q;
+    q += strlen(q) + 1;
+  }
+}
+
+void build_value_ptrs(const gpuagg_result *r) {
+  const size_t ns = r->series.size();
+  r->voff.resize(ns + 1);
+  uint64_t nv = 0;
+  for (size_t i = 0; i < ns; ++i) {
+    r->voff[i] = nv;
+    nv += r->fam[r->series[i].fam].names.size();
+  }
+  r->voff[ns] = nv;
+  r->value_ptrs.resize(nv);
+  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)std::max(1u, std::thread::hardware_concurrency()),
+                                                                    ns / 65536 + 1}));
+  run_par(T, [&](unsigned t) {
+    for (size_t i = ns * t / T; i < ns * (t + 1) / T; ++i)
+      series_values(r, r->series[i], r->voff[i + 1] - r->voff[i], r->value_ptrs.data() + r->voff[i]);
+  });
+}
+
+// A sample value as expfmt writes it (go_float_u64_into) at w; returns its length.
+inline size_t put_value(char *w, uint64_t x) {
+  if (x < 1000000) {  // plain integer digits (go_float_u64_into's short case)
+    char d[8];
+    size_t m = 0;
+    do {
+      d[m++] = (char)('0' + x % 10);
+      x /= 10;
+    } while (x);
+    for (size_t k = 0; k < m; ++k) w[k] = d[m - 1 - k];
+    return m;
+  }
+  std::string f;
+  go_float_u64_into(f, x);
+  memcpy(w, f.data(), f.size());
+  return f.size();
+}
+
+inline size_t escaped_len(const char *s) {
+  size_t e = 0;
+  for (; *s; ++s) e += 1 + (*s == '\\' || *s == '"' || *s == '\n');
+  return e;
+}
+
 // gpuagg_result_render_text's text, built once per result: families sorted by name
-// (expfmt), each family's series in client_golang's order, rendered in parallel chunks
-// and copied into place in parallel.
+// (expfmt), each family's series in client_golang's order.  Every series' exact length is
+// known first (its label bytes from render_series), so the threads write straight into
+// the final buffer at their offsets.
 void render_text(const gpuagg_result *r) {
   std::vector<std::vector<size_t>> by_fam(r->fam.size());
   for (size_t i = 0; i < r->series.size(); ++i) by_fam[r->series[i].fam].push_back(i);
@@ -3540,99 +3580,132 @@ void render_text(const gpuagg_result *r) {
   for (size_t f = 0; f < by_fam.size(); ++f)
     if (!by_fam[f].empty()) fam[r->fam[f].metric] = f;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  // pieces in output order: (pointer, size); text they point at lives in `store`
-  std::vector<std::pair<const char *, size_t>> piece;
-  std::vector<std::unique_ptr<std::string>> store;
+  struct Job {
+    const std::string *text = nullptr;  // a fixed block (extra family, header) ...
+    std::string own;
+    size_t f = 0;  // ... or family f's series
+    unsigned T = 1;
+    std::vector<std::string> lab;
+    std::vector<uint64_t> at;  // series q's offset within the job (n + 1)
+    uint64_t base = 0, size = 0;
+  };
+  std::vector<Job> jobs;
   std::map<std::string, int> names;  // every family name, extra blocks included
   for (auto &kv : r->extra_text) names[kv.first] = 0;
   for (auto &kv : fam) names[kv.first] = 0;
   for (auto &nk : names) {
     auto ex = r->extra_text.find(nk.first);
-    if (ex != r->extra_text.end()) piece.push_back({ex->second.data(), ex->second.size()});
+    if (ex != r->extra_text.end()) {
+      jobs.emplace_back();
+      jobs.back().text = &ex->second;
+      jobs.back().size = ex->second.size();
+    }
     auto fi = fam.find(nk.first);
     if (fi == fam.end()) continue;
-    std::vector<size_t> &idx = by_fam[fi->second];
-    const ResultFamily &F = r->fam[fi->second];
-    const size_t nl = F.names.size();
-    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, idx.size() / 8192 + 1}));
-    sort_family(r, F, idx, T);
+    const size_t f = fi->second;
+    std::vector<size_t> &idx = by_fam[f];
+    const ResultFamily &F = r->fam[f];
+    const size_t nl = F.names.size(), n = idx.size();
+    jobs.emplace_back();
+    Job &h = jobs.back();
+    h.own = "# HELP " + nk.first + " ";
+    escape_cstr(h.own, F.help, false);
+    h.own += "\n# TYPE " + nk.first + " " + F.type + "\n";
+    h.size = h.own.size();
+    jobs.emplace_back();
+    Job &j = jobs.back();
+    j.f = f;
+    j.T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, n / 8192 + 1}));
+    sort_family(r, F, idx, j.T);
     // label prefixes: {name=" then ",name=" ; closed by "}
-    std::vector<std::string> lab(nl);
-    for (size_t k = 0; k < nl; ++k) lab[k] = (k ? "\"," : "{") + F.names[F.by_name[k]] + "=\"";
-    auto head = std::make_unique<std::string>("# HELP " + nk.first + " ");
-    escape_cstr(*head, F.help, false);
-    *head += "\n# TYPE " + nk.first + " " + F.type + "\n";
-    piece.push_back({head->data(), head->size()});
-    store.push_back(std::move(head));
-    std::vector<std::unique_ptr<std::string>> chunk(T);
-    for (auto &c : chunk) c = std::make_unique<std::string>();
-    run_par(T, [&](unsigned t) {
-      const size_t q0 = idx.size() * t / T, q1 = idx.size() * (t + 1) / T;
-      size_t bound = 0;
-      for (size_t q = q0; q < q1; ++q) {
-        const char *const *v = r->value_ptrs.data() + r->voff[idx[q]];
-        bound += F.metric.size() + 2 + 32;
-        for (size_t k = 0; k < nl; ++k) bound += lab[k].size() + 2 * strlen(v[F.by_name[k]]);
+    j.lab.resize(nl);
+    size_t fixed = F.metric.size() + 2 + (nl ? 2 : 0);  // ' ' '\n' and '"}'
+    for (size_t k = 0; k < nl; ++k) {
+      j.lab[k] = (k ? "\"," : "{") + F.names[F.by_name[k]] + "=\"";
+      fixed += j.lab[k].size();
+    }
+    j.at.assign(n + 1, 0);
+    std::vector<uint64_t> part(j.T + 1, 0);
+    run_par(j.T, [&](unsigned t) {  // lengths, then chunk sums
+      char scratch[32];
+      std::vector<const char *> v(nl);
+      uint64_t sum = 0;
+      for (size_t q = n * t / j.T; q < n * (t + 1) / j.T; ++q) {
+        const SeriesRec &sr = r->series[idx[q]];
+        uint64_t len = fixed + put_value(scratch, sr.value);
+        if (!sr.esc) {
+          len += sr.len - nl;
+        } else {
+          series_values(r, sr, nl, v.data());
+          for (size_t k = 0; k < nl; ++k) len += escaped_len(v[k]);
+        }
+        j.at[q + 1] = len;
+        sum += len;
       }
-      std::string &o = *chunk[t];
-      o.resize(bound);
-      char *w = &o[0];
-      for (size_t q = q0; q < q1; ++q) {
+      part[t + 1] = sum;
+    });
+    for (unsigned t = 0; t < j.T; ++t) part[t + 1] += part[t];
+    run_par(j.T, [&](unsigned t) {  // offsets
+      uint64_t o = part[t];
+      for (size_t q = n * t / j.T; q < n * (t + 1) / j.T; ++q) {
+        const uint64_t len = j.at[q + 1];
+        j.at[q] = o;
+        o += len;
+      }
+    });
+    j.at[n] = part[j.T];
+    j.size = part[j.T];
+  }
+  uint64_t N = 0;
+  for (Job &j : jobs) {
+    j.base = N;
+    N += j.size;
+  }
+  r->text.reset(new char[N + 1]);  // (not zeroed: every byte is written below, page faults spread over the threads)
+  r->text_len = N;
+  char *out = r->text.get();
+  out[N] = '\0';
+  for (Job &j : jobs) {
+    if (j.text || !j.own.empty()) {
+      const std::string &t = j.text ? *j.text : j.own;
+      memcpy(out + j.base, t.data(), t.size());
+      continue;
+    }
+    const ResultFamily &F = r->fam[j.f];
+    const std::vector<size_t> &idx = by_fam[j.f];
+    const size_t nl = F.names.size(), n = idx.size();
+    run_par(j.T, [&](unsigned t) {
+      std::vector<const char *> v(nl);
+      for (size_t q = n * t / j.T; q < n * (t + 1) / j.T; ++q) {
         const size_t i = idx[q];
+        const SeriesRec &sr = r->series[i];
+        char *w = out + j.base + j.at[q];
         memcpy(w, F.metric.data(), F.metric.size());
         w += F.metric.size();
-        const char *const *v = r->value_ptrs.data() + r->voff[i];
+        series_values(r, sr, nl, v.data());
+        const char *end = r->arenas[sr.arena].data() + sr.off + sr.len;
         for (size_t k = 0; k < nl; ++k) {
-          memcpy(w, lab[k].data(), lab[k].size());
-          w += lab[k].size();
-          w = escape_raw(w, v[F.by_name[k]]);
+          memcpy(w, j.lab[k].data(), j.lab[k].size());
+          w += j.lab[k].size();
+          const size_t p = F.by_name[k];
+          if (!sr.esc) {
+            const size_t L = (size_t)((p + 1 < nl ? v[p + 1] : end) - v[p]) - 1;
+            memcpy(w, v[p], L);
+            w += L;
+          } else {
+            w = escape_raw(w, v[p]);
+          }
         }
         if (nl) {
           *w++ = '"';
           *w++ = '}';
         }
         *w++ = ' ';
-        const uint64_t x = r->series[i].value;
-        if (x < 1000000) {  // plain integer digits (go_float_u64_into's short case)
-          char d[8];
-          int m = 0;
-          uint64_t y = x;
-          do {
-            d[m++] = (char)('0' + y % 10);
-            y /= 10;
-          } while (y);
-          while (m) *w++ = d[--m];
-        } else {
-          std::string f;
-          go_float_u64_into(f, x);
-          memcpy(w, f.data(), f.size());
-          w += f.size();
-        }
+        w += put_value(w, sr.value);
         *w++ = '\n';
       }
-      o.resize((size_t)(w - o.data()));
     });
-    for (auto &c : chunk) {
-      piece.push_back({c->data(), c->size()});
-      store.push_back(std::move(c));
-    }
   }
-  std::vector<size_t> at(piece.size() + 1, 0);
-  for (size_t i = 0; i < piece.size(); ++i) at[i + 1] = at[i] + piece[i].second;
-  const size_t N = at[piece.size()];
-  r->text.reset(new char[N + 1]);  // (not zeroed: every byte is copied below, page faults spread over the threads)
-  r->text_len = N;
-  char *out = r->text.get();
-  out[N] = '\0';
-  const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, N / (1u << 22) + 1}));
-  run_par(T, [&](unsigned t) {  // byte range [t * N / T, (t + 1) * N / T) of the output
-    const size_t b0 = N * t / T, b1 = N * (t + 1) / T;
-    size_t i = std::upper_bound(at.begin(), at.end(), b0) - at.begin() - 1;
-    for (; i < piece.size() && at[i] < b1; ++i) {
-      const size_t s0 = std::max(b0, at[i]), s1 = std::min(b1, at[i + 1]);
-      if (s1 > s0) memcpy(out + s0, piece[i].first + (s0 - at[i]), s1 - s0);
-    }
-  });
   r->text_done = true;
 }
 }  // namespace
@@ -3655,7 +3728,10 @@ int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, 
   if (metric) *metric = f.metric.c_str();
   if (n_labels) *n_labels = (uint32_t)f.names.size();
   if (names) *names = f.name_ptrs.data();
-  if (values) *values = r->value_ptrs.data() + r->voff[i];
+  if (values) {
+    std::call_once(r->ptrs_once, [r] { build_value_ptrs(r); });
+    *values = r->value_ptrs.data() + r->voff[i];
+  }
   if (value) *value = s.value;
   return GPUAGG_OK;
 }
