@@ -3163,24 +3163,35 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   run([&](unsigned p) {
     size_t total = 0;
     for (unsigned t = 0; t < T; ++t) total += parts[t][p].size();
-    std::unordered_map<LKey, std::pair<uint64_t, uint64_t>, LKeyHash> m;
-    m.reserve(total);
+    // open addressing (linear probing, at most half full); w[0] (the view) is never ~0
+    size_t cap = 16;
+    while (cap < 2 * total) cap <<= 1;
+    std::vector<LItem> tab(cap);
+    for (LItem &e : tab) e.k.w[0] = ~0u;
+    size_t NM = 0;
     for (unsigned t = 0; t < T; ++t) {
       for (const LItem &it : parts[t][p]) {
-        auto &a = m[it.k];
-        a.first += it.cnt;
-        a.second += it.byt;
+        size_t h = fmix64(LKeyHash()(it.k)) & (cap - 1);
+        while (tab[h].k.w[0] != ~0u && !(tab[h].k == it.k)) h = (h + 1) & (cap - 1);
+        LItem &e = tab[h];
+        if (e.k.w[0] == ~0u) {
+          e = it;
+          ++NM;
+        } else {
+          e.cnt += it.cnt;
+          e.byt += it.byt;
+        }
       }
       std::vector<LItem>().swap(parts[t][p]);
     }
-    const size_t NM = m.size();
     std::vector<char> &ar = r->arenas[p];
     std::vector<uint32_t> &tk = r->toks[p];
-    ar.reserve(m.size() * 48);
-    tk.reserve(m.size() * 4);
-    out[p].reserve(m.size() * 2);
-    for (const auto &kv : m) {
-      const LKey &k = kv.first;
+    ar.reserve(NM * 48);
+    tk.reserve(NM * 4);
+    out[p].reserve(NM * 2);
+    for (const LItem &kv : tab) {
+      if (kv.k.w[0] == ~0u) continue;
+      const LKey &k = kv.k;
       const View &v = views[k.w[0]];
       const Group &g = c->groups[v.group];
       // the view's instances (count / bytes objects) share the labels: rendered once
@@ -3233,7 +3244,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
       const char *b = ar.data() + off;
       const uint32_t esc = memchr(b, '\\', len) || memchr(b, '"', len) || memchr(b, '\n', len);
       for (uint32_t ii : v.insts)
-        out[p].push_back(SeriesRec{ii, p, off, c->inst[ii].vk == VK_BYTES ? kv.second.second : kv.second.first, tok,
+        out[p].push_back(SeriesRec{ii, p, off, c->inst[ii].vk == VK_BYTES ? kv.byt : kv.cnt, tok,
                                    len, esc});
     }
   });
