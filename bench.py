@@ -344,6 +344,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
     ap.add_argument("--no-scrape", action="store_true", help="skip the snapshot / render timing")
+    ap.add_argument("--production-only", action="store_true",
+                    help="diagnostic: only the production-geometry launches (for rocprof), no bench line")
     ap.add_argument("--no-production", action="store_true",
                     help="skip the Go-batch-size (1M-record) device-resident launches")
     args = ap.parse_args()
@@ -388,6 +390,11 @@ def main():
     for p in last.dns:
         g.dns_intern(p.rcode, p.qtypes, p.query, p.ips, p.num_answers)
     dcols = GpuAgg.device_columns(*cols)
+
+    if args.production_only:  # diagnostic (rocprof of the 2^20-record launches)
+        print(json.dumps({"production": production_geometry(g, cols, n, bpr, 0.0)}), flush=True)
+        g.close()
+        return
 
     for _ in range(args.warmup):
         g.submit_device(dcols, n)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, bench lines, rocprofv3 summaries, PMC passes.
 #   bash scripts/gpu_check.sh TAG STEP...
-# STEP: build | tests[:PYTEST_ARGS] | smoke | bench:CFG | prof:CFG | pmc:CFG | micro | microlds
+# STEP: build | tests[:PYTEST_ARGS] | smoke | bench:CFG | prof:CFG | pprof:CFG | pmc:CFG | micro | microlds
 #       (CFG = c1..c5, default c2; tests:k=A,B runs `-k "A or B"`)
 # Every GPU step has its own time limit; a crash, abort or timeout stops the script.
 TAG=${1:-run}
@@ -43,6 +43,12 @@ for s in $STEPS; do
         > "$OUT/${TAG}_prof_${cfg}.log" 2>&1
       rc=$?; echo "prof rc=$rc" >> "$OUT/${TAG}_prof_${cfg}.log"; [ $rc -ne 0 ] && exit $rc
       find "$OUT/${TAG}_prof_${cfg}" -name "*kernel_stats.csv" -exec cp {} "$OUT/${TAG}_${cfg}_kernel_stats.csv" \; ;;
+    pprof)
+      # the production-geometry launches alone (bench.py --production-only)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_pprof_${cfg}" -o run \
+        -- python3 "$R/bench.py" --config "$cfg" --production-only > "$OUT/${TAG}_pprof_${cfg}.log" 2>&1
+      rc=$?; echo "pprof rc=$rc" >> "$OUT/${TAG}_pprof_${cfg}.log"; [ $rc -ne 0 ] && exit $rc
+      find "$OUT/${TAG}_pprof_${cfg}" -name "*kernel_stats.csv" -exec cp {} "$OUT/${TAG}_${cfg}_pprof_kernel_stats.csv" \; ;;
     pmc)
       # one counter group per pass (MI355X_MICROARCH.md: rocprofv3 PMC slots; TCC: FETCH_SIZE
       # uses 3 of 4, WRITE_SIZE 2, so they take separate passes)
