@@ -3186,8 +3186,9 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     }
     std::vector<char> &ar = r->arenas[p];
     std::vector<uint32_t> &tk = r->toks[p];
-    ar.reserve(NM * 48);
-    tk.reserve(NM * 4);
+    // (reserved generously: pages never written are never faulted in)
+    ar.reserve(NM * 320);
+    tk.reserve(NM * 16);
     out[p].reserve(NM * 2);
     for (const LItem &kv : tab) {
       if (kv.k.w[0] == ~0u) continue;
@@ -3462,8 +3463,11 @@ void escape_into(std::string &out, const std::string &s, bool quote) { escape_cs
 // Series of one family in exposition order (client_golang sorts a family's metrics by
 // their label values taken in label-name order; MetricSorter), on the values' sort tokens
 // (render_series): packed into one 128-bit key when their widths fit, else as rows.
-void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size_t> &idx, unsigned T) {
+void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size_t> &idx, unsigned T,
+                 std::vector<uint32_t> &perm) {
   const size_t n = idx.size(), nl = F.names.size();
+  perm.resize(n);
+  for (size_t q = 0; q < n; ++q) perm[q] = (uint32_t)q;
   if (n < 2 || nl == 0) return;
   std::vector<uint32_t> rk(n * nl);  // tokens in name order
   std::vector<std::vector<uint32_t>> mx(T, std::vector<uint32_t>(nl, 0));
@@ -3486,7 +3490,6 @@ void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size
     while (bits[k] < 32 && (m >> bits[k])) ++bits[k];
     tbits += bits[k];
   }
-  const std::vector<size_t> old = idx;
   if (tbits <= 128) {
     using K = std::pair<unsigned __int128, uint32_t>;
     std::vector<K> keys(n);
@@ -3498,7 +3501,7 @@ void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size
       }
     });
     par_sort(keys, [](const K &a, const K &b) { return a.first < b.first; }, T);
-    for (size_t q = 0; q < n; ++q) idx[q] = old[keys[q].second];
+    for (size_t q = 0; q < n; ++q) perm[q] = keys[q].second;
   } else {
     std::vector<uint32_t> ord(n);
     for (size_t q = 0; q < n; ++q) ord[q] = (uint32_t)q;
@@ -3508,8 +3511,10 @@ void sort_family(const gpuagg_result *r, const ResultFamily &F, std::vector<size
         if (x[k] != y[k]) return x[k] < y[k];
       return false;
     }, T);
-    for (size_t q = 0; q < n; ++q) idx[q] = old[ord[q]];
+    perm = std::move(ord);
   }
+  const std::vector<size_t> old = idx;
+  for (size_t q = 0; q < n; ++q) idx[q] = old[perm[q]];
 }
 
 // expfmt escaping of a label value into a raw buffer sized for the worst case (2x)
@@ -3591,6 +3596,20 @@ void render_text(const gpuagg_result *r) {
   for (size_t f = 0; f < by_fam.size(); ++f)
     if (!by_fam[f].empty()) fam[r->fam[f].metric] = f;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  // families whose series share their labels series for series (the count and bytes
+  // objects of one view): sorted once, the partner takes the same permutation
+  std::vector<int> partner(r->fam.size(), -1);
+  for (size_t f = 0; f < by_fam.size(); ++f)
+    for (size_t g = 0; g < f && partner[f] < 0; ++g) {
+      if (by_fam[g].size() != by_fam[f].size() || by_fam[f].empty() || r->fam[g].names != r->fam[f].names) continue;
+      bool same = true;
+      for (size_t q = 0; same && q < by_fam[f].size(); ++q) {
+        const SeriesRec &a = r->series[by_fam[f][q]], &b = r->series[by_fam[g][q]];
+        same = a.arena == b.arena && a.off == b.off;
+      }
+      if (same) partner[f] = (int)g;
+    }
+  std::vector<std::vector<uint32_t>> perms(r->fam.size());
   struct Job {
     const std::string *text = nullptr;  // a fixed block (extra family, header) ...
     std::string own;
@@ -3627,7 +3646,17 @@ void render_text(const gpuagg_result *r) {
     Job &j = jobs.back();
     j.f = f;
     j.T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, n / 8192 + 1}));
-    sort_family(r, F, idx, j.T);
+    const int pg = partner[f] >= 0 ? partner[f] : -1;
+    int done = -1;  // a sorted family of this one's group
+    for (size_t g = 0; g < r->fam.size(); ++g)
+      if (!perms[g].empty() && ((int)g == pg || partner[g] == (int)f || (pg >= 0 && partner[g] == pg))) done = (int)g;
+    if (done >= 0) {
+      const std::vector<size_t> old = idx;
+      for (size_t q = 0; q < n; ++q) idx[q] = old[perms[done][q]];
+      perms[f] = perms[done];
+    } else {
+      sort_family(r, F, idx, j.T, perms[f]);
+    }
     // label prefixes: {name=" then ",name=" ; closed by "}
     j.lab.resize(nl);
     size_t fixed = F.metric.size() + 2 + (nl ? 2 : 0);  // ' ' '\n' and '"}'
@@ -3687,7 +3716,12 @@ void render_text(const gpuagg_result *r) {
     const size_t nl = F.names.size(), n = idx.size();
     run_par(j.T, [&](unsigned t) {
       std::vector<const char *> v(nl);
-      for (size_t q = n * t / j.T; q < n * (t + 1) / j.T; ++q) {
+      const size_t q1 = n * (t + 1) / j.T;
+      for (size_t q = n * t / j.T; q < q1; ++q) {
+        if (q + 8 < q1) {  // the series 8 ahead: its labels are a random arena line
+          const SeriesRec &ahead = r->series[idx[q + 8]];
+          __builtin_prefetch(r->arenas[ahead.arena].data() + ahead.off);
+        }
         const size_t i = idx[q];
         const SeriesRec &sr = r->series[i];
         char *w = out + j.base + j.at[q];
