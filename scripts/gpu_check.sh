@@ -66,7 +66,10 @@ for s in $STEPS; do
       done
       python scripts/pmc_summary.py "$OUT/${TAG}_pmc_${cfg}.json" "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" roofline.kernel)" \
         "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" config.records_per_gpu)" \
-        "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" build_id)" "$OUT"/${TAG}_pmc_${cfg}_[0-9]* > /dev/null 2>> "$OUT/${TAG}_pmc_${cfg}_1.log" ;;
+        "$(python scripts/bench_field.py "$OUT/${TAG}_pmc_${cfg}_1.log" build_id)" "$OUT"/${TAG}_pmc_${cfg}_[0-9]* > /dev/null 2>> "$OUT/${TAG}_pmc_${cfg}_1.log"
+      # this box's later bench lines read the fresh summary (bench.py takes it only when its
+      # build id is the loaded library's); scripts/collect_round.py copies it into the tree
+      [ -s "$OUT/${TAG}_pmc_${cfg}.json" ] && cp "$OUT/${TAG}_pmc_${cfg}.json" "$R/profiles/pmc_${cfg}.json" ;;
     ablate)
       ABLATE_ONLY="$arg" timeout -k 10 600 python scripts/ablate.py > "$OUT/${TAG}_ablate.jsonl" 2> "$OUT/${TAG}_ablate.err"
       rc=$?; echo "ablate rc=$rc" >> "$OUT/${TAG}_ablate.err"; [ $rc -ne 0 ] && exit $rc ;;
