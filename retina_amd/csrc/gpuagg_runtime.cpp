@@ -630,13 +630,10 @@ constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 // snapshot), state export, merge, slot retirement and dense re-layout.
 int fold_pending_sketch(gpuagg_ctx *c);
 
-int fold_pending(gpuagg_ctx *c) {
-  if (c->cpu) {  // the host threads' accumulators into the ctx's counters and table
-    c->cpu->flush();
-    return GPUAGG_OK;
-  }
-  if (int rc = fold_pending_sketch(c)) return rc;
-  if (!c->pend.active) return GPUAGG_OK;
+// The aggregation launches' deferred lists only (their own budget ran out: the sketch
+// lists keep theirs).
+int fold_pending_dense(gpuagg_ctx *c) {
+  if (c->cpu || !c->pend.active) return GPUAGG_OK;
   c->pend.active = false;
   LaunchArgs f = c->pend.a;
   if (!f.stage_defer) f.stage_a = nullptr;  // summed per launch, unless the copies accumulate
@@ -655,6 +652,15 @@ int fold_pending(gpuagg_ctx *c) {
     c->pending_fold.push_back(ev);
   }
   return GPUAGG_OK;
+}
+
+int fold_pending(gpuagg_ctx *c) {
+  if (c->cpu) {  // the host threads' accumulators into the ctx's counters and table
+    c->cpu->flush();
+    return GPUAGG_OK;
+  }
+  if (int rc = fold_pending_sketch(c)) return rc;
+  return fold_pending_dense(c);
 }
 
 // The state is being cleared: the waiting lists are discarded with it.
@@ -1402,7 +1408,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       a.stage_a_stride = (a.lds_bins + 3u) & ~3u;
       // accumulating copies are summed before their buffer can be reallocated
       if (c->pend.active && c->pend.a.stage_defer && (size_t)a.blocks * a.stage_a_stride > c->stage_a_alloc &&
-          (rc = fold_pending(c)))
+          (rc = fold_pending_dense(c)))
         return rc;
       if ((rc = ensure_buf(c, &c->d_stage_a, &c->stage_a_alloc, (size_t)a.blocks * a.stage_a_stride)))
         return rc;
@@ -1488,7 +1494,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
               q.lds_bins == a.lds_bins && q.dense_len == c->dense_len && q.dense_cnt == c->d_dense_cnt &&
               q.dense_byt == c->d_dense_byt && q.sparse.k0 == c->sv.k0;
       if (accum) budget = c->pend.budget;
-      else if ((rc = fold_pending(c))) return rc;
+      else if ((rc = fold_pending_dense(c))) return rc;
     }
     const Geom g = geom(budget);
     if (g.nwin) {
