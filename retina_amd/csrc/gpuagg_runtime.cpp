@@ -846,9 +846,9 @@ constexpr uint32_t kCmsWindowShift = 15, kCmsMaxWindows = 4096;
 // pod-in-window in 8 bits and the register index in 18, so p <= 17 and shift <= 8)
 constexpr uint32_t kHllWindowLog2Bytes = 17, kHllMaxWindows = 8192;
 
-// Records per scatter workgroup between deferred sketch folds (64 launches of the Go
-// plugin's 2^20-record batches over 256 workgroups).
-constexpr uint64_t kSketchDeferRecords = 1ull << 18;
+// Records per scatter workgroup between deferred sketch folds (256 launches of the Go
+// plugin's 2^20-record batches over 256 workgroups; ~3.8 GB of lists at C3's geometry).
+constexpr uint64_t kSketchDeferRecords = 1ull << 20;
 
 // HLL level-2 (split) lists for `records` scatter entries at most: m / (nsup * b2 * nfine)
 // per list, +25 % + 64 of headroom (a full list applies the update with the global CAS).
@@ -1210,7 +1210,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 }
 
 // Launches whose list folds may wait for one fold_pending (see Pending).
-constexpr uint64_t kDeferLaunches = 16;
+constexpr uint64_t kDeferLaunches = 64;
 // Default device memory for the wide-key segment lists of one ctx (32-byte entries;
 // gpuagg_config.wide_list_mib overrides it): 32 GiB (1024 entries per workgroup and segment at 2^24
 // slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
@@ -1466,7 +1466,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       return g;
     };
     // Deferred folds: while the geometry holds, launches keep appending to the same lists
-    // (their counters start from the stored fill) for up to kDeferLaunches (16) launches' worth
+    // (their counters start from the stored fill) for up to kDeferLaunches (64) launches' worth
     // of records per workgroup, and fold_pending folds them once.
     // Plans with compact-key lists always defer: their fold pays a fixed pass over the
     // group-by table.  Spill-only plans (C2, C4) defer only small launches (at most

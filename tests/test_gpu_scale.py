@@ -127,14 +127,14 @@ DEFER = [
 @pytest.mark.parametrize("cid,sp,remote,npods,gen", DEFER, ids=[d[0] for d in DEFER])
 def test_deferred_folds_exact(gpu_device, cid, sp, remote, npods, gen):
     """Spill / segment lists of consecutive launches are folded once (gpuagg_sync or any
-    state read).  43 batches of unequal sizes: a growing chunk changes the list geometry,
-    a snapshot folds early, then 36 equal batches exhaust the 16-launch budget twice --
+    state read).  143 batches of unequal sizes: a growing chunk changes the list geometry,
+    a snapshot folds early, then 136 equal batches exhaust the 64-launch budget twice --
     every case equals the C port and the engine folding after each batch."""
     from retina_amd import GpuAgg, _abi
     from .helpers import to_device
     pods = W.make_pods(npods, seed=8)
     recs = W.gen_records(2_000_000, pods, seed=81, **gen)
-    sizes = [30_000, 30_000, 250_000, 20_000] + [25_000] * 36 + [400_000, 10_007, 333_333]
+    sizes = [30_000, 30_000, 250_000, 20_000] + [6_800] * 136 + [400_000, 10_007, 333_333]
     bounds = np.concatenate([[0], np.cumsum(sizes)])
     assert bounds[-1] <= len(recs)
     n_mid, n = int(bounds[4]), int(bounds[-1])
@@ -146,7 +146,7 @@ def test_deferred_folds_exact(gpu_device, cid, sp, remote, npods, gen):
             mid = None
             for k, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
                 g.submit_device(GpuAgg.device_columns(*[x[int(a):] for x in ts]), int(b - a))
-                if k == 3:  # then 36 equal batches: more than kDeferLaunches (16) per budget
+                if k == 3:  # then 136 equal batches: more than kDeferLaunches (64) per budget
                     mid = g.snapshot()
             return mid, g.snapshot()
         finally:
