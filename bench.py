@@ -296,8 +296,9 @@ SCRAPE_EPOCH_S = 15.0
 def scrape_cost(g, reps: int = 3):
     """Host-side cost of one scrape on the state the timed region left: gpuagg_snapshot
     (device sync, table compaction and D2H, label rendering of every series) and
-    gpuagg_result_render_text (client_golang's text exposition: rendered by the sizing call,
-    then copied into the caller's buffer), median of `reps` after a first, cold scrape
+    gpuagg_result_text (client_golang's text exposition, rendered once and handed out
+    without a copy; the copying gpuagg_result_render_text is timed beside it), median of
+    `reps` after a first, cold scrape
     (whose snapshot also builds the canonical label tables, as a scrape does after pod churn
     or new DNS payloads).  The walk a Go publish does over the result is not included."""
     snap, rend, copy, nser, nbytes = [], [], [], 0, 0
@@ -312,12 +313,14 @@ def scrape_cost(g, reps: int = 3):
         try:
             nser = int(g.lib.gpuagg_result_count(r))
             ln = C.c_size_t()
+            ptr = C.c_void_p()
             t2 = time.perf_counter()
-            rc = g.lib.gpuagg_result_render_text(r, None, 0, C.byref(ln))
+            rc = g.lib.gpuagg_result_text(r, C.byref(ptr), C.byref(ln))  # renders; no copy
             t3 = time.perf_counter()
             if out is None or out.size < ln.value + 1:
                 out = np.empty(ln.value + 1, np.uint8)
             t4 = time.perf_counter()
+            # the copying form (gpuagg_result_render_text into a caller buffer), for reference
             rc = rc or g.lib.gpuagg_result_render_text(r, out.ctypes.data_as(C.c_char_p), out.size, C.byref(ln))
             t5 = time.perf_counter()
             if rc != 0:
@@ -331,10 +334,11 @@ def scrape_cost(g, reps: int = 3):
     sm, rm, cm = (float(np.median(x[1:])) for x in (snap, rend, copy))
     return {"series": nser, "text_bytes": nbytes, "snapshot_ms": sm, "render_ms": rm, "copy_ms": cm,
             "cold_snapshot_ms": snap[0], "cold_render_ms": rend[0],
-            "epoch_frac": (sm + rm + cm) / (SCRAPE_EPOCH_S * 1e3),
-            "cold_epoch_frac": (snap[0] + rend[0] + copy[0]) / (SCRAPE_EPOCH_S * 1e3), "epoch_s": SCRAPE_EPOCH_S,
-            "note": "gpuagg_snapshot + gpuagg_result_render_text (render, then copy into the caller's buffer) on "
-                    "the timed region's state: median of %d warm scrapes, and the first (cold) one; host cost per "
+            "epoch_frac": (sm + rm) / (SCRAPE_EPOCH_S * 1e3),
+            "cold_epoch_frac": (snap[0] + rend[0]) / (SCRAPE_EPOCH_S * 1e3), "epoch_s": SCRAPE_EPOCH_S,
+            "note": "gpuagg_snapshot + gpuagg_result_text (the exposition rendered, handed out without a copy) on "
+                    "the timed region's state: median of %d warm scrapes, and the first (cold) one; copy_ms is the "
+                    "extra cost of the copying form gpuagg_result_render_text (not in epoch_frac); host cost per "
                     "scrape epoch, outside `value`" % reps}
 
 

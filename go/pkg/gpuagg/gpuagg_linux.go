@@ -30,6 +30,7 @@ import (
 	"encoding/binary"
 	"errors"
 	"fmt"
+	"io"
 	"net"
 	"strings"
 	"sync"
@@ -748,6 +749,44 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 // AdvancedRegistry vectors with the reference's names, types, Help texts and labels
 // (forward.go:18-26, drops.go:18-23, tcpflags.go:18-24, tcpretrans.go:18-24 -- GaugeVec;
 // dns.go:21-30,50-66 -- CounterVec), then retires the slots of deleted pods.
+// WriteExposition writes the engine's series to w in the Prometheus text exposition
+// format (what the AdvancedRegistry's /metrics handler would serve for them), straight from
+// the library's rendering (gpuagg_result_text: no copy into Go memory).  A /metrics
+// handler for very high cardinalities can serve this instead of walking every series
+// into the GaugeVec/CounterVec objects (publish).
+func (g *gpuAgg) WriteExposition(w io.Writer) error {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if g.stopping || len(g.devs) == 0 {
+		return nil
+	}
+	if len(g.devs) > 1 {
+		ctxs := make([]*C.gpuagg_ctx, len(g.devs))
+		for i, d := range g.devs {
+			ctxs[i] = d.ctx
+		}
+		if err := check(ctxs[0], C.gpuagg_merge(&ctxs[0], C.size_t(len(ctxs))), "gpuagg_merge"); err != nil {
+			return err
+		}
+	}
+	ctx := g.devs[0].ctx
+	var r *C.gpuagg_result
+	if err := check(ctx, C.gpuagg_snapshot(ctx, &r), "gpuagg_snapshot"); err != nil {
+		return err
+	}
+	defer C.gpuagg_result_free(r)
+	var text *C.char
+	var n C.size_t
+	if err := check(ctx, C.gpuagg_result_text(r, &text, &n), "gpuagg_result_text"); err != nil {
+		return err
+	}
+	if n == 0 {
+		return nil
+	}
+	_, err := w.Write(unsafe.Slice((*byte)(unsafe.Pointer(text)), int(n))) // valid until the free above
+	return err
+}
+
 func (g *gpuAgg) publish() error {
 	g.mu.Lock()
 	defer g.mu.Unlock()

@@ -345,6 +345,10 @@ uint64_t gpuagg_result_dropped(const gpuagg_result *r);
  * full length; buf (cap bytes, may be NULL) gets the text and a NUL when it fits,
  * else GPUAGG_ECAPACITY. */
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len);
+/* The same text without a copy: *text points at the result's own NUL-terminated rendering
+ * (valid until gpuagg_result_free), *len its length -- for a /metrics handler that writes
+ * it out as is (a 13.7M-series exposition is 5 GB: the copy alone is ~0.2 s). */
+int gpuagg_result_text(const gpuagg_result *r, const char **text, size_t *len);
 void gpuagg_result_free(gpuagg_result *r);
 
 /* ------------------------------------------------------------------------------

@@ -151,6 +151,7 @@ SIGNATURES = [
     ("gpuagg_result_family", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
     ("gpuagg_result_dropped", C.c_uint64, [C.c_void_p]),
     ("gpuagg_result_render_text", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("gpuagg_result_text", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     ("gpuagg_set_apiserver_ips", C.c_int, [C.c_void_p, u32p, C.c_size_t]),
     ("gpuagg_latency_read", C.c_int, [C.c_void_p, C.POINTER(LatencyState)]),
     ("gpuagg_set_time_offset", C.c_int, [C.c_void_p, C.c_int64]),

@@ -3771,6 +3771,14 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
   return GPUAGG_OK;
 }
 
+int gpuagg_result_text(const gpuagg_result *r, const char **text, size_t *len) {
+  if (!r || !text || !len) return GPUAGG_EINVAL;
+  if (!r->text_done) render_text(r);
+  *text = r->text.get();
+  *len = r->text_len;
+  return GPUAGG_OK;
+}
+
 int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, uint32_t *n_labels,
                          const char *const **names, const char *const **values, uint64_t *value) {
   if (!r || i >= r->series.size()) return GPUAGG_EINVAL;

@@ -359,15 +359,14 @@ class GpuAgg:
 
     # -- output ------------------------------------------------------------------------
     def snapshot_text(self) -> str:
-        """The snapshot in the Prometheus text exposition format (gpuagg_result_render_text)."""
+        """The snapshot in the Prometheus text exposition format (gpuagg_result_text)."""
         r = C.c_void_p()
         self._check(self.lib.gpuagg_snapshot(self.h, C.byref(r)))
         try:
             n = C.c_size_t()
-            self._check(self.lib.gpuagg_result_render_text(r, None, 0, C.byref(n)))
-            buf = C.create_string_buffer(n.value + 1)
-            self._check(self.lib.gpuagg_result_render_text(r, buf, n.value + 1, C.byref(n)))
-            return buf.value.decode()
+            p = C.c_void_p()
+            self._check(self.lib.gpuagg_result_text(r, C.byref(p), C.byref(n)))
+            return C.string_at(p.value, n.value).decode() if n.value else ""
         finally:
             self.lib.gpuagg_result_free(r)
 

@@ -249,6 +249,9 @@ def test_exposition_text_cpu_backend():
             text = buf.value.decode()
             small = C.create_string_buffer(8)
             assert g.lib.gpuagg_result_render_text(r, small, 8, C.byref(n)) != 0  # too small: refused
+            ptr, n2 = C.c_void_p(), C.c_size_t()  # the zero-copy form: the same bytes
+            assert g.lib.gpuagg_result_text(r, C.byref(ptr), C.byref(n2)) == 0
+            assert C.string_at(ptr.value, n2.value) == buf.raw[:n.value] and n2.value == n.value
         finally:
             g.lib.gpuagg_result_free(r)
     finally:
