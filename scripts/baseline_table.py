@@ -49,7 +49,7 @@ def rows(path):
 
 def scrape_rows(paths):
     """Scrape cost per config: gpuagg_snapshot + gpuagg_result_render_text on the bench's state."""
-    out = ["| Config | series | text MB | snapshot ms | render + copy ms | % of a 15 s epoch (warm) | cold scrape ms | % (cold) |",
+    out = ["| Config | series | text MB | snapshot ms | render ms (+ copy, copying API) | % of a 15 s epoch (warm) | cold scrape ms | % (cold) |",
            "|---|---|---|---|---|---|---|---|"]
     for path in paths:
         d = json.load(open(path))
@@ -58,8 +58,8 @@ def scrape_rows(paths):
             continue
         cfg = path.rsplit("_bench_", 1)[-1].replace(".json", "")
         cold = sc.get("cold_snapshot_ms")
-        out.append("| %s | %d | %.1f | %.1f | %.1f | %.2f %% | %s | %s |" % (
-            LABEL[cfg], sc["series"], sc["text_bytes"] / 1e6, sc["snapshot_ms"], sc["render_ms"] + sc.get("copy_ms", 0.0),
+        out.append("| %s | %d | %.1f | %.1f | %.1f (+ %.1f) | %.2f %% | %s | %s |" % (
+            LABEL[cfg], sc["series"], sc["text_bytes"] / 1e6, sc["snapshot_ms"], sc["render_ms"], sc.get("copy_ms", 0.0),
             100 * sc["epoch_frac"], "%.0f" % (cold + sc["cold_render_ms"]) if cold is not None else "—",
             "%.2f %%" % (100 * sc["cold_epoch_frac"]) if cold is not None else "—"))
     return out
