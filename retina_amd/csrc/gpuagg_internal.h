@@ -253,14 +253,6 @@ GA_HD uint32_t iprd_block(uint32_t ip, uint32_t p0, uint32_t p1, uint32_t p2, ui
   return rel < ((d >> 8) & 0x1FFu) ? (d >> 17) + rel : 0u;
 }
 
-// iprd_block of an image with one /16 prefix (the other descriptors are 0, so the 4-way
-// select above gives the same block): one compare instead of four per IP.
-GA_HD uint32_t iprd_block1(uint32_t ip, uint32_t p0, uint32_t d0) {
-  const uint32_t d = (ip & 0xFFFFu) == p0 ? d0 : 0u;
-  const uint32_t rel = ((ip >> 16) & 0xFFu) - (d & 0xFFu);
-  return rel < ((d >> 8) & 0x1FFu) ? (d >> 17) + rel : 0u;
-}
-
 // 32-bit LDS bins of the tier-1 kernel: bytes families pack count:12 | bytes:20 and
 // correct the rare carry / wrap exactly with global atomics; count-only families
 // (tcpflags, tcpretrans) use the whole word (<= 2^20 records per workgroup).

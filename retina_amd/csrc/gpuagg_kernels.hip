@@ -715,15 +715,13 @@ __device__ __forceinline__ uint32_t ipl_probe_index(const uint32_t *keys, uint32
 __device__ __forceinline__ uint32_t ipl_slot(const uint16_t *vals, uint32_t j) { return vals[j]; }
 
 // One IP through the tier-1 LDS image: slot or kIplNoSlot (inactive lanes: kIplNoSlot).
-// kIp 1: the radix image (two dependent u16 reads); 2: the dense radix image (one read);
-// 3: the dense radix image with a single /16 prefix (dense_lds_kernel only); 0: cuckoo.
+// kRadix: the radix image (two dependent u16 reads); else the cuckoo image.
 template <int kIp>
 struct IplView {
   const uint8_t *smem;
   uint32_t nb, seed, npfx, p0, p1, p2, p3;
   uint32_t d0, d1, d2, d3;  // kIp 2: the dense radix descriptors
   __device__ __forceinline__ uint32_t lookup(uint32_t ip) const {
-    if (kIp == 3) return ((const uint16_t *)smem)[(iprd_block1(ip, p0, d0) << 8) | (ip >> 24)];
     if (kIp == 2)
       return ((const uint16_t *)smem)[(iprd_block(ip, p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip >> 24)];
     if (kIp == 1) {
@@ -736,11 +734,7 @@ struct IplView {
   // for every lane (inactive lanes hold a clamped real record) and the result is masked
   // after: a select on the index made the compiler branch per IP
   __device__ __forceinline__ void lookup8(const uint32_t (&ip)[8], bool act, uint32_t (&sl)[8]) const {
-    if (kIp == 3) {  // dense radix image of one /16 prefix
-      const uint16_t *blk = (const uint16_t *)smem;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sl[k] = blk[(iprd_block1(ip[k], p0, d0) << 8) | (ip[k] >> 24)];
-    } else if (kIp == 2) {  // one LDS read per IP
+    if (kIp == 2) {  // one LDS read per IP
       const uint16_t *blk = (const uint16_t *)smem;
 #pragma unroll
       for (int k = 0; k < 8; ++k) sl[k] = blk[(iprd_block(ip[k], p0, p1, p2, p3, d0, d1, d2, d3) << 8) | (ip[k] >> 24)];
@@ -3017,12 +3011,10 @@ static hipError_t launch_k(K kern, const KArgs &k, uint32_t blocks, uint32_t thr
 // dense_lds_kernel<NG, ., SIG, .> by the launch's vector loads and LDS image form
 template <int NG, uint32_t SIG>
 static hipError_t launch_lds(const LaunchArgs &a, const KArgs &k, uint32_t B, uint32_t T, size_t lds, hipStream_t st) {
-  // (a dense image of one /16 prefix -- C2's 10k pods -- takes the one-compare probe)
   if (a.vec)
-    return a.ipl_dense && a.ipl_npfx == 1 ? launch_k(dense_lds_kernel<NG, true, SIG, 3>, k, B, T, lds, st)
-           : a.ipl_dense                  ? launch_k(dense_lds_kernel<NG, true, SIG, 2>, k, B, T, lds, st)
-           : a.ipl_radix                  ? launch_k(dense_lds_kernel<NG, true, SIG, 1>, k, B, T, lds, st)
-                                          : launch_k(dense_lds_kernel<NG, true, SIG, 0>, k, B, T, lds, st);
+    return a.ipl_dense   ? launch_k(dense_lds_kernel<NG, true, SIG, 2>, k, B, T, lds, st)
+           : a.ipl_radix ? launch_k(dense_lds_kernel<NG, true, SIG, 1>, k, B, T, lds, st)
+                         : launch_k(dense_lds_kernel<NG, true, SIG, 0>, k, B, T, lds, st);
   return a.ipl_dense   ? launch_k(dense_lds_kernel<NG, false, SIG, 2>, k, B, T, lds, st)
          : a.ipl_radix ? launch_k(dense_lds_kernel<NG, false, SIG, 1>, k, B, T, lds, st)
                        : launch_k(dense_lds_kernel<NG, false, SIG, 0>, k, B, T, lds, st);
@@ -3179,7 +3171,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     if (a.tier1)
       snprintf(name, sizeof name, "dense_lds_kernel<%u, %s, %uu, %d>",
                variant >= 200 ? (variant == 202 ? 1u : 2u) : a.dense_ng, a.vec ? "true" : "false",
-               variant >= 200 ? a.sig : 0u, a.ipl_dense ? (a.vec && a.ipl_npfx == 1 ? 3 : 2) : a.ipl_radix ? 1 : 0);
+               variant >= 200 ? a.sig : 0u, a.ipl_dense ? 2 : a.ipl_radix ? 1 : 0);
     else if (a.dense_ng)
       snprintf(name, sizeof name, "dense_local_kernel<%u, %s, %s, %uu%s>", a.dense_ng, a.vec ? "true" : "false",
                a.dns_compact ? "true" : "false", variant >= 305 ? a.sig : 0u, variant == 306 ? ", true" : "");
