@@ -173,13 +173,66 @@ struct OptCopy {
   std::vector<std::string> src, dst;
 };
 
+struct LKey {
+  uint32_t w[8];  // view, prefix (direction / reason / flag / DNS payload), src ip / attrs / port, dst ...
+  bool operator==(const LKey &o) const { return memcmp(w, o.w, sizeof w) == 0; }
+};
+struct LKeyHash {
+  size_t operator()(const LKey &k) const {
+    uint64_t h = 0x8BADF00DULL;
+    for (int i = 0; i < 8; i += 2) h = fmix64(h ^ ((uint64_t)k.w[i] | ((uint64_t)k.w[i + 1] << 32)));
+    return (size_t)h;
+  }
+};
+struct LItem {
+  LKey k;
+  uint64_t cnt, byt;
+};
+
+// std::allocator whose resize leaves new elements default-initialized (no zero fill:
+// every element is written right after)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U> &) {}
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new ((void *)p) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new ((void *)p) U(std::forward<A>(a)...);
+  }
+};
+using SeriesVec = std::vector<SeriesRec, NoInitAlloc<SeriesRec>>;
+
+// The scrape's large buffers, kept mapped between snapshots: a result borrows them and
+// gpuagg_result_free hands them back, so the next scrape writes into pages that are
+// already faulted in (c4-remote's scrape touches ~3 GB per snapshot; on the GPU box the
+// page faults of fresh buffers were most of its host time).  Shared by the ctx and its
+// results, so a result may outlive its ctx.
+struct ScrapePool {
+  std::mutex mu;
+  std::vector<std::vector<char>> arenas;
+  std::vector<std::vector<uint32_t>> toks;
+  SeriesVec series;
+  std::unique_ptr<char[]> text;
+  size_t text_cap = 0;
+};
+
 }  // namespace
 
 struct gpuagg_result {
   std::vector<ResultFamily> fam;  // one per registered metric object
-  std::vector<SeriesRec> series;
+  SeriesVec series;
   std::vector<std::vector<char>> arenas;
   std::vector<std::vector<uint32_t>> toks;  // per arena: label sort tokens (render_series)
+  std::shared_ptr<ScrapePool> pool;         // where the buffers go back
   // series i's label values: value_ptrs[voff[i] ...], built on the first gpuagg_result_series
   // (the exposition text walks the arenas itself)
   mutable std::vector<const char *> value_ptrs;
@@ -190,8 +243,8 @@ struct gpuagg_result {
   // name -> exposition text block
   std::map<std::string, std::string> extra_text;
   // gpuagg_result_render_text's output, rendered once (callers size, then fill)
-  mutable std::unique_ptr<char[]> text;  // text_len bytes + NUL
-  mutable size_t text_len = 0;
+  mutable std::unique_ptr<char[]> text;  // text_len bytes + NUL, text_cap allocated
+  mutable size_t text_len = 0, text_cap = 0;
   mutable bool text_done = false;
 };
 
@@ -247,6 +300,13 @@ struct gpuagg_ctx {
   std::vector<uint64_t> dns_req_boff{0}, dns_resp_boff{0};
   // canonical slot attributes per option mask (snapshot), valid for slots_version
   std::map<uint8_t, SlotCanon> slot_canon;
+  // the scrape's buffers, reused between snapshots (results borrow the large ones)
+  std::shared_ptr<ScrapePool> scrape_pool = std::make_shared<ScrapePool>();
+  struct AggScratch {
+    std::vector<std::vector<std::vector<LItem>>> parts;
+    std::vector<std::vector<LItem>> tab;
+    std::vector<SeriesVec> out;
+  } agg_scratch;
   uint64_t slots_version = 0;
 
   // IP table
@@ -2724,22 +2784,6 @@ namespace {
 // pod attributes and DNS payloads are canonicalised by their strings -- so equal tuples are
 // summed in hash maps on integers (partitioned over host threads) and each distinct series
 // is rendered to strings once, into per-partition arenas.
-struct LKey {
-  uint32_t w[8];  // view, prefix (direction / reason / flag / DNS payload), src ip / attrs / port, dst ...
-  bool operator==(const LKey &o) const { return memcmp(w, o.w, sizeof w) == 0; }
-};
-struct LKeyHash {
-  size_t operator()(const LKey &k) const {
-    uint64_t h = 0x8BADF00DULL;
-    for (int i = 0; i < 8; i += 2) h = fmix64(h ^ ((uint64_t)k.w[i] | ((uint64_t)k.w[i + 1] << 32)));
-    return (size_t)h;
-  }
-};
-struct LItem {
-  LKey k;
-  uint64_t cnt, byt;
-};
-
 void append_str(std::vector<char> &a, const char *s, size_t n) {
   const size_t o = a.size();
   a.resize(o + n + 1);
@@ -3077,7 +3121,13 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t work = nent + (size_t)c->dense_len;
   const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)16, (size_t)hw, work / 65536 + 1}));
-  std::vector<std::vector<std::vector<LItem>>> parts(T, std::vector<std::vector<LItem>>(T));
+  // (the ctx's scratch: kept between snapshots, so its pages stay faulted in)
+  auto &parts = c->agg_scratch.parts;
+  if (parts.size() < T) parts.resize(T);
+  for (unsigned t = 0; t < T; ++t) {
+    if (parts[t].size() < T) parts[t].resize(T);
+    for (unsigned q = 0; q < T; ++q) parts[t][q].clear();
+  }
   std::vector<int> err(T, GPUAGG_OK);
   auto run = [&](auto &&fn) {  // fn(t) on T threads
     if (T == 1) {
@@ -3163,17 +3213,40 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     if (e) return fail(c, e, "snapshot: a group-by key names a dns_id that was not interned");
   // per partition: sum equal keys, then render each distinct key's series into the
   // partition's arena
-  std::vector<std::vector<SeriesRec>> out(T);
-  r->arenas.resize(T);
-  r->toks.resize(T);
+  auto &out = c->agg_scratch.out;
+  auto &tabs = c->agg_scratch.tab;
+  if (out.size() < T) out.resize(T);
+  if (tabs.size() < T) tabs.resize(T);
+  for (unsigned p = 0; p < T; ++p) out[p].clear();
+  r->pool = c->scrape_pool;
+  {  // the pool's arenas / token lists (capacity kept), fresh ones past them
+    std::lock_guard<std::mutex> lk(r->pool->mu);
+    r->arenas.resize(T);
+    r->toks.resize(T);
+    for (unsigned p = 0; p < T; ++p) {
+      if (!r->pool->arenas.empty()) {
+        r->arenas[p].swap(r->pool->arenas.back());
+        r->pool->arenas.pop_back();
+      }
+      if (!r->pool->toks.empty()) {
+        r->toks[p].swap(r->pool->toks.back());
+        r->pool->toks.pop_back();
+      }
+      r->arenas[p].clear();
+      r->toks[p].clear();
+    }
+    r->series.swap(r->pool->series);
+    r->series.clear();
+  }
   run([&](unsigned p) {
     size_t total = 0;
     for (unsigned t = 0; t < T; ++t) total += parts[t][p].size();
     // open addressing (linear probing, at most half full); w[0] (the view) is never ~0
     size_t cap = 16;
     while (cap < 2 * total) cap <<= 1;
-    std::vector<LItem> tab(cap);
-    for (LItem &e : tab) e.k.w[0] = ~0u;
+    std::vector<LItem> &tab = tabs[p];
+    if (tab.size() < cap) tab.resize(cap);
+    for (size_t i = 0; i < cap; ++i) tab[i].k.w[0] = ~0u;
     size_t NM = 0;
     for (unsigned t = 0; t < T; ++t) {
       for (const LItem &it : parts[t][p]) {
@@ -3188,7 +3261,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
           e.byt += it.byt;
         }
       }
-      std::vector<LItem>().swap(parts[t][p]);
+      parts[t][p].clear();
     }
     std::vector<char> &ar = r->arenas[p];
     std::vector<uint32_t> &tk = r->toks[p];
@@ -3196,7 +3269,8 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     ar.reserve(NM * 320);
     tk.reserve(NM * 16);
     out[p].reserve(NM * 2);
-    for (const LItem &kv : tab) {
+    for (size_t ti = 0; ti < cap; ++ti) {  // (the reused table may be longer than cap)
+      const LItem &kv = tab[ti];
       if (kv.k.w[0] == ~0u) continue;
       const LKey &k = kv.k;
       const View &v = views[k.w[0]];
@@ -3261,7 +3335,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   r->series.resize(sbase[T]);
   run([&](unsigned p) {
     std::copy(out[p].begin(), out[p].end(), r->series.begin() + sbase[p]);
-    std::vector<SeriesRec>().swap(out[p]);
+    out[p].clear();
   });
   return GPUAGG_OK;
 }
@@ -3707,7 +3781,18 @@ void render_text(const gpuagg_result *r) {
     j.base = N;
     N += j.size;
   }
-  r->text.reset(new char[N + 1]);  // (not zeroed: every byte is written below, page faults spread over the threads)
+  if (r->text_cap < N + 1 && r->pool) {  // the pool's buffer when it is large enough
+    std::lock_guard<std::mutex> lk(r->pool->mu);
+    if (r->pool->text_cap >= N + 1) {
+      r->text = std::move(r->pool->text);
+      r->text_cap = r->pool->text_cap;
+      r->pool->text_cap = 0;
+    }
+  }
+  if (r->text_cap < N + 1) {  // (not zeroed: every byte is written below, page faults spread over the threads)
+    r->text.reset(new char[N + 1]);
+    r->text_cap = N + 1;
+  }
   r->text_len = N;
   char *out = r->text.get();
   out[N] = '\0';
@@ -3795,7 +3880,23 @@ int gpuagg_result_series(const gpuagg_result *r, size_t i, const char **metric, 
   return GPUAGG_OK;
 }
 
-void gpuagg_result_free(gpuagg_result *r) { delete r; }
+void gpuagg_result_free(gpuagg_result *r) {
+  if (!r) return;
+  if (r->pool) {  // the large buffers back to the ctx's pool (kept: at most a few sets)
+    std::lock_guard<std::mutex> lk(r->pool->mu);
+    ScrapePool &p = *r->pool;
+    if (p.arenas.size() < 64)
+      for (auto &a : r->arenas) p.arenas.push_back(std::move(a));
+    if (p.toks.size() < 64)
+      for (auto &t : r->toks) p.toks.push_back(std::move(t));
+    if (r->series.capacity() > p.series.capacity()) p.series.swap(r->series);
+    if (r->text_cap > p.text_cap) {
+      p.text = std::move(r->text);
+      p.text_cap = r->text_cap;
+    }
+  }
+  delete r;
+}
 
 // ---- sketches ---------------------------------------------------------------------
 int gpuagg_sketch_refresh(gpuagg_ctx *c) {

@@ -341,3 +341,41 @@ def test_exposition_order_across_growth_and_churn():
         assert g.snapshot_text() == X.render(series)
     finally:
         g.close()
+
+
+def test_scrape_buffers_reused_across_results():
+    """The scrape's buffers go back to the context's pool when a result is freed and the
+    next snapshot reuses them: results held at the same time, freed in either order and
+    re-taken, all render the same text, and a result outliving its context stays valid."""
+    import ctypes as C
+    from oracle import exposition as X
+    pods = W.make_pods(300, seed=41)
+    recs = W.gen_records(30_000, pods, seed=42, **MIX)
+    sp = spec(["forward_count", "forward_bytes", "drop_count"], ["ip", "podname"], ["namespace", "port"])
+    g = make_engine(pods, sp, True, recs=recs, flags=CPU)
+
+    def snap():
+        r = C.c_void_p()
+        assert g.lib.gpuagg_snapshot(g.h, C.byref(r)) == 0
+        return r
+
+    def text(r):
+        p, n = C.c_void_p(), C.c_size_t()
+        assert g.lib.gpuagg_result_text(r, C.byref(p), C.byref(n)) == 0
+        return C.string_at(p.value, n.value)
+
+    try:
+        g.submit_numpy(recs)
+        want = X.render(g.snapshot()).encode()
+        a, b = snap(), snap()  # two alive: the second takes fresh buffers
+        assert text(a) == want and text(b) == want
+        g.lib.gpuagg_result_free(a)
+        c = snap()  # reuses a's buffers
+        assert text(c) == want
+        g.lib.gpuagg_result_free(c)
+        g.lib.gpuagg_result_free(b)
+        d = snap()
+    finally:
+        g.close()
+    assert text(d) == want  # the context is gone; the result's buffers are its own
+    g.lib.gpuagg_result_free(d)
