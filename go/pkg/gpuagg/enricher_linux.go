@@ -24,8 +24,7 @@ package gpuagg
 
 import (
 	"context"
-	"encoding/binary"
-	"net"
+	"runtime"
 	"strconv"
 	"strings"
 	"sync"
@@ -43,40 +42,64 @@ import (
 // flows converted per WriteBatch slice
 const enricherSlice = 4096
 
+// conversion workers at most (GOMAXPROCS below that)
+const enricherMaxWorkers = 16
+
 // Enricher implements enricher.EnricherInterface over the plugin.
+//
+// The reference enriches on one goroutine (enricher.go:68-99).  Here the per-flow cost is
+// the conversion back to a record -- one Any UnmarshalTo of the RetinaMetadata extension,
+// two IPv4 parses (ipv4LE: no allocation on dotted quads), the field reads -- so it runs on
+// GOMAXPROCS workers (at most enricherMaxWorkers).  Write picks a flow's worker by a hash
+// of its direction-free (ip, port) ends and protocol, so a connection's request and reply
+// keep their order through one worker (the node-apiserver latency join pairs a request
+// with the reply after it); each worker fills its own []Record slice and hands it over
+// with one WriteBatch per enricherSlice flows or flushInterval.
 type Enricher struct {
 	ctx context.Context
 	g   *gpuAgg
 	l   *log.ZapLogger
 
-	in  chan *v1.Event
+	in  []chan *v1.Event // one input channel per conversion worker
 	out *container.Ring
 	// enriched flows from the engine (the plugin's SetupChannel consumer)
 	enriched chan *v1.Event
 
-	dnsMu  sync.Mutex
+	dnsMu  sync.RWMutex
 	dnsIDs map[string]uint32 // AddDNSInfo payload -> dns_id (gpuagg_dns_intern), cached
 	once   sync.Once
 }
 
 // NewEnricher returns the engine-backed enricher; g is the registered plugin (Instance()).
 func NewEnricher(ctx context.Context, g *gpuAgg) *Enricher {
+	w := runtime.GOMAXPROCS(0)
+	if w > enricherMaxWorkers {
+		w = enricherMaxWorkers
+	}
+	if w < 1 {
+		w = 1
+	}
 	e := &Enricher{
 		ctx: ctx, g: g, l: log.Logger().Named("gpuagg-enricher"),
-		in: make(chan *v1.Event, channelDepth), out: container.NewRing(container.Capacity1023),
+		in: make([]chan *v1.Event, w), out: container.NewRing(container.Capacity1023),
 		enriched: make(chan *v1.Event, channelDepth), dnsIDs: map[string]uint32{},
+	}
+	for i := range e.in {
+		e.in[i] = make(chan *v1.Event, channelDepth)
 	}
 	return e
 }
 
-// Run starts the conversion loop and the export loop (enricher.go:69-98 starts one
+// Run starts the conversion workers and the export loop (enricher.go:69-98 starts one
 // goroutine reading the input ring).
 func (e *Enricher) Run() {
 	e.once.Do(func() {
 		if err := e.g.SetupChannel(e.enriched); err != nil {
 			e.l.Error("gpuagg enricher: SetupChannel failed; no enriched flows will be exported", zap.Error(err))
 		}
-		go e.convert()
+		for i := range e.in {
+			go e.convert(e.in[i])
+		}
 		go e.export()
 	})
 }
@@ -84,11 +107,46 @@ func (e *Enricher) Run() {
 // Write never blocks the producer: a full input channel drops the flow and counts it, as
 // the reference's ring overwrites its oldest entry (enricher.go:185-187).
 func (e *Enricher) Write(ev *v1.Event) {
+	w := 0
+	if len(e.in) > 1 {
+		w = int(flowKey(ev) % uint64(len(e.in)))
+	}
 	select {
-	case e.in <- ev:
+	case e.in[w] <- ev:
 	default:
 		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, "gpuagg-enricher").Inc()
 	}
+}
+
+// flowKey is FNV-1a over a flow's direction-free 5-tuple as text: the two (ip, port)
+// ends in order, then the protocol.  It reads the strings in place (no parse, no
+// allocation); a non-flow event hashes to 0.
+func flowKey(ev *v1.Event) uint64 {
+	f, ok := ev.GetEvent().(*flow.Flow)
+	if !ok || f == nil {
+		return 0
+	}
+	a, b := f.GetIP().GetSource(), f.GetIP().GetDestination()
+	var pa, pb, proto uint32
+	if tcp := f.GetL4().GetTCP(); tcp != nil {
+		pa, pb, proto = tcp.GetSourcePort(), tcp.GetDestinationPort(), 6
+	} else if udp := f.GetL4().GetUDP(); udp != nil {
+		pa, pb, proto = udp.GetSourcePort(), udp.GetDestinationPort(), 17
+	}
+	if a > b || (a == b && pa > pb) {
+		a, b, pa, pb = b, a, pb, pa
+	}
+	const prime = 1099511628211
+	h := uint64(14695981039346656037)
+	for i := 0; i < len(a); i++ {
+		h = (h ^ uint64(a[i])) * prime
+	}
+	h = (h ^ uint64(pa) ^ 0x100000000) * prime
+	for i := 0; i < len(b); i++ {
+		h = (h ^ uint64(b[i])) * prime
+	}
+	h = (h ^ uint64(pb) ^ uint64(proto)<<16 ^ 0x200000000) * prime
+	return h
 }
 
 // ExportReader is enricher.go:189-191: a reader from the oldest write of the output ring.
@@ -96,7 +154,7 @@ func (e *Enricher) ExportReader() *container.RingReader {
 	return container.NewRingReader(e.out, e.out.OldestWrite())
 }
 
-func (e *Enricher) convert() {
+func (e *Enricher) convert(in chan *v1.Event) {
 	buf := make([]Record, 0, enricherSlice)
 	tick := time.NewTicker(flushInterval)
 	defer tick.Stop()
@@ -112,7 +170,7 @@ func (e *Enricher) convert() {
 		case <-e.ctx.Done():
 			flush()
 			return
-		case ev := <-e.in:
+		case ev := <-in:
 			f, ok := ev.GetEvent().(*flow.Flow)
 			if !ok || f == nil {
 				continue // enricher.go:86-96: only flows are enriched
@@ -203,9 +261,9 @@ func (e *Enricher) flowToRecord(f *flow.Flow) (Record, bool) {
 func (e *Enricher) dnsID(rcode uint32, qtypes []string, query string, ips []string, n uint32) (uint32, error) {
 	key := strings.Join([]string{query, strings.Join(qtypes, ","), strings.Join(ips, ","),
 		strconv.FormatUint(uint64(rcode), 10), strconv.FormatUint(uint64(n), 10)}, "\x00")
-	e.dnsMu.Lock()
+	e.dnsMu.RLock()
 	id, ok := e.dnsIDs[key]
-	e.dnsMu.Unlock()
+	e.dnsMu.RUnlock()
 	if ok {
 		return id, nil
 	}
@@ -217,21 +275,4 @@ func (e *Enricher) dnsID(rcode uint32, qtypes []string, query string, ips []stri
 	e.dnsIDs[key] = id
 	e.dnsMu.Unlock()
 	return id, nil
-}
-
-// ipv4LE is the inverse of utils.Int2ip (utils_linux.go:51-55): the u32 whose
-// little-endian bytes are the address.
-func ipv4LE(s string) (uint32, bool) {
-	ip := net.ParseIP(s).To4()
-	if ip == nil {
-		return 0, false
-	}
-	return binary.LittleEndian.Uint32(ip), true
-}
-
-func b2u(b bool) uint32 {
-	if b {
-		return 1
-	}
-	return 0
 }

@@ -31,6 +31,7 @@ import (
 	"errors"
 	"fmt"
 	"io"
+	"math/bits"
 	"net"
 	"strings"
 	"sync"
@@ -718,6 +719,14 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 				}
 				break
 			}
+			// single Write()s that arrived before this slice go first: the latency join
+			// pairs a request with the reply after it, so arrival order is kept
+			if len(g.recBuf) > 0 {
+				if err := putRecords(g.recBuf, false); err != nil {
+					g.l.Error("record submit failed", zap.Error(err))
+				}
+				g.recBuf = g.recBuf[:0]
+			}
 			if err := putRecords(rs, false); err != nil {
 				g.l.Error("record submit failed", zap.Error(err))
 			}
@@ -953,12 +962,114 @@ func (g *gpuAgg) commitLocked() error {
 	return g.each("gpuagg_cache_commit", func(ctx *C.gpuagg_ctx) C.int { return C.gpuagg_cache_commit(ctx, v) })
 }
 
-func ipv4LE(ip string) (uint32, bool) {
-	p := net.ParseIP(ip).To4()
+// ipv4LE is net.ParseIP(s).To4() read little-endian -- the record encoding
+// (include/gpuagg.h), the inverse of utils.Int2ip (utils_linux.go:51-55) -- without the
+// allocation on the common form: a dotted quad of 1-3 digit decimal octets <= 255 with no
+// leading zeros (net.ParseIP rejects those since Go 1.17).  Anything else (IPv4-mapped
+// IPv6 text, malformed input) takes net.ParseIP itself, so the result is always exactly
+// net.ParseIP's (tests/test_enricher_inverse.py checks a transcription of both paths).
+func ipv4LE(s string) (uint32, bool) {
+	var v, oct, digits uint32
+	dots := uint32(0)
+	for i := 0; i < len(s); i++ {
+		c := s[i]
+		switch {
+		case c >= '0' && c <= '9':
+			if digits > 0 && oct == 0 { // a leading zero
+				return ipv4LESlow(s)
+			}
+			oct = oct*10 + uint32(c-'0')
+			digits++
+			if digits > 3 || oct > 255 {
+				return ipv4LESlow(s)
+			}
+		case c == '.':
+			if digits == 0 || dots == 3 {
+				return ipv4LESlow(s)
+			}
+			v |= oct << (8 * dots)
+			dots++
+			oct, digits = 0, 0
+		default:
+			return ipv4LESlow(s)
+		}
+	}
+	if dots != 3 || digits == 0 {
+		return ipv4LESlow(s)
+	}
+	return v | oct<<24, true
+}
+
+func ipv4LESlow(s string) (uint32, bool) {
+	p := net.ParseIP(s).To4()
 	if p == nil {
 		return 0, false
 	}
-	return binary.LittleEndian.Uint32(p), true // the record encoding (include/gpuagg.h)
+	return binary.LittleEndian.Uint32(p), true
+}
+
+func b2u(b bool) uint32 {
+	if b {
+		return 1
+	}
+	return 0
+}
+
+// PacketRecord is the record of one packetparser event -- the fields of
+// packetparserPacket (packetparser_bpfel_x86.go:45-70) as processRecord turns them into a
+// flow (packetparser_linux.go:571-631: ToFlow with FORWARDED, HostToNetShort ports,
+// ktime.MonotonicOffset added to T_nsec, IsReply, TrafficDirection, TCP flags, TCP id) --
+// with exactly the columns packet_decode_kernel produces from the raw sample
+// (gpuagg_decode.hip).  Producers that decode themselves call
+// gpuAgg.Write(gpuagg.PacketRecord(...)) instead of building a *flow.Flow.
+func PacketRecord(tNsec uint64, bytes, srcIP, dstIP uint32, srcPort, dstPort uint16, tsval, tsecr uint32,
+	obsPoint, trafficDirection, proto, flags uint8, isReply bool) Record {
+	verdict := uint32(flow.Verdict_FORWARDED)
+	if trafficDirection > 3 { // not encodable in the meta word: no metric consumes the row
+		verdict = 255
+	}
+	tcpFlags := uint32(0)
+	if proto == 6 {
+		tcpFlags = uint32(flags) & 0x3f
+	}
+	obs := uint32(obsPoint)
+	if obs > 3 {
+		obs = 0
+	}
+	r := Record{
+		SrcIP: srcIP, DstIP: dstIP, Bytes: bytes,
+		Meta: uint32(proto) | verdict<<8 | uint32(trafficDirection&3)<<16 | tcpFlags<<21 | b2u(isReply)<<27 |
+			obs<<30,
+		Ports:  uint32(bits.ReverseBytes16(srcPort)) | uint32(bits.ReverseBytes16(dstPort))<<16,
+		DNSID:  0xffffffff,
+		TimeNs: uint64(ktime.MonotonicOffset.Nanoseconds() + int64(tNsec)),
+	}
+	switch obsPoint { // TO_NETWORK carries the request's TSval, FROM_NETWORK the reply's TSecr
+	case 3:
+		r.TcpID = tsval
+	case 2:
+		r.TcpID = tsecr
+	}
+	return r
+}
+
+// DropRecord is the record of one dropreason event (dropreason's kernel struct,
+// drop_reason.c:39-54, as processRecord builds its flow, dropreason_linux.go:345-386:
+// DROPPED, observation point FROM_NETWORK = INGRESS, DropReason = dropType, Bytes =
+// skbLen), the columns drop_decode_kernel produces.
+func DropRecord(tNsec uint64, srcIP, dstIP uint32, srcPort, dstPort uint16, skbLen uint32, dropType uint16,
+	proto uint8) Record {
+	verdict := uint32(flow.Verdict_DROPPED)
+	if dropType > 7 {
+		verdict = 255
+	}
+	return Record{
+		SrcIP: srcIP, DstIP: dstIP, Bytes: skbLen,
+		Meta:   uint32(proto) | verdict<<8 | 1<<16 | uint32(dropType&7)<<18 | 2<<30,
+		Ports:  uint32(bits.ReverseBytes16(srcPort)) | uint32(bits.ReverseBytes16(dstPort))<<16,
+		DNSID:  0xffffffff,
+		TimeNs: uint64(ktime.MonotonicOffset.Nanoseconds() + int64(tNsec)),
+	}
 }
 
 // CacheTee is a cache.CacheInterface that forwards to the agent's cache and mirrors

@@ -88,3 +88,118 @@ def test_adapter_drops_what_enrich_drops():
     f = O.to_flow("10.0.0.1", "10.0.0.2", 1, 2, 6, 3, 1)
     f.ip.destination = ""  # enricher.go:121-124
     assert go_flow_to_record(f, None) is None
+
+
+# ---- go/pkg/gpuagg/gpuagg_linux.go helpers, transcribed ------------------------------
+
+def go_ipv4_le(s: str):
+    """gpuagg_linux.go ipv4LE, line for line: the allocation-free dotted-quad path, else
+    ('slow', s) -- the net.ParseIP fallback."""
+    v = oct_ = digits = dots = 0
+    for ch in s:
+        if "0" <= ch <= "9":
+            if digits > 0 and oct_ == 0:
+                return ("slow", s)
+            oct_ = oct_ * 10 + (ord(ch) - 48)
+            digits += 1
+            if digits > 3 or oct_ > 255:
+                return ("slow", s)
+        elif ch == ".":
+            if digits == 0 or dots == 3:
+                return ("slow", s)
+            v |= oct_ << (8 * dots)
+            dots += 1
+            oct_ = digits = 0
+        else:
+            return ("slow", s)
+    if dots != 3 or digits == 0:
+        return ("slow", s)
+    return v | oct_ << 24
+
+
+def _parse_ip_to4(s: str):
+    """net.ParseIP(s).To4() read little-endian (Go >= 1.17: IPv4 octets with leading zeros
+    rejected; IPv4-mapped IPv6 text gives its IPv4).  Python's ipaddress has the same
+    IPv4 rules (3.9.5+)."""
+    import ipaddress
+    try:
+        a = ipaddress.ip_address(s)
+    except ValueError:
+        return None
+    if a.version == 6:
+        a = a.ipv4_mapped
+        if a is None:
+            return None
+    return int.from_bytes(a.packed, "little")
+
+
+def test_ipv4le_fast_path_is_parseip():
+    import random
+    rng = random.Random(7)
+    cases = ["0.0.0.0", "255.255.255.255", "10.0.0.1", "1.2.3.4", "01.2.3.4", "1.2.3.04", "1.2.3", "1.2.3.4.5",
+             "256.1.1.1", "1..2.3", ".1.2.3", "1.2.3.", "", "a.b.c.d", "1.2.3.4 ", "::ffff:10.1.2.3", "::1",
+             "1000.1.1.1", "00.0.0.0", "0.00.0.0", "192.168.001.1", "-1.2.3.4", "1.2.3.+4"]
+    for _ in range(3000):
+        parts = [str(rng.choice([rng.randrange(256), rng.randrange(1000), 0])) for _ in range(rng.choice([3, 4, 4, 5]))]
+        if rng.random() < 0.1:
+            i = rng.randrange(len(parts))
+            parts[i] = "0" + parts[i]
+        cases.append(".".join(parts))
+    fast = 0
+    for s in cases:
+        want = _parse_ip_to4(s)
+        got = go_ipv4_le(s)
+        if isinstance(got, tuple):
+            got = _parse_ip_to4(got[1])  # the fallback is net.ParseIP itself
+        else:
+            fast += 1
+            assert want is not None, s  # the fast path never accepts what ParseIP rejects
+        assert got == want, s
+        if want is not None and ":" not in s:
+            assert not isinstance(go_ipv4_le(s), tuple), s  # every dotted quad takes the fast path
+    assert fast > 300
+
+
+def go_packet_record(r):
+    """gpuagg_linux.go PacketRecord on the fields of one struct packet (time offset 0)."""
+    swap = lambda x: ((x & 0xFF) << 8) | (x >> 8)  # bits.ReverseBytes16
+    verdict = 255 if r["tdir"] > 3 else 1
+    tcp_flags = int(r["flags"]) & 0x3F if r["proto"] == 6 else 0
+    obs = int(r["obs"]) if r["obs"] <= 3 else 0
+    meta = (int(r["proto"]) | verdict << 8 | (int(r["tdir"]) & 3) << 16 | tcp_flags << 21 |
+            int(bool(r["is_reply"])) << 27 | obs << 30)
+    tcp_id = int(r["tsval"]) if r["obs"] == 3 else int(r["tsecr"]) if r["obs"] == 2 else 0
+    return (int(r["src_ip"]), int(r["dst_ip"]), int(r["bytes"]), meta,
+            swap(int(r["src_port"])) | swap(int(r["dst_port"])) << 16, 0xFFFFFFFF, tcp_id, int(r["t_nsec"]))
+
+
+def go_drop_record(r):
+    """gpuagg_linux.go DropRecord on the fields of one dropreason struct packet."""
+    swap = lambda x: ((x & 0xFF) << 8) | (x >> 8)
+    verdict = 255 if r["drop_type"] > 7 else 2
+    meta = int(r["proto"]) | verdict << 8 | 1 << 16 | (int(r["drop_type"]) & 7) << 18 | 2 << 30
+    return (int(r["src_ip"]), int(r["dst_ip"]), int(r["skb_len"]), meta,
+            swap(int(r["src_port"])) | swap(int(r["dst_port"])) << 16, 0xFFFFFFFF, 0, int(r["ts"]))
+
+
+@pytest.mark.parametrize("kind", ["packet", "drop"])
+def test_record_constructors_equal_the_decode(kind):
+    """PacketRecord / DropRecord (the INTEGRATION.md producer snippets) give the columns the
+    raw decode gives (oracle/decode.py, pinned to the per-record oracle)."""
+    import numpy as np
+    from oracle import decode as D
+    pods = W.make_pods(100, seed=3)
+    if kind == "packet":
+        raw = W.gen_raw_packets(3000, pods, seed=11, odd_frac=0.3, out_of_range_frac=0.05)
+        batch, _ = D.decode_packets(raw)
+        rows = np.frombuffer(raw.tobytes(), D.PACKET_DTYPE)
+        conv = go_packet_record
+    else:
+        raw = W.gen_raw_drops(3000, pods, seed=12, out_of_range_frac=0.05)
+        batch, _ = D.decode_drops(raw)
+        rows = np.frombuffer(raw.tobytes(), D.DROP_DTYPE)
+        conv = go_drop_record
+    cols = [batch.src_ip, batch.dst_ip, batch.bytes, batch.meta, batch.ports, batch.dns_id, batch.tcp_id,
+            batch.time_ns]
+    for i in range(len(rows)):
+        assert conv(rows[i]) == tuple(int(c[i]) for c in cols), i
