@@ -208,45 +208,75 @@ def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
             "note": "pinned host batches through gpuagg_submit (PCIe H2D included; not `value`)"}
 
 
-def host_fed_raw_rate(g, pods, seed: int, batches: int = 16, batch: int = GO_BATCH):
+def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 48, batch: int = GO_BATCH):
     """The Go plugin's raw path (gpuagg_linux.go Start -> submitRaw): raw 72-byte
     packetparser samples (conntrack.c:34-49) handed to the library feed in 2^16-sample
-    pieces (gpuagg_raw_feed_put: shard by the 5-tuple, copy into the device's pinned
-    staging, submit each full 2^20-record staging -- H2D DMA, on-GPU decode, aggregation),
-    then a flush and sync.  Also the host-side sharding rate over 8 devices
-    (gpuagg_shard_raw), the per-sample cost the plugin pays before any copy."""
-    from retina_amd import RawFeed, _abi
+    pieces (rawPiece) -- gpuagg_raw_feed_put: the feed's host threads shard by the 5-tuple
+    and write into one of the device's two pinned 2^20-record stagings; a full staging's
+    H2D DMA starts without a wait while the other fills -- then a flush and sync.
+    `value`: the feed's defaults -- samples copied as they are (72 B per record over PCIe)
+    and decoded on the GPU (GPUAGG_FEED_RAW_DMA), 4 feed threads; `modes` times both modes
+    (GPUAGG_FEED_HOST_DECODE: decoded on the feed's threads, only the columns the metrics
+    read cross PCIe) at 1-16 feed threads, and
+    `shard8`: the same feed over 8 contexts of this one GPU (the 8-device node's shard +
+    scatter path; the 8 stagings share this GPU and its PCIe link).  `shard_rate_8_devices`
+    times gpuagg_shard_raw alone (its host threads)."""
+    from retina_amd import GpuAgg, RawFeed, _abi
     from retina_amd import workloads as W
     raw = W.gen_raw_packets(batch, pods, seed=seed)  # one Go batch of samples, resubmitted
     piece = 1 << 16
-    feed = RawFeed([g], _abi.RAW_PACKET, capacity=batch)
-    try:
-        for a in range(0, batch, piece):  # warm-up: staging and device buffers
-            feed.put(raw[a * 72:(a + piece) * 72])
-        feed.flush()
-        g.sync()
-        t0 = time.perf_counter()
-        for _ in range(batches):
-            for a in range(0, batch, piece):
+
+    def run(engines, mode, threads, nb):
+        feed = RawFeed(engines, _abi.RAW_PACKET, capacity=batch, threads=threads, mode=mode)
+        try:
+            for a in range(0, batch, piece):  # warm-up: stagings, device buffers, pool threads
                 feed.put(raw[a * 72:(a + piece) * 72])
-        feed.flush()
-        g.sync()
-        dt = time.perf_counter() - t0
+            feed.flush()
+            for e in set(engines):
+                e.sync()
+            t0 = time.perf_counter()
+            for _ in range(nb):
+                for a in range(0, batch, piece):
+                    feed.put(raw[a * 72:(a + piece) * 72])
+            feed.flush()
+            for e in set(engines):
+                e.sync()
+            return nb * batch / (time.perf_counter() - t0)
+        finally:
+            feed.close()
+
+    modes = {}
+    for name, mode in (("host_decode", _abi.FEED_HOST_DECODE), ("raw_dma", _abi.FEED_RAW_DMA)):
+        modes[name] = {str(t): run([g], mode, t, batches) for t in (1, 2, 4, 8, 16)}
+    best = max(((m, t) for m in modes for t in modes[m]), key=lambda mt: modes[mt[0]][mt[1]])
+    # 8 contexts on this GPU, the plan of `g` (the shard + scatter path of an 8-GPU node)
+    extra = [GpuAgg(device=g.device, remote_context=False, max_slots=len(pods.endpoints) + 16,
+                    max_ips=2 * len(pods.endpoints) + 16) for _ in range(7)]
+    try:
+        for e in extra:
+            e.reconcile(spec)
+            e.load_endpoints(pods.endpoints)
+        shard8 = {name: {str(t): run([g] + extra, mode, t, batches // 2) for t in (4, 8, 16)}
+                  for name, mode in (("host_decode", _abi.FEED_HOST_DECODE), ("raw_dma", _abi.FEED_RAW_DMA))}
     finally:
-        feed.close()
+        for e in extra:
+            e.close()
     shards = np.zeros(batch, np.uint32)
     t1 = time.perf_counter()
-    for _ in range(4):
+    for _ in range(8):
         rc = g.lib.gpuagg_shard_raw(_abi.RAW_PACKET, raw.ctypes.data_as(C.c_void_p), batch, 8,
                                     shards.ctypes.data_as(_abi.u32p))
         if rc != 0:
             raise RuntimeError("gpuagg_shard_raw: %d" % rc)
-    shard_rate = 4 * batch / (time.perf_counter() - t1)
-    return {"value": batches * batch / dt, "unit": "records/s", "batch_records": batch, "batches": batches,
-            "piece_records": piece, "record_bytes": 72, "shard_rate_8_devices": shard_rate,
-            "note": "raw packetparser samples through gpuagg_raw_feed_put (pinned staging, H2D DMA, on-GPU "
-                    "decode + aggregation) -- the Go plugin's real raw path; PCIe included, not `value`; "
-                    "shard_rate_8_devices = gpuagg_shard_raw samples/s on one host thread"}
+    shard_rate = 8 * batch / (time.perf_counter() - t1)
+    return {"value": modes["raw_dma"]["4"], "unit": "records/s", "batch_records": batch, "batches": batches,
+            "piece_records": piece, "record_bytes": 72, "feed_threads": 4, "feed_mode": "raw_dma", "modes": modes,
+            "best": {"mode": best[0], "threads": int(best[1]), "value": modes[best[0]][best[1]]},
+            "shard8": shard8, "shard_rate_8_devices": shard_rate,
+            "note": "raw packetparser samples through gpuagg_raw_feed_put in 2^16-sample pieces, 2 pinned 2^20-record "
+                    "stagings per context, async H2D -- the Go plugin's real raw path; PCIe included, not `value`. "
+                    "value = the feed's defaults (raw_dma, 4 threads); modes = records/s by mode and feed threads; shard8 = "
+                    "one feed over 8 contexts of this GPU; shard_rate_8_devices = gpuagg_shard_raw (threaded) samples/s"}
 
 
 def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, launches: int = 100,
@@ -493,7 +523,7 @@ def main():
         result["production"] = production_geometry(g, cols, n, bpr, stats["kernel_ms"] / max(1, stats["kernel_launches"]))
     if rank == 0 and world == 1 and not args.no_host_fed:
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
-        result["host_fed_raw"] = host_fed_raw_rate(g, pods, cfg["seed"] + 17)
+        result["host_fed_raw"] = host_fed_raw_rate(g, pods, spec, cfg["seed"] + 17)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         go_s, tu_s = (400_000, 4_000_000) if args.config == "c5" else (args.cpu_sample // 8, args.cpu_sample)
         result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s,

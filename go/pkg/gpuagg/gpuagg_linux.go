@@ -60,12 +60,13 @@ import (
 const (
 	name          = "gpuagg"
 	batchCapacity = 1 << 20
-	rawPiece      = 1 << 16 // raw samples buffered in Go before each gpuagg_raw_feed_put
+	rawPiece      = 1 << 16 // samples / records buffered in Go before each hand-over to Start
 	flushInterval = 100 * time.Millisecond
 	scrapeEpoch   = 5 * time.Second
 	maxSlots      = 1 << 20 // hard cap; dense counters grow with the pods actually seen
 	sparseLog2    = 22
 	channelDepth  = 10000 // like packetparser's recordsChannel (types_linux.go:37-38)
+	pieceDepth    = 16    // full pieces of rawPiece waiting for Start (1M samples)
 )
 
 // Record is one decoded flow in the column layout of include/gpuagg.h. Producers
@@ -88,9 +89,18 @@ const (
 
 var rawSize = map[int]int{RawPacket: int(C.GPUAGG_RAW_PACKET_SIZE), RawDrop: int(C.GPUAGG_RAW_DROP_SIZE)}
 
+// rawPiece is up to rawPiece back-to-back samples of one kind, handed to Start at once.
 type rawSample struct {
 	kind int
 	b    []byte
+}
+
+// rawBatcher collects one kind's samples from the producers (WriteRaw): an append under a
+// mutex per sample, one channel operation per rawPiece samples (the reference pays a
+// channel operation per sample, packetparser_linux.go:643-651).
+type rawBatcher struct {
+	mu  sync.Mutex
+	buf []byte
 }
 
 // device is one engine context and its pinned batch.
@@ -110,10 +120,8 @@ type gpuAgg struct {
 	// guards the fields below.
 	mu       sync.Mutex
 	devs     []*device
-	rawBuf   map[int][]byte                // per kind: back-to-back raw records awaiting submit
 	feeds    map[int]*C.gpuagg_raw_feed    // per kind: shard + scatter into pinned per-device staging
 	recFeed  *C.gpuagg_raw_feed            // decoded records: shard + transpose into pinned SoA batches
-	recBuf   []Record                      // single Write()s awaiting the record feed
 	spec     *api.MetricsSpec
 	vecs     map[string]*prometheus.GaugeVec
 	ctrs     map[string]*prometheus.CounterVec
@@ -131,10 +139,15 @@ type gpuAgg struct {
 	enrichSrc []int32
 	enrichDst []int32
 
-	records chan Record
-	batches chan []Record // WriteBatch: one channel operation per slice of records
-	raw     chan rawSample
-	done    chan struct{} // closed when Start returns
+	// producer side: single Write()s collect in recIn (recMu also orders them against
+	// WriteBatch slices), raw samples in a batcher per kind; full pieces go to Start
+	recMu   sync.Mutex
+	recIn   []Record
+	batches chan []Record // record pieces and WriteBatch slices, in arrival order
+	rawIn   map[int]*rawBatcher
+	raw     chan rawSample // full raw pieces
+	rawFree chan []byte    // recycled piece buffers
+	done    chan struct{}  // closed when Start returns
 
 	// node-apiserver latency (latency.go): apiserver IP set from the pubsub topic, the
 	// histograms as a collector, no_response as a counter vec
@@ -205,8 +218,9 @@ func init() {
 
 // New is the registry.PluginFunc (registry.go:37).
 func New(cfg *kcfg.Config) registry.Plugin {
-	g := &gpuAgg{cfg: cfg, l: log.Logger().Named(name), records: make(chan Record, channelDepth),
-		raw: make(chan rawSample, channelDepth), rawBuf: map[int][]byte{},
+	g := &gpuAgg{cfg: cfg, l: log.Logger().Named(name),
+		raw: make(chan rawSample, pieceDepth), rawFree: make(chan []byte, pieceDepth),
+		rawIn:   map[int]*rawBatcher{RawPacket: {}, RawDrop: {}},
 		batches: make(chan []Record, channelDepth/64+1)}
 	instanceMu.Lock()
 	instance = g
@@ -514,23 +528,37 @@ func (g *gpuAgg) apiserverCallback(obj interface{}) {
 }
 
 // Write is what producers call per decoded record (Enricher.Write's replacement). It
-// never blocks the reader: a full channel drops the record and counts it, like
-// packetparser's readData (packetparser_linux.go:643-651,689-695).
+// never blocks the reader: records collect in recIn and go to Start rawPiece at a time; a
+// full channel drops the piece and counts it, like packetparser's readData
+// (packetparser_linux.go:643-651,689-695).
 func (g *gpuAgg) Write(r Record) {
-	select {
-	case g.records <- r:
-	default:
-		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Inc()
+	g.recMu.Lock()
+	g.recIn = append(g.recIn, r)
+	if len(g.recIn) >= rawPiece {
+		g.sendRecordsLocked(g.recIn)
+		g.recIn = nil
 	}
+	g.recMu.Unlock()
 }
 
 // WriteBatch hands over a slice of decoded records with one channel operation (a
 // producer draining several perf records per wake-up); the slice is owned by the plugin
-// afterwards.  A full channel drops the whole slice and counts every record.
+// afterwards.  Records of earlier Write()s go first (the latency join pairs a request
+// with the reply after it).  A full channel drops the whole slice and counts every record.
 func (g *gpuAgg) WriteBatch(rs []Record) {
 	if len(rs) == 0 {
 		return
 	}
+	g.recMu.Lock()
+	defer g.recMu.Unlock()
+	if len(g.recIn) > 0 {
+		g.sendRecordsLocked(g.recIn)
+		g.recIn = nil
+	}
+	g.sendRecordsLocked(rs)
+}
+
+func (g *gpuAgg) sendRecordsLocked(rs []Record) {
 	select {
 	case g.batches <- rs:
 	default:
@@ -539,17 +567,71 @@ func (g *gpuAgg) WriteBatch(rs []Record) {
 }
 
 // WriteRaw takes one perf RawSample of the given kind; a sample of the wrong size is
-// refused like binary.Read's size mismatch (dropreason_linux.go:347-352).
+// refused like binary.Read's size mismatch (dropreason_linux.go:347-352).  Samples are
+// appended to the kind's piece (one copy, under a mutex); every rawPiece samples the piece
+// goes to Start with one channel operation.
 func (g *gpuAgg) WriteRaw(kind int, sample []byte) error {
-	if sz, ok := rawSize[kind]; !ok || len(sample) != sz {
+	sz, ok := rawSize[kind]
+	if !ok || len(sample) != sz {
 		return fmt.Errorf("gpuagg: raw sample of %d bytes for kind %d", len(sample), kind)
 	}
-	select {
-	case g.raw <- rawSample{kind, sample}:
-	default:
-		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Inc()
+	b := g.rawIn[kind]
+	b.mu.Lock()
+	if b.buf == nil {
+		b.buf = g.rawBuffer()
 	}
+	b.buf = append(b.buf, sample...)
+	if len(b.buf) >= rawPiece*sz {
+		g.sendRaw(kind, b.buf)
+		b.buf = nil
+	}
+	b.mu.Unlock()
 	return nil
+}
+
+// sendRaw hands a piece to Start (non-blocking: a full channel drops it and counts its samples).
+func (g *gpuAgg) sendRaw(kind int, buf []byte) {
+	select {
+	case g.raw <- rawSample{kind, buf}:
+	default:
+		metrics.LostEventsCounter.WithLabelValues(utils.BufferedChannel, name).Add(float64(len(buf) / rawSize[kind]))
+		g.recycleRaw(buf)
+	}
+}
+
+func (g *gpuAgg) rawBuffer() []byte {
+	select {
+	case b := <-g.rawFree:
+		return b[:0]
+	default:
+		return make([]byte, 0, rawPiece*int(C.GPUAGG_RAW_PACKET_SIZE))
+	}
+}
+
+func (g *gpuAgg) recycleRaw(b []byte) {
+	select {
+	case g.rawFree <- b:
+	default: // enough spares
+	}
+}
+
+// flushProducers moves the partial pieces (records, each raw kind) to Start's channels,
+// behind everything already queued, so the flush that follows keeps arrival order.
+func (g *gpuAgg) flushProducers() {
+	g.recMu.Lock()
+	if len(g.recIn) > 0 {
+		g.sendRecordsLocked(g.recIn)
+		g.recIn = nil
+	}
+	g.recMu.Unlock()
+	for kind, b := range g.rawIn {
+		b.mu.Lock()
+		if len(b.buf) > 0 {
+			g.sendRaw(kind, b.buf)
+			b.buf = nil
+		}
+		b.mu.Unlock()
+	}
 }
 
 // shardOf is retina_amd/dist.py shard_of and the library's gpuagg_shard_columns (whose
@@ -619,68 +701,37 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 		d.n = 0
 		return err
 	}
-	// submitRaw hands the kind's buffered samples to its feed: the library shards them by
+	// putRaw hands one piece of a kind's samples to its feed: the library shards them by
 	// the 5-tuple at the records' fixed offsets (conntrack.c:34-49, drop_reason.c:39-54;
 	// the function of shardOf and dist.shard_of, so a flow's raw and decoded records meet
-	// on one device) and copies each into its device's pinned staging, submitting the
-	// stagings that fill; flush also submits the partial ones (flushInterval, Stop).
-	submitRaw := func(kind int, flush bool) error {
-		buf := g.rawBuf[kind]
+	// on one device) and copies each into its device's pinned staging, starting the DMA of
+	// the stagings that fill; the piece's buffer is recycled once the call returns.
+	putRaw := func(s rawSample) error {
+		defer g.recycleRaw(s.b)
 		g.mu.Lock()
 		defer g.mu.Unlock()
 		if err := g.commitLocked(); err != nil {
 			return err
 		}
-		f := g.feeds[kind]
-		if len(buf) > 0 {
-			n := len(buf) / rawSize[kind]
-			g.rawBuf[kind] = buf[:0]
-			if err := check(g.devs[0].ctx, C.gpuagg_raw_feed_put(f, unsafe.Pointer(&buf[0]), C.size_t(n)),
-				"gpuagg_raw_feed_put"); err != nil {
-				return err
-			}
+		if len(s.b) == 0 {
+			return nil
 		}
-		if flush {
-			return check(g.devs[0].ctx, C.gpuagg_raw_feed_flush(f), "gpuagg_raw_feed_flush")
-		}
-		return nil
+		return check(devs[0].ctx, C.gpuagg_raw_feed_put(g.feeds[s.kind], unsafe.Pointer(&s.b[0]),
+			C.size_t(len(s.b)/rawSize[s.kind])), "gpuagg_raw_feed_put")
 	}
 	// putRecords hands a slice of decoded records to the record feed (the enriched-flow
 	// path keeps the per-record batches: emitLocked rebuilds flows from them)
-	putRecords := func(rs []Record, flush bool) error {
+	putRecords := func(rs []Record) error {
 		g.mu.Lock()
 		defer g.mu.Unlock()
 		if err := g.commitLocked(); err != nil {
 			return err
 		}
-		if len(rs) > 0 {
-			if err := check(devs[0].ctx, C.gpuagg_raw_feed_put(g.recFeed, unsafe.Pointer(&rs[0]), C.size_t(len(rs))),
-				"gpuagg_raw_feed_put(records)"); err != nil {
-				return err
-			}
+		if len(rs) == 0 {
+			return nil
 		}
-		if flush {
-			return check(devs[0].ctx, C.gpuagg_raw_feed_flush(g.recFeed), "gpuagg_raw_feed_flush(records)")
-		}
-		return nil
-	}
-	submitAll := func() error {
-		var err error
-		for _, d := range devs {
-			if e := submit(d); e != nil && err == nil {
-				err = e
-			}
-		}
-		if e := putRecords(g.recBuf, true); e != nil && err == nil {
-			err = e
-		}
-		g.recBuf = g.recBuf[:0]
-		for kind := range rawSize {
-			if e := submitRaw(kind, true); e != nil && err == nil {
-				err = e
-			}
-		}
-		return err
+		return check(devs[0].ctx, C.gpuagg_raw_feed_put(g.recFeed, unsafe.Pointer(&rs[0]), C.size_t(len(rs))),
+			"gpuagg_raw_feed_put(records)")
 	}
 	// put copies one decoded record into its device's pinned batch (device by shardOf)
 	put := func(r *Record) {
@@ -696,49 +747,64 @@ func (g *gpuAgg) Start(ctx context.Context) error {
 			}
 		}
 	}
+	takeBatch := func(rs []Record) {
+		if g.external != nil {
+			for i := range rs {
+				put(&rs[i])
+			}
+			return
+		}
+		if err := putRecords(rs); err != nil {
+			g.l.Error("record submit failed", zap.Error(err))
+		}
+	}
+	takeRaw := func(s rawSample) {
+		if err := putRaw(s); err != nil {
+			g.l.Error("raw submit failed", zap.Error(err))
+		}
+	}
+	// submitAll: the producers' partial pieces join the queues, everything queued is
+	// handed over in arrival order, then every partial staging is submitted (flushInterval,
+	// the scrape epoch, Stop)
+	submitAll := func() error {
+		g.flushProducers()
+	drain:
+		for {
+			select {
+			case rs := <-g.batches:
+				takeBatch(rs)
+			case s := <-g.raw:
+				takeRaw(s)
+			default:
+				break drain
+			}
+		}
+		var err error
+		for _, d := range devs {
+			if e := submit(d); e != nil && err == nil {
+				err = e
+			}
+		}
+		g.mu.Lock()
+		defer g.mu.Unlock()
+		if e := check(devs[0].ctx, C.gpuagg_raw_feed_flush(g.recFeed), "gpuagg_raw_feed_flush(records)"); e != nil && err == nil {
+			err = e
+		}
+		for kind := range rawSize {
+			if e := check(devs[0].ctx, C.gpuagg_raw_feed_flush(g.feeds[kind]), "gpuagg_raw_feed_flush"); e != nil && err == nil {
+				err = e
+			}
+		}
+		return err
+	}
 	for {
 		select {
 		case <-ctx.Done():
 			return submitAll()
-		case r := <-g.records:
-			if g.external != nil {
-				put(&r)
-				break
-			}
-			g.recBuf = append(g.recBuf, r)
-			if len(g.recBuf) >= rawPiece {
-				if err := putRecords(g.recBuf, false); err != nil {
-					g.l.Error("record submit failed", zap.Error(err))
-				}
-				g.recBuf = g.recBuf[:0]
-			}
 		case rs := <-g.batches:
-			if g.external != nil {
-				for i := range rs {
-					put(&rs[i])
-				}
-				break
-			}
-			// single Write()s that arrived before this slice go first: the latency join
-			// pairs a request with the reply after it, so arrival order is kept
-			if len(g.recBuf) > 0 {
-				if err := putRecords(g.recBuf, false); err != nil {
-					g.l.Error("record submit failed", zap.Error(err))
-				}
-				g.recBuf = g.recBuf[:0]
-			}
-			if err := putRecords(rs, false); err != nil {
-				g.l.Error("record submit failed", zap.Error(err))
-			}
+			takeBatch(rs)
 		case s := <-g.raw:
-			g.rawBuf[s.kind] = append(g.rawBuf[s.kind], s.b...)
-			// hand over in pieces of 64k samples: the feed submits a device's staging
-			// whenever it holds batchCapacity records
-			if len(g.rawBuf[s.kind]) >= rawPiece*rawSize[s.kind] {
-				if err := submitRaw(s.kind, false); err != nil {
-					g.l.Error("raw submit failed", zap.Error(err))
-				}
-			}
+			takeRaw(s)
 		case <-flush.C:
 			if err := submitAll(); err != nil {
 				g.l.Error("submit failed", zap.Error(err))

@@ -285,18 +285,33 @@ typedef struct gpuagg_record {
 
 /* Node-wide raw ingestion (the Go plugin's raw path, gpuagg_linux.go Start/submitRaw):
  * one call shards a buffer of back-to-back raw samples over the node's contexts (one per
- * device; the gpuagg_shard_raw function) and copies each sample into its context's
- * pinned staging of `capacity` records; a full staging is submitted on the spot
- * (gpuagg_submit_raw from pinned memory: the H2D copy is a DMA, and the call returns once
- * it is done, so staging refills while the device decodes and aggregates).  Replaces
- * the per-record Go re-append into per-device slices and the pageable H2D copy of the
- * packetparser_linux.go:556-654 reader loop's batches.  _flush submits every partial
- * staging (the plugin's flushInterval tick and Stop); _submitted reports the records
- * handed to each context.  Not thread-safe: one feed per reader goroutine. */
+ * device; the gpuagg_shard_raw function) into each context's pinned staging of `capacity`
+ * records, in input order.  Replaces the packetparser_linux.go:556-654 reader loop's
+ * hand-over to its two decode goroutines (:669-696) and the per-record Go re-append.
+ *  - Two pinned stagings per context: a full one is submitted without waiting for its
+ *    H2D DMA (the call returns once the copy is enqueued) while the other fills; a
+ *    staging is refilled only after its own copy-done event.
+ *  - The work of a put is split over the feed's host threads (default 4 for one context,
+ *    16 for several, at most the cores): shard, then scatter at per-thread prefix
+ *    positions through cache-resident tiles.
+ *  - Raw kinds are copied as they are and decoded on the GPU (GPUAGG_FEED_RAW_DMA, the
+ *    default: one memcpy per sample on the host) or decoded on those threads into pinned
+ *    SoA columns (GPUAGG_FEED_HOST_DECODE: only the columns the metric plan reads cross
+ *    PCIe, 16 B per record for forward/drop instead of the 72-byte sample; rows counted in
+ *    gpuagg_stats.decoded / decode_out_of_range at put).  Both give the same columns.
+ * _flush submits every partial staging (the plugin's flushInterval tick and Stop);
+ * _submitted reports the records handed to each context.  Not thread-safe: one feed per
+ * reader goroutine.  gpuagg_destroy of a context detaches its feeds: their puts and
+ * flushes then return GPUAGG_ESTATE, and _destroy still releases them. */
 typedef struct gpuagg_raw_feed gpuagg_raw_feed;
+#define GPUAGG_FEED_HOST_DECODE 0
+#define GPUAGG_FEED_RAW_DMA 1
 /* kind: GPUAGG_RAW_PACKET / GPUAGG_RAW_DROP (perf samples) or GPUAGG_RECORD (gpuagg_record) */
 int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
                            gpuagg_raw_feed **out);
+/* threads: host threads per put (0: keep); mode: GPUAGG_FEED_* (raw kinds; ignored for
+ * GPUAGG_RECORD).  Only on an empty feed (after create or _flush), else GPUAGG_ESTATE. */
+int gpuagg_raw_feed_configure(gpuagg_raw_feed *feed, uint32_t threads, int mode);
 int gpuagg_raw_feed_put(gpuagg_raw_feed *feed, const void *raw, size_t n);
 int gpuagg_raw_feed_flush(gpuagg_raw_feed *feed);
 int gpuagg_raw_feed_submitted(const gpuagg_raw_feed *feed, uint64_t *per_ctx, size_t n_ctx);

@@ -89,6 +89,7 @@ class Stats(C.Structure):
 RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
 RECORD = 3  # GPUAGG_RECORD: decoded records, struct gpuagg_record (40 bytes)
 RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32, RECORD: 40}
+FEED_HOST_DECODE, FEED_RAW_DMA = 0, 1  # GPUAGG_FEED_* (gpuagg_raw_feed_configure)
 
 
 KERNEL_NAMES = {0: None, 1: "aggregate_kernel", 2: "dense_local_kernel", 3: "dense_lds_kernel", 4: "cpu"}
@@ -162,6 +163,7 @@ SIGNATURES = [
     ("gpuagg_submit_enrich", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     ("gpuagg_raw_feed_create", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, C.c_int, C.c_size_t,
                                          C.POINTER(C.c_void_p)]),
+    ("gpuagg_raw_feed_configure", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("gpuagg_raw_feed_put", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("gpuagg_raw_feed_flush", C.c_int, [C.c_void_p]),
     ("gpuagg_raw_feed_submitted", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t]),

@@ -322,45 +322,24 @@ void Engine::sketch(const SketchArgs &s) {
 
 // packet_decode_kernel / drop_decode_kernel of gpuagg_decode.hip.
 uint64_t Engine::decode(const DecodeArgs &a) {
-  auto bswap16 = [](uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); };
-  auto swap_ports = [&](uint32_t w) { return bswap16(w & 0xFFFFu) | (bswap16(w >> 16) << 16); };
   std::atomic<uint64_t> bad{0};
   const OutCols &o = a.out;
   parallel(threads_, a.n, [&](unsigned, size_t lo, size_t hi) {
     uint64_t nbad = 0;
     for (size_t i = lo; i < hi; ++i) {
-      if (a.kind == kRawPacket) {
-        uint32_t w[18];
-        memcpy(w, (const uint8_t *)a.raw + i * 72, 72);
-        const uint32_t obs = w[10] & 0xFFu, tdir = (w[10] >> 8) & 0xFFu, proto = (w[10] >> 16) & 0xFFu;
-        const uint32_t flags = w[10] >> 24, tcp_flags = proto == 6u ? (flags & 0x3Fu) : 0u;
-        const bool b = tdir > 3u;
-        nbad += b;
-        o.src_ip[i] = w[3];
-        o.dst_ip[i] = w[4];
-        o.bytes[i] = w[2];
-        o.meta[i] = proto | ((b ? kVerdictUnencodable : kVerdictForwarded) << 8) | ((tdir & 3u) << 16) |
-                    (tcp_flags << 21) | ((w[11] & 0xFFu) ? (1u << 27) : 0u) | ((obs <= 3u ? obs : 0u) << 30);
-        if (o.ports) o.ports[i] = swap_ports(w[5]);
-        if (o.dns_id) o.dns_id[i] = 0xFFFFFFFFu;
-        if (o.tcp_id) o.tcp_id[i] = obs == 3u ? w[8] : obs == 2u ? w[9] : 0u;
-        if (o.time_ns) o.time_ns[i] = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + a.time_offset;
-      } else {
-        uint32_t d[8];
-        memcpy(d, (const uint8_t *)a.raw + i * 32, 32);
-        const uint32_t drop_type = d[5] & 0xFFFFu, proto = (d[5] >> 16) & 0xFFu;
-        const bool b = drop_type > 7u;
-        nbad += b;
-        o.src_ip[i] = d[0];
-        o.dst_ip[i] = d[1];
-        o.bytes[i] = d[3];
-        o.meta[i] = proto | ((b ? kVerdictUnencodable : kVerdictDropped) << 8) | (1u << 16) | ((drop_type & 7u) << 18) |
-                    (2u << 30);
-        if (o.ports) o.ports[i] = swap_ports(d[2]);
-        if (o.dns_id) o.dns_id[i] = 0xFFFFFFFFu;
-        if (o.tcp_id) o.tcp_id[i] = 0u;
-        if (o.time_ns) o.time_ns[i] = ((uint64_t)d[6] | ((uint64_t)d[7] << 32)) + a.time_offset;
-      }
+      uint32_t w[18];
+      const bool pkt = a.kind == kRawPacket;
+      memcpy(w, (const uint8_t *)a.raw + i * (pkt ? 72 : 32), pkt ? 72 : 32);
+      const RawRow r = pkt ? decode_packet_words(w, a.time_offset) : decode_drop_words(w, a.time_offset);
+      nbad += r.bad;
+      o.src_ip[i] = r.src;
+      o.dst_ip[i] = r.dst;
+      o.bytes[i] = r.bytes;
+      o.meta[i] = r.meta;
+      if (o.ports) o.ports[i] = r.ports;
+      if (o.dns_id) o.dns_id[i] = 0xFFFFFFFFu;
+      if (o.tcp_id) o.tcp_id[i] = r.tcp_id;
+      if (o.time_ns) o.time_ns[i] = r.time_ns;
     }
     bad += nbad;
   });

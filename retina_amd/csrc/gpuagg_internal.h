@@ -40,6 +40,51 @@ constexpr uint32_t kVerdictForwarded = 1, kVerdictDropped = 2, kVerdictRetrans =
 // decoded raw row whose field does not fit the meta word: no metric consumes it
 constexpr uint32_t kVerdictUnencodable = 255;
 constexpr uint32_t kDnsQuery = 1, kDnsResponse = 2;
+
+// ---- host decode of one raw perf record ---------------------------------------------
+// The host restatement of packet_decode_kernel / drop_decode_kernel (gpuagg_decode.hip:
+// field offsets and meta packing documented there), shared by the CPU backend and the
+// host-decoding raw feed (gpuagg_feed.cpp).  `w` are the record's little-endian dwords.
+struct RawRow {
+  uint32_t src, dst, bytes, meta, ports, tcp_id;
+  uint64_t time_ns;
+  bool bad;  // a field that does not fit the meta word (verdict kVerdictUnencodable)
+};
+inline uint32_t raw_swap_ports(uint32_t w) {  // utils.HostToNetShort of both u16 halves
+  return ((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu) | ((w & 0xFF0000u) << 8) | ((w >> 8) & 0xFF0000u);
+}
+// struct packet of packetparser (72 B, conntrack.c:34-49; packetparser_linux.go:571-631)
+inline RawRow decode_packet_words(const uint32_t *w, uint64_t time_offset) {
+  const uint32_t obs = w[10] & 0xFFu, tdir = (w[10] >> 8) & 0xFFu, proto = (w[10] >> 16) & 0xFFu;
+  const uint32_t tcp_flags = proto == 6u ? ((w[10] >> 24) & 0x3Fu) : 0u;
+  RawRow r;
+  r.bad = tdir > 3u;
+  r.src = w[3];
+  r.dst = w[4];
+  r.bytes = w[2];
+  r.meta = proto | ((r.bad ? kVerdictUnencodable : kVerdictForwarded) << 8) | ((tdir & 3u) << 16) |
+           (tcp_flags << 21) | ((w[11] & 0xFFu) ? (1u << 27) : 0u) | ((obs <= 3u ? obs : 0u) << 30);
+  r.ports = raw_swap_ports(w[5]);
+  r.tcp_id = obs == 3u ? w[8] : obs == 2u ? w[9] : 0u;
+  r.time_ns = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + time_offset;
+  return r;
+}
+// struct packet of dropreason (32 B, drop_reason.c:39-54; dropreason_linux.go:345-386)
+inline RawRow decode_drop_words(const uint32_t *d, uint64_t time_offset) {
+  const uint32_t drop_type = d[5] & 0xFFFFu, proto = (d[5] >> 16) & 0xFFu;
+  RawRow r;
+  r.bad = drop_type > 7u;
+  r.src = d[0];
+  r.dst = d[1];
+  r.bytes = d[3];
+  r.meta = proto | ((r.bad ? kVerdictUnencodable : kVerdictDropped) << 8) | (1u << 16) | ((drop_type & 7u) << 18) |
+           (2u << 30);
+  r.ports = raw_swap_ports(d[2]);
+  r.tcp_id = 0u;
+  r.time_ns = ((uint64_t)d[6] | ((uint64_t)d[7] << 32)) + time_offset;
+  return r;
+}
+
 // kernel flag bits (pkg/plugin/packetparser/types_linux.go:22-31)
 constexpr uint32_t kFin = 1, kSyn = 2, kRst = 4, kPsh = 8, kAck = 16, kUrg = 32;
 
@@ -102,6 +147,16 @@ GA_HD uint64_t fmix64(uint64_t k) {
   k *= 0xc4ceb9fe1a85ec53ULL;
   k ^= k >> 33;
   return k;
+}
+
+// dist.shard_of (retina_amd/dist.py), the Go plugin's shardOf and the feeds: fmix64 of the
+// direction-free 5-tuple -- lo <= hi the two (ip << 16 | port) ends, so a request and its
+// reply meet on one device for the latency join -- mod n.
+GA_HD uint32_t shard_5tuple(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto, uint32_t n) {
+  const uint64_t a = ((uint64_t)src << 16) | (ports & 0xFFFFu), b = ((uint64_t)dst << 16) | (ports >> 16);
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  const uint64_t h = fmix64(lo ^ fmix64(hi ^ ((uint64_t)(proto & 0xFFu) << 48) ^ 0x1F2E3D4C5B6A7988ULL));
+  return (uint32_t)(h % n);
 }
 
 // IP table: open addressing, linear probing. Entry = ip | slot << 32 | apiserver << 53.

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "gpuagg_build_id.h"
+#include "gpuagg_feed.h"
 #include "gpuagg_internal.h"
 #include "ipl_build.h"
 #include "gpuagg_launch.h"
@@ -475,6 +476,9 @@ struct gpuagg_ctx {
   uint32_t *d_hll_counts2 = nullptr;
   size_t hll_counts2_alloc = 0;
   std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch pass start, end
+  // node-wide feeds over this context (gpuagg_feed.cpp): detached by gpuagg_destroy
+  std::vector<gpuagg_raw_feed *> feeds;
+  uint64_t host_decode_oor = 0;  // out-of-range rows the feeds decoded on the host
 };
 
 // ------------------------------------------------------------------------------------
@@ -667,13 +671,20 @@ int acquire_staging(gpuagg_ctx *c, gpuagg_ctx::Staging **out) {
 // for them, `launch_fn` enqueues the kernels, s is released behind them, and the call
 // returns once the copies (not the kernels) are complete, so the caller's host buffer
 // may be refilled while the aggregation runs.
+// With `host_done` (the feeds' async submits) that event is recorded behind the copies and
+// the call returns without waiting for them.
 template <class F>
-int run_staged(gpuagg_ctx *c, gpuagg_ctx::Staging &s, F &&launch_fn) {
+int run_staged(gpuagg_ctx *c, gpuagg_ctx::Staging &s, F &&launch_fn, hipEvent_t host_done = nullptr) {
   HIPCHK(c, hipEventRecord(s.copied, c->copy_stream));
+  if (host_done) HIPCHK(c, hipEventRecord(host_done, c->copy_stream));
   HIPCHK(c, hipStreamWaitEvent(c->stream, s.copied, 0));
   int rc = launch_fn();
   HIPCHK(c, hipEventRecord(s.released, c->stream));
   s.in_use = true;
+  if (host_done) {
+    c->stats.async_returns += 1;
+    return rc;
+  }
   HIPCHK(c, hipEventSynchronize(s.copied));
   if (hipEventQuery(s.released) == hipErrorNotReady) c->stats.async_returns += 1;
   return rc;
@@ -1771,6 +1782,10 @@ void gpuagg_destroy(gpuagg_ctx *c) {
     if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
     if (c->stream) hipStreamSynchronize(c->stream);
   }
+  // feeds over this context release their stagings of it now and refuse further puts
+  const std::vector<gpuagg_raw_feed *> feeds = c->feeds;
+  for (gpuagg_raw_feed *f : feeds) gpuagg::feed_on_ctx_destroy(f, c);
+  c->feeds.clear();
   drain_timing(c);
   for (auto *b : c->batches) {
     free_batch_cols(c, b);
@@ -2652,16 +2667,7 @@ int enrich_launch(gpuagg_ctx *c, const uint32_t *src, const uint32_t *dst, size_
 
 int gpuagg_submit(gpuagg_ctx *c, gpuagg_batch *b, size_t n) {
   if (!c || !b || n > b->capacity) return GPUAGG_EINVAL;
-  int rc = bind(c);
-  if (rc) return rc;
-  if (n == 0) return GPUAGG_OK;
-  if (c->cpu)  // the batch's host columns are read in place
-    return launch(c, ColsView{b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports,
-                              b->cols.dns_id, b->cols.tcp_id, b->cols.time_ns}, n);
-  gpuagg_ctx::Staging *s;
-  ColsView cv{};
-  if ((rc = stage_batch(c, b, n, &s, &cv))) return rc;
-  return run_staged(c, *s, [&] { return launch(c, cv, n); });
+  return gpuagg::gx_submit_batch_async(c, b, n, nullptr);
 }
 
 int gpuagg_submit_enrich(gpuagg_ctx *c, gpuagg_batch *b, size_t n, int32_t *src_slot, int32_t *dst_slot) {
@@ -2712,6 +2718,9 @@ int gpuagg_sync(gpuagg_ctx *c) {
   drain_timing(c);
   if (c->d_decode_oor)
     HIPCHK(c, x_copy(c, &c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
+  else
+    c->stats.decode_out_of_range = 0;
+  c->stats.decode_out_of_range += c->host_decode_oor;
   if (c->sparse_slots)
     HIPCHK(c, x_copy(c, &c->stats.sparse_dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
   return GPUAGG_OK;
@@ -2742,6 +2751,27 @@ int gpuagg_submit_raw_device(gpuagg_ctx *c, int kind, const void *dev_raw, size_
 
 int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
   if (!c || (n && !host_raw)) return GPUAGG_EINVAL;
+  return gpuagg::gx_submit_raw_async(c, kind, host_raw, n, nullptr);
+}
+
+}  // extern "C"
+
+namespace gpuagg {
+
+int gx_submit_batch_async(gpuagg_ctx *c, gpuagg_batch *b, size_t n, hipEvent_t host_done) {
+  int rc = bind(c);
+  if (rc) return rc;
+  if (n == 0) return GPUAGG_OK;
+  if (c->cpu)  // the batch's host columns are read in place
+    return launch(c, ColsView{b->cols.src_ip, b->cols.dst_ip, b->cols.bytes, b->cols.meta, b->cols.ports,
+                              b->cols.dns_id, b->cols.tcp_id, b->cols.time_ns}, n);
+  gpuagg_ctx::Staging *s;
+  ColsView cv{};
+  if ((rc = stage_batch(c, b, n, &s, &cv))) return rc;
+  return run_staged(c, *s, [&] { return launch(c, cv, n); }, host_done);
+}
+
+int gx_submit_raw_async(gpuagg_ctx *c, int kind, const void *host_raw, size_t n, hipEvent_t host_done) {
   if (kind != kRawPacket && kind != kRawDrop) return fail(c, GPUAGG_EINVAL, "unknown raw record kind %d", kind);
   int rc = bind(c);
   if (rc) return rc;
@@ -2758,8 +2788,37 @@ int gpuagg_submit_raw(gpuagg_ctx *c, int kind, const void *host_raw, size_t n) {
     s->raw_alloc = n * rec;
   }
   HIPCHK(c, x_copy_async(c, s->raw, host_raw, n * rec, hipMemcpyHostToDevice, c->copy_stream));
-  return run_staged(c, *s, [&] { return decode_and_launch(c, *s, kind, s->raw, n); });
+  return run_staged(c, *s, [&] { return decode_and_launch(c, *s, kind, s->raw, n); }, host_done);
 }
+
+bool gx_is_cpu(const gpuagg_ctx *c) { return c->cpu != nullptr; }
+int gx_bind(gpuagg_ctx *c) { return bind(c); }
+int gx_fail(gpuagg_ctx *c, int code, const char *msg) { return fail(c, code, "%s", msg); }
+int gx_host_alloc(gpuagg_ctx *c, void **p, size_t n) {
+  if (int rc = bind(c)) return rc;
+  if (x_host_alloc(c, p, n) != hipSuccess) return fail(c, GPUAGG_ENOMEM, "pinned host allocation (%zu bytes)", n);
+  return GPUAGG_OK;
+}
+void gx_host_free(gpuagg_ctx *c, void *p) { x_host_free(c, p); }
+int gx_prepare(gpuagg_ctx *c, size_t cap) {
+  if (c->cpu) return GPUAGG_OK;
+  if (int rc = bind(c)) return rc;
+  return ensure_staging(c, cap);
+}
+uint64_t gx_time_offset(const gpuagg_ctx *c) { return (uint64_t)c->time_offset; }
+void gx_count_host_decode(gpuagg_ctx *c, uint64_t n, uint64_t out_of_range) {
+  c->stats.decoded += n;
+  c->host_decode_oor += out_of_range;
+  c->stats.decode_out_of_range += out_of_range;  // also visible before the next sync
+}
+void gx_feed_attach(gpuagg_ctx *c, gpuagg_raw_feed *f) { c->feeds.push_back(f); }
+void gx_feed_detach(gpuagg_ctx *c, gpuagg_raw_feed *f) {
+  c->feeds.erase(std::remove(c->feeds.begin(), c->feeds.end(), f), c->feeds.end());
+}
+
+}  // namespace gpuagg
+
+extern "C" {
 
 int gpuagg_reset(gpuagg_ctx *c) {
   if (!c) return GPUAGG_EINVAL;
@@ -4439,193 +4498,54 @@ void *gpuagg_stream(gpuagg_ctx *c) { return c && !c->cpu ? (void *)c->stream : n
 
 const char *gpuagg_build_id(void) { return GPUAGG_BUILD_ID; }
 
-// dist.shard_of: h = fmix64(lo ^ fmix64(hi ^ proto << 48 ^ seed)) with lo <= hi the two
-// (ip << 16 | port) ends; shard = h mod n.
-static inline uint32_t shard_one(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto, uint32_t n) {
-  const uint64_t a = ((uint64_t)src << 16) | (ports & 0xFFFFu), b = ((uint64_t)dst << 16) | (ports >> 16);
-  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
-  const uint64_t h = fmix64(lo ^ fmix64(hi ^ ((uint64_t)(proto & 0xFFu) << 48) ^ 0x1F2E3D4C5B6A7988ULL));
-  return (uint32_t)(h % n);
-}
+}  // extern "C"
 
+namespace {
+// Splits [0, n) over host threads for the standalone shard functions (one thread below
+// 2^18 records: thread start-up would cost more than the hashing).
+template <class F>
+void shard_threads(size_t n, F &&f) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned T = n < (1u << 18) ? 1u : std::min(16u, hw);
+  if (T == 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T); });
+  f(0, n / T);
+  for (auto &x : th) x.join();
+}
+}  // namespace
+
+extern "C" {
+
+// dist.shard_of (shard_5tuple): the device of each record.
 int gpuagg_shard_columns(const uint32_t *src, const uint32_t *dst, const uint32_t *ports, const uint32_t *meta,
                          size_t n, uint32_t n_shards, uint32_t *out) {
   if (!n) return GPUAGG_OK;
   if (!src || !dst || !meta || !out || !n_shards) return GPUAGG_EINVAL;
-  for (size_t i = 0; i < n; ++i) out[i] = shard_one(src[i], dst[i], ports ? ports[i] : 0u, meta[i], n_shards);
+  shard_threads(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) out[i] = shard_5tuple(src[i], dst[i], ports ? ports[i] : 0u, meta[i], n_shards);
+  });
   return GPUAGG_OK;
 }
 
 int gpuagg_shard_raw(int kind, const void *raw, size_t n, uint32_t n_shards, uint32_t *out) {
   if (!n) return GPUAGG_OK;
   if (!raw || !out || !n_shards || (kind != GPUAGG_RAW_PACKET && kind != GPUAGG_RAW_DROP)) return GPUAGG_EINVAL;
-  const uint8_t *p = (const uint8_t *)raw;
   auto u32 = [](const uint8_t *q) { uint32_t v; memcpy(&v, q, 4); return v; };
-  auto bswap16 = [](uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); };
   // field offsets: conntrack.c:34-49 (src 12, dst 16, ports 20, proto 42) and
   // drop_reason.c:39-54 (src 0, dst 4, ports 8, proto 22); ports as HostToNetShort decodes them
   const size_t sz = kind == GPUAGG_RAW_PACKET ? GPUAGG_RAW_PACKET_SIZE : GPUAGG_RAW_DROP_SIZE;
   const size_t o_ip = kind == GPUAGG_RAW_PACKET ? 12 : 0, o_port = o_ip + 8;
   const size_t o_proto = kind == GPUAGG_RAW_PACKET ? 42 : 22;
-  for (size_t i = 0; i < n; ++i, p += sz) {
-    const uint32_t w = u32(p + o_port);
-    out[i] = shard_one(u32(p + o_ip), u32(p + o_ip + 4), bswap16(w & 0xFFFFu) | (bswap16(w >> 16) << 16), p[o_proto],
-                       n_shards);
-  }
+  shard_threads(n, [&](size_t lo, size_t hi) {
+    const uint8_t *p = (const uint8_t *)raw + lo * sz;
+    for (size_t i = lo; i < hi; ++i, p += sz)
+      out[i] = shard_5tuple(u32(p + o_ip), u32(p + o_ip + 4), raw_swap_ports(u32(p + o_port)), p[o_proto], n_shards);
+  });
   return GPUAGG_OK;
-}
-// ---- node-wide raw ingestion: shard + scatter into pinned per-device staging ------------
-}  // extern "C"
-
-struct gpuagg_raw_feed {
-  std::vector<gpuagg_ctx *> ctxs;
-  int kind = 0;
-  size_t rec = 0, cap = 0;         // bytes per record, records per device staging
-  std::vector<uint8_t *> buf;      // pinned (CPU backend: host) staging, one per context
-  std::vector<gpuagg_batch *> bat; // GPUAGG_RECORD: each context's pinned SoA batch
-  std::vector<size_t> fill;        // records staged per context
-  std::vector<uint32_t> shard;     // scratch: the device of each record of one piece
-  std::vector<uint64_t> submitted; // records handed to each context so far
-};
-
-namespace {
-int feed_submit(gpuagg_raw_feed *f, size_t d) {
-  if (!f->fill[d]) return GPUAGG_OK;
-  // gpuagg_submit(_raw) returns once the H2D copy (a DMA: the staging is pinned) is done,
-  // so the staging is refilled while the device decodes and aggregates it
-  const int rc = f->kind == GPUAGG_RECORD ? gpuagg_submit(f->ctxs[d], f->bat[d], f->fill[d])
-                                          : gpuagg_submit_raw(f->ctxs[d], f->kind, f->buf[d], f->fill[d]);
-  if (rc == GPUAGG_OK) f->submitted[d] += f->fill[d];
-  f->fill[d] = 0;
-  return rc;
-}
-
-void feed_free(gpuagg_raw_feed *f) {
-  for (size_t d = 0; d < f->buf.size(); ++d)
-    if (f->buf[d]) x_host_free(f->ctxs[d], f->buf[d]);
-  for (size_t d = 0; d < f->bat.size(); ++d)
-    if (f->bat[d]) gpuagg_free_batch(f->ctxs[d], f->bat[d]);
-  delete f;
-}
-
-// One decoded record into position i of a SoA batch.
-inline void put_record(gpuagg_batch *b, size_t i, const gpuagg_record &r) {
-  b->cols.src_ip[i] = r.src_ip;
-  b->cols.dst_ip[i] = r.dst_ip;
-  b->cols.bytes[i] = r.bytes;
-  b->cols.meta[i] = r.meta;
-  b->cols.ports[i] = r.ports;
-  b->cols.dns_id[i] = r.dns_id;
-  b->cols.tcp_id[i] = r.tcp_id;
-  b->cols.time_ns[i] = r.time_ns;
-}
-}  // namespace
-
-extern "C" {
-
-int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
-                           gpuagg_raw_feed **out) {
-  if (!ctxs || !n_ctx || !out || !capacity || (kind != kRawPacket && kind != kRawDrop && kind != GPUAGG_RECORD))
-    return GPUAGG_EINVAL;
-  *out = nullptr;
-  for (size_t d = 0; d < n_ctx; ++d)
-    if (!ctxs[d]) return GPUAGG_EINVAL;
-  auto *f = new gpuagg_raw_feed();
-  f->ctxs.assign(ctxs, ctxs + n_ctx);
-  f->kind = kind;
-  f->rec = kind == kRawPacket ? GPUAGG_RAW_PACKET_SIZE : kind == kRawDrop ? GPUAGG_RAW_DROP_SIZE : sizeof(gpuagg_record);
-  f->cap = capacity;
-  f->buf.assign(n_ctx, nullptr);
-  f->bat.assign(n_ctx, nullptr);
-  f->fill.assign(n_ctx, 0);
-  f->submitted.assign(n_ctx, 0);
-  for (size_t d = 0; d < n_ctx; ++d) {
-    gpuagg_ctx *c = ctxs[d];
-    if (kind == GPUAGG_RECORD) {  // the context's own pinned SoA batch (gpuagg_submit)
-      if (int rc = gpuagg_alloc_batch(c, capacity, &f->bat[d])) {
-        feed_free(f);
-        return rc;
-      }
-      continue;
-    }
-    if (bind(c) || x_host_alloc(c, (void **)&f->buf[d], capacity * f->rec) != hipSuccess) {
-      fail(c, GPUAGG_ENOMEM, "raw feed staging (%zu records)", capacity);
-      feed_free(f);
-      return GPUAGG_ENOMEM;
-    }
-    if (!c->cpu) {  // device staging sized once, not at the first submit
-      if (int rc = ensure_staging(c, capacity)) {
-        feed_free(f);
-        return rc;
-      }
-    }
-  }
-  *out = f;
-  return GPUAGG_OK;
-}
-
-int gpuagg_raw_feed_put(gpuagg_raw_feed *f, const void *raw, size_t n) {
-  if (!f || (n && !raw)) return GPUAGG_EINVAL;
-  const uint8_t *p = (const uint8_t *)raw;
-  const size_t nd = f->ctxs.size(), rec = f->rec;
-  int err = GPUAGG_OK;
-  if (f->kind == GPUAGG_RECORD) {  // decoded records: shard and transpose into the SoA batches
-    const gpuagg_record *r = (const gpuagg_record *)raw;
-    for (size_t i = 0; i < n; ++i) {
-      const size_t d = nd == 1 ? 0 : shard_one(r[i].src_ip, r[i].dst_ip, r[i].ports, r[i].meta, (uint32_t)nd);
-      put_record(f->bat[d], f->fill[d], r[i]);
-      if (++f->fill[d] == f->cap)
-        if (int rc = feed_submit(f, d)) err = err ? err : rc;
-    }
-    return err;
-  }
-  if (nd == 1) {  // one device: straight into its staging
-    while (n) {
-      const size_t m = std::min(n, f->cap - f->fill[0]);
-      memcpy(f->buf[0] + f->fill[0] * rec, p, m * rec);
-      f->fill[0] += m;
-      p += m * rec;
-      n -= m;
-      if (f->fill[0] == f->cap)
-        if (int rc = feed_submit(f, 0)) err = err ? err : rc;
-    }
-    return err;
-  }
-  // pieces of <= 2^16 records: the device of each (gpuagg_shard_raw), then one copy of
-  // each record into its device's staging (a full staging is submitted on the spot)
-  constexpr size_t kPiece = 1u << 16;
-  if (f->shard.size() < std::min(n, kPiece)) f->shard.resize(std::min(n, kPiece));
-  while (n) {
-    const size_t m = std::min(n, kPiece);
-    gpuagg_shard_raw(f->kind, p, m, (uint32_t)nd, f->shard.data());
-    for (size_t i = 0; i < m; ++i) {
-      const uint32_t d = f->shard[i];
-      memcpy(f->buf[d] + f->fill[d] * rec, p + i * rec, rec);
-      if (++f->fill[d] == f->cap)
-        if (int rc = feed_submit(f, d)) err = err ? err : rc;
-    }
-    p += m * rec;
-    n -= m;
-  }
-  return err;
-}
-
-int gpuagg_raw_feed_flush(gpuagg_raw_feed *f) {
-  if (!f) return GPUAGG_EINVAL;
-  int err = GPUAGG_OK;
-  for (size_t d = 0; d < f->ctxs.size(); ++d)
-    if (int rc = feed_submit(f, d)) err = err ? err : rc;
-  return err;
-}
-
-int gpuagg_raw_feed_submitted(const gpuagg_raw_feed *f, uint64_t *per_ctx, size_t n_ctx) {
-  if (!f || !per_ctx || n_ctx < f->ctxs.size()) return GPUAGG_EINVAL;
-  for (size_t d = 0; d < f->ctxs.size(); ++d) per_ctx[d] = f->submitted[d];
-  return GPUAGG_OK;
-}
-
-void gpuagg_raw_feed_destroy(gpuagg_raw_feed *f) {
-  if (f) feed_free(f);
 }
 
 const char *gpuagg_kernel_name(const gpuagg_ctx *c) { return c ? c->kernel_name.c_str() : ""; }

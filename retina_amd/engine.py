@@ -492,7 +492,7 @@ class RawFeed:
     5-tuple (gpuagg_shard_raw's / gpuagg_shard_columns' function) and copied into each
     context's pinned staging in the library; full stagings are submitted as they fill."""
 
-    def __init__(self, engines, kind: int, capacity: int = 1 << 20):
+    def __init__(self, engines, kind: int, capacity: int = 1 << 20, threads: int = 0, mode: int = None):
         self.engines = list(engines)
         self.lib = self.engines[0].lib
         self.kind = kind
@@ -504,6 +504,16 @@ class RawFeed:
             msg = self.lib.gpuagg_last_error(self.engines[0].h)
             raise GpuAggError(rc, "gpuagg_raw_feed_create: %s" % (msg.decode() if msg else ""))
         self.h = h
+        if threads or mode is not None:
+            self.configure(threads, _abi.FEED_RAW_DMA if mode is None else mode)
+
+    def configure(self, threads: int = 0, mode: int = _abi.FEED_RAW_DMA) -> None:
+        """Host threads per put (0: keep) and, for raw kinds, where samples are decoded
+        (FEED_RAW_DMA, the default: the 72/32-byte samples are copied and decoded on the
+        GPU; FEED_HOST_DECODE: on the feed's threads, only the plan's columns cross PCIe)."""
+        rc = self.lib.gpuagg_raw_feed_configure(self.h, threads, mode)
+        if rc != _abi.OK:
+            raise GpuAggError(rc, "gpuagg_raw_feed_configure")
 
     def put(self, raw: np.ndarray) -> None:
         raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)

@@ -411,7 +411,55 @@ def undefined_calls(files: list) -> list:
     return errs
 
 
+def struct_fields(files: list) -> dict:
+    """type name -> field names (embedded fields by their type name) of the package's structs."""
+    out = {}
+    for f in files:
+        for mm in re.finditer(r"^type\s+(\w+)\s+struct\s*\{(.*?)^\}", f.code, re.M | re.S):
+            names = set()
+            depth = 0
+            for ln in mm.group(2).splitlines():
+                t = ln.strip()
+                if depth == 0 and t:
+                    m2 = re.match(r"([A-Za-z_]\w*(?:\s*,\s*[A-Za-z_]\w*)*)\s+\S", t)
+                    if m2:
+                        names.update(re.split(r"\s*,\s*", m2.group(1)))
+                    else:  # embedded: *pkg.Type or Type
+                        m3 = re.match(r"\*?(?:\w+\.)?(\w+)\s*$", t)
+                        if m3:
+                            names.add(m3.group(1))
+                depth += ln.count("{") - ln.count("}")
+            out[mm.group(1)] = names
+    return out
+
+
+def selector_errors(files: list) -> list:
+    """Inside a method of struct T, `recv.x` must be a field or method of T."""
+    errs = []
+    fields = struct_fields(files)
+    meths: dict = {}
+    for f in files:
+        for rt, nm, _ in f.methods:
+            meths.setdefault(rt, set()).add(nm)
+    for f in files:
+        heads = [(m.start(), m) for m in re.finditer(r"^func\s+\(\s*(\w+)\s+\*?\s*(\w+)\s*\)", f.code, re.M)]
+        starts = sorted([m.start() for m in re.finditer(r"^func\b", f.code, re.M)] + [len(f.code)])
+        for pos, m in heads:
+            recv, typ = m.group(1), m.group(2)
+            if typ not in fields:
+                continue
+            end = next(x for x in starts if x > pos)
+            body = f.code[pos:end]
+            allowed = fields[typ] | meths.get(typ, set())
+            for sm in re.finditer(r"(?<![\w.])" + recv + r"\.(\w+)", body):
+                if sm.group(1) not in allowed:
+                    errs.append(f"{os.path.basename(f.path)}:{_line(f.code, pos + sm.start())}: {recv}.{sm.group(1)} "
+                                f"undefined (type *{typ} has no field or method {sm.group(1)})")
+    return errs
+
+
 def all_errors() -> list:
     files = load_package()
     return (duplicate_declarations(files) + import_errors(files) + cgo_errors(files) + record_layout_errors(files)
-            + undefined_calls(files) + snippet_errors(os.path.join(ROOT, "INTEGRATION.md"), files))
+            + undefined_calls(files) + selector_errors(files)
+            + snippet_errors(os.path.join(ROOT, "INTEGRATION.md"), files))

@@ -68,12 +68,16 @@ def test_bad_arguments(lib):
     assert lib.gpuagg_shard_raw(_abi.RAW_PACKET, raw.ctypes.data_as(C.c_void_p), 1, 0, _u32p(out)) == _abi.EINVAL
 
 
-@pytest.mark.parametrize("world,cap", [(1, 5_000), (3, 4_096), (8, 1_000)])
-def test_raw_feed_scatter(lib, world, cap):
+@pytest.mark.parametrize("world,cap,threads,mode", [(1, 5_000, 1, 0), (1, 5_000, 8, 0), (1, 5_000, 3, 1),
+                                                    (3, 4_096, 4, 0), (3, 4_096, 1, 1), (8, 1_000, 8, 0),
+                                                    (8, 1_000, 5, 1)])
+def test_raw_feed_scatter(lib, world, cap, threads, mode):
     """gpuagg_raw_feed_* (the Go plugin's node-wide raw path) on CPU-backend contexts:
     every context receives exactly the records gpuagg_shard_raw assigns it, its series
     equal the oracle over that shard, and the merged state equals one context fed
-    everything.  Capacities smaller than the input force submits in the middle of a put."""
+    everything.  Capacities smaller than the input force submits in the middle of a put
+    (and pieces that straddle the two stagings); host-decoded (mode 0) and raw-copied
+    (mode 1, decoded by the context) samples, one and several feed threads."""
     from retina_amd import RawFeed, _abi
     from .helpers import diff_series, make_engine, oracle_series
     pods = W.make_pods(300, seed=21)
@@ -86,7 +90,7 @@ def test_raw_feed_scatter(lib, world, cap):
         shard = np.zeros(n, np.uint32)
         assert lib.gpuagg_shard_raw(kind, raw.ctypes.data_as(C.c_void_p), n, world, _u32p(shard)) == 0
         engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(world)]
-        feed = RawFeed(engines, kind, capacity=cap)
+        feed = RawFeed(engines, kind, capacity=cap, threads=threads, mode=mode)
         try:
             step = 2_500  # several puts, unaligned with the capacity
             for a in range(0, n, step):
@@ -99,10 +103,80 @@ def test_raw_feed_scatter(lib, world, cap):
                 want = oracle_series(part, pods, sp, False)
                 got = g.snapshot()
                 assert got == want, diff_series(got, want)
+            st = [g.stats() for g in engines]
+            assert sum(x["decoded"] for x in st) == n
+            assert sum(x["decode_out_of_range"] for x in st) == 0
         finally:
             feed.close()
             for g in engines:
                 g.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_raw_feed_out_of_range_rows_counted(lib, mode):
+    """Rows whose traffic direction does not fit the meta word are counted in
+    gpuagg_stats.decode_out_of_range whichever side decodes them, and feed no metric."""
+    from retina_amd import RawFeed, _abi
+    from .helpers import diff_series, make_engine, oracle_series
+    pods = W.make_pods(100, seed=41)
+    sp = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+    raw = W.gen_raw_packets(6_000, pods, seed=42, out_of_range_frac=0.05)
+    b, bad = D.decode_packets(raw)
+    g = make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND)
+    feed = RawFeed([g], _abi.RAW_PACKET, capacity=2_000, threads=4, mode=mode)
+    try:
+        feed.put(raw)
+        feed.flush()
+        g.sync()
+        assert g.stats()["decode_out_of_range"] == int(bad.sum()) > 0
+        part = W.Records(b.src_ip, b.dst_ip, b.bytes, b.meta, b.ports, b.dns_id)
+        want = oracle_series(part, pods, sp, False)
+        got = g.snapshot()
+        assert got == want, diff_series(got, want)
+    finally:
+        feed.close()
+        g.close()
+
+
+def test_raw_feed_after_context_destroy(lib):
+    """gpuagg_destroy detaches the feeds over the context: later puts and flushes return
+    GPUAGG_ESTATE, and the feed's own destroy is still safe (no use after free)."""
+    from retina_amd import GpuAggError, RawFeed, _abi
+    from .helpers import make_engine
+    pods = W.make_pods(50, seed=43)
+    sp = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+    raw = W.gen_raw_packets(1_000, pods, seed=44)
+    engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(2)]
+    feed = RawFeed(engines, _abi.RAW_PACKET, capacity=4_096)
+    feed.put(raw)
+    engines[1].close()
+    with pytest.raises(GpuAggError) as e:
+        feed.put(raw)
+    assert e.value.code == _abi.ESTATE
+    with pytest.raises(GpuAggError):
+        feed.flush()
+    feed.close()
+    engines[0].close()
+
+
+def test_raw_feed_configure_needs_an_empty_feed(lib):
+    from retina_amd import GpuAggError, RawFeed, _abi
+    from .helpers import make_engine
+    pods = W.make_pods(50, seed=45)
+    sp = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+    g = make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND)
+    feed = RawFeed([g], _abi.RAW_PACKET, capacity=4_096)
+    try:
+        feed.put(W.gen_raw_packets(100, pods, seed=46))
+        with pytest.raises(GpuAggError) as e:
+            feed.configure(4, _abi.FEED_RAW_DMA)
+        assert e.value.code == _abi.ESTATE
+        feed.flush()
+        feed.configure(4, _abi.FEED_RAW_DMA)
+        assert lib.gpuagg_raw_feed_configure(feed.h, 0, 7) == _abi.EINVAL
+    finally:
+        feed.close()
+        g.close()
 
 
 def test_raw_feed_rejects_bad_args(lib):

@@ -128,3 +128,13 @@ def test_integration_snippet_check(tmp_path):
 def test_every_file_has_the_build_tag(name):
     f = gs.parse_go(os.path.join(gs.GO_PKG, name))
     assert f.build == "linux && gpuagg" and f.package == "gpuagg"
+
+
+def test_receiver_selectors_are_checked(tmp_path):
+    fs = _pkg(tmp_path, {
+        "a.go": HDR + "type T struct {\n\tmu sync.Mutex\n\ta, b int\n\t*Embedded\n}\n\n"
+                      "func (t *T) f() int { t.mu.Lock(); t.g(); return t.a + t.b + t.rawBuf + t.Embedded.x }\n\n"
+                      "func (t *T) g() {}\n",
+    })
+    errs = gs.selector_errors(fs)
+    assert len(errs) == 1 and "t.rawBuf undefined" in errs[0]

@@ -111,6 +111,54 @@ def test_raw_aggregate_vs_oracle(gpu_device, remote, host_fed):
     assert got == want, diff_series(got, want)
 
 
+@pytest.mark.parametrize("mode", [_abi.FEED_HOST_DECODE, _abi.FEED_RAW_DMA], ids=["host-decode", "raw-dma"])
+@pytest.mark.parametrize("world,threads", [(1, 1), (1, 8), (3, 4)])
+@pytest.mark.parametrize("remote", [False, True], ids=["local", "remote"])
+def test_raw_feed_vs_oracle(gpu_device, remote, world, threads, mode):
+    """The Go plugin's raw path: gpuagg_raw_feed_put over `world` contexts (all on this GPU),
+    two pinned stagings per context submitted without waiting for their DMA, samples decoded
+    on the feed's threads or on the GPU.  Every context's series equal the oracle over the
+    records gpuagg_shard_raw gives it; capacities force many stagings and straddling pieces."""
+    import ctypes as C
+    from retina_amd import RawFeed
+    pods = W.make_pods(300, seed=24)
+    pk = W.gen_raw_packets(60_000, pods, seed=25, odd_frac=0.1, out_of_range_frac=0.01)
+    dr = W.gen_raw_drops(20_000, pods, seed=26, out_of_range_frac=0.01)
+    spec = SPEC_REMOTE if remote else SPEC_LOCAL
+    engines = [make_engine(pods, spec, remote, gpu_device) for _ in range(world)]
+    feeds = [RawFeed(engines, k, capacity=cap, threads=threads, mode=mode)
+             for k, cap in ((_abi.RAW_PACKET, 6_000), (_abi.RAW_DROP, 3_000))]
+    try:
+        for feed, raw in zip(feeds, (pk, dr)):
+            sz = feed.size
+            n = len(raw) // sz
+            for a in range(0, n, 7_000):
+                feed.put(raw[a * sz:min(n, a + 7_000) * sz])
+            feed.flush()
+        shards = []
+        for kind, raw, sz in ((_abi.RAW_PACKET, pk, 72), (_abi.RAW_DROP, dr, 32)):
+            sh = np.zeros(len(raw) // sz, np.uint32)
+            assert engines[0].lib.gpuagg_shard_raw(kind, raw.ctypes.data_as(C.c_void_p), len(sh), world,
+                                                   sh.ctypes.data_as(_abi.u32p)) == 0
+            shards.append(sh)
+        assert feeds[0].submitted() == [int((shards[0] == d).sum()) for d in range(world)]
+        _, bad_p = D.decode_packets(pk)
+        _, bad_d = D.decode_drops(dr)
+        for d, g in enumerate(engines):
+            mp, md = shards[0] == d, shards[1] == d
+            # out-of-range rows are counted and consumed by no metric (the oracle would label them)
+            want = _oracle_raw_series(pk.reshape(-1, 72)[mp & ~bad_p].reshape(-1),
+                                      dr.reshape(-1, 32)[md & ~bad_d].reshape(-1), pods, spec, remote)
+            got = g.snapshot()
+            assert got == want, diff_series(got, want)
+            assert g.stats()["decode_out_of_range"] == int(bad_p[mp].sum() + bad_d[md].sum())
+    finally:
+        for f in feeds:
+            f.close()
+        for g in engines:
+            g.close()
+
+
 def test_unencodable_rows_are_not_aggregated(gpu_device):
     """traffic_direction > 3 / drop_type > 7: counted, consumed by no metric."""
     pods = W.make_pods(100, seed=31)

@@ -85,10 +85,13 @@ def test_host_fed_and_text(gpu_device):
     assert "networkobservability_adv_forward_count" in text
 
 
-def test_raw_packet_decode_path(gpu_device):
+@pytest.mark.parametrize("path", ["device", "feed-host-decode", "feed-raw-dma"])
+def test_raw_packet_decode_path(gpu_device, path):
     """72-byte packetparser records: TcpId from TSval / TSecr by observation point, the
-    time from t_nsec + the monotonic offset."""
-    from retina_amd import _abi
+    time from t_nsec + the monotonic offset -- decoded on the GPU from device memory, or
+    handed to a raw feed (decoded on its host threads, or copied and decoded on the GPU)
+    in pieces across several 256-record stagings (requests carried between batches)."""
+    from retina_amd import RawFeed, _abi
     import torch
     pods = W.make_pods(100, seed=31)
     recs = W.gen_latency_records(150, pods, API, seed=32, background=500)
@@ -110,8 +113,19 @@ def test_raw_packet_decode_path(gpu_device):
     g = _engine(pods, gpu_device)
     try:
         g.set_time_offset(off)
-        d = torch.from_numpy(raw.reshape(-1)).to(torch.device("cuda", gpu_device))
-        g.submit_raw_device(_abi.RAW_PACKET, d.data_ptr(), n)
+        if path == "device":
+            d = torch.from_numpy(raw.reshape(-1)).to(torch.device("cuda", gpu_device))
+            g.submit_raw_device(_abi.RAW_PACKET, d.data_ptr(), n)
+        else:
+            mode = _abi.FEED_HOST_DECODE if path == "feed-host-decode" else _abi.FEED_RAW_DMA
+            feed = RawFeed([g], _abi.RAW_PACKET, capacity=256, threads=4, mode=mode)
+            try:
+                flat = raw.reshape(-1)
+                for a in range(0, n, 100):
+                    feed.put(flat[a * 72:min(n, a + 100) * 72])
+                feed.flush()
+            finally:
+                feed.close()
         got = _state(g)
     finally:
         g.close()
