@@ -381,6 +381,8 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: config size)")
     ap.add_argument("--cpu-sample", type=int, default=16_000_000,
                     help="records in the tuned CPU baseline sample (go-shaped: 1/8 of it)")
+    ap.add_argument("--settle-ms", type=float, default=40.0,
+                    help="untimed passes of the step for this long before the warm-up steps (clock settle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
     ap.add_argument("--no-scrape", action="store_true", help="skip the snapshot / render timing")
@@ -436,6 +438,17 @@ def main():
         g.close()
         return
 
+    # settle: untimed passes of the same step until the GPU's clocks reach the steady
+    # state an always-on agent runs at.  After idle the tier-1 kernel's time rises for
+    # ~10 launches and settles after ~25 (0.409 -> 0.425 -> 0.404 ms at C2, the same after
+    # 2 s idle: profiles/round5/r5k_ramp.jsonl), so the driver's 5 warm-up steps left the
+    # timed region in the hump.  Reported as `settle`; the timed region is unchanged.
+    settle_n, t_settle = 0, time.perf_counter()
+    while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        g.submit_device(dcols, n)
+        g.sync()
+        settle_n += 1
+    settle_s = time.perf_counter() - t_settle
     for _ in range(args.warmup):
         g.submit_device(dcols, n)
     g.sync()
@@ -516,6 +529,9 @@ def main():
             "step_bytes_per_record": bpr,
         },
         "build_id": build_id,
+        "settle": {"launches": settle_n, "s": settle_s,
+                   "note": "untimed passes of the step before the warm-up steps, so the timed region runs at "
+                           "steady-state clocks (profiles/round5/r5k_ramp.jsonl)"},
     }
     if rank == 0 and not args.no_scrape:
         result["scrape"] = scrape_cost(g)

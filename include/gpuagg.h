@@ -394,8 +394,10 @@ typedef struct gpuagg_state_desc {
   size_t sparse_len;                            /* group-by table slots (0: none): an
                                                    upper bound on exported entries */
   uint64_t *latency;       size_t latency_len;  /* node-apiserver latency histograms, counts,
-                                                   sums and no_response: sum u64 (NULL / 0
-                                                   when latency metrics are off)          */
+                                                   sums, no_response, capacity evictions and
+                                                   batches: words [0, 35) sum u64, words
+                                                   [35, latency_len) (peak live requests)
+                                                   max u64 (NULL / 0 when latency is off)  */
 } gpuagg_state_desc;
 
 int gpuagg_state(gpuagg_ctx *ctx, gpuagg_state_desc *out);

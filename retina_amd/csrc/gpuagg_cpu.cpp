@@ -439,6 +439,7 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
   auto bucket = [](int64_t v) -> uint32_t { return v <= 0 ? 0u : v >= 5 ? 10u : (uint32_t)(2 * v); };
   uint64_t clk = st[kLatClock];
   uint64_t seq = st[kLatSeqBase], peak = live.size();
+  bool bound = false;  // the capacity evicted in this batch (the device's sequential-pass batches)
   for (size_t i = 0; i < a.n; ++i) {
     clk = std::max<uint64_t>(clk, a.time_ns[i]);
     const uint32_t m = a.meta[i];
@@ -472,6 +473,7 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
           live.erase(front());
           lru.pop_front();
           st[kLatCapEvictions] += 1;
+          bound = true;
         }
         live[key] = E{clk + kLatTtlNs, my_seq, nanos, syn};
         peak = std::max<uint64_t>(peak, live.size());
@@ -508,6 +510,7 @@ void Engine::latency(const LatArgs &a, uint32_t enabled) {
   st[kLatClock] = clk;
   st[kLatPending] = carry_.size();
   st[kLatPeakLive] = std::max<uint64_t>(st[kLatPeakLive], peak);
+  st[kLatCapBatches] += bound ? 1u : 0u;
 }
 
 void Engine::latency_reset() { carry_.clear(); }

@@ -26,8 +26,10 @@
 // without counting it.  The capacity couples the keys, so before step 5 a first walk
 // (kPass 0) books every entry's life as +1 / -1 at event positions, a scan gives the live
 // count before each event and its maximum; while it stays within the limit (the normal
-// case) the keys are independent and step 5 is exact, else step 5 stands down and
-// lat_serial_kernel replays the batch in event order with an LRU queue (exact, slow, rare).
+// case) the keys are independent and step 5 is exact, else the host replays the batch in
+// event order with an LRU queue (gpuagg_runtime.cpp lat_serial_host: exact, rare; it was a
+// one-thread kernel until round 5, 1.7 s per capacity-bound 2^20-record batch,
+// profiles/round5/r5l_lat_serial.jsonl).
 // Latency traffic is a small share of a node's records; the filter pass (1, 3) streams
 // 36 B per record (src, dst, meta, ports, tcp_id, time_ns).
 #include <cstring>  // rocprim's texture iterator uses memset
@@ -214,7 +216,7 @@ __device__ __forceinline__ uint32_t lat_bucket(int64_t v) {
 
 // kPass 0: each entry's life as event positions (delta[first] += 1, delta[gone] -= 1; no
 // other effect) for the capacity check.  kPass 1: the join's effects -- histograms,
-// no_response, the carry-out -- unless the capacity bound (lat_serial_kernel's batch).
+// no_response, the carry-out -- unless the capacity bound (the host's sequential replay).
 // An entry leaves at the reply that deletes it, or just before the first record event
 // whose clock passes its expiry (the cleaner evicts it then).
 template <int kPass>
@@ -321,129 +323,6 @@ __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32
   }
 }
 
-// The batch in event order when the capacity binds: the ttlcache itself, single-threaded
-// (every event depends on the live set the earlier ones left).  Items live in a pool, a
-// linear-probing table maps keys to them, and a queue of touches in order is the LRU
-// list (a record is stale once its item is touched again or freed): its front valid item
-// is the least recently touched, which is also the first to expire.
-__global__ __launch_bounds__(1024) void lat_serial_kernel(LatArgs a, uint32_t enabled) {
-  if (*a.max_live <= (int64_t)a.limit) return;
-  for (uint32_t k = threadIdx.x; k <= a.table_mask; k += blockDim.x) a.table[k] = 0u;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  unsigned long long *st = a.state;
-  const uint64_t n = st[kLatEvents], pend = st[kLatPending];
-  const uint32_t mask = a.table_mask;
-  uint32_t top = 0, nfree = 0;  // pool: never-used prefix, free stack
-  uint64_t qh = 0, qt = 0, live = 0;
-  auto home = [&](uint64_t k0, uint64_t k1) { return (uint32_t)lat_hash(k0, k1) & mask; };
-  auto find = [&](uint64_t k0, uint64_t k1) -> int64_t {  // table slot, or -1
-    for (uint32_t s = home(k0, k1);; s = (s + 1) & mask) {
-      const uint32_t v = a.table[s];
-      if (!v) return -1;
-      const LatEntry &x = a.pool[v - 1];
-      if (x.k0 == k0 && x.k1 == k1) return s;
-    }
-  };
-  auto erase = [&](uint32_t s) {  // backward-shift deletion, frees the item
-    const uint32_t idx = a.table[s] - 1;
-    a.pool[idx].seq = ~0ULL;
-    a.free_idx[nfree++] = idx;
-    for (uint32_t t = (s + 1) & mask;; t = (t + 1) & mask) {
-      const uint32_t v = a.table[t];
-      if (!v) break;
-      const uint32_t hm = home(a.pool[v - 1].k0, a.pool[v - 1].k1);
-      // the item at t may move to s unless its home lies cyclically in (s, t]
-      const bool stay = s <= t ? (hm > s && hm <= t) : (hm > s || hm <= t);
-      if (!stay) {
-        a.table[s] = v;
-        s = t;
-      }
-    }
-    a.table[s] = 0u;
-    --live;
-  };
-  auto insert = [&](const LatEntry &x) {
-    const uint32_t idx = nfree ? a.free_idx[--nfree] : top++;
-    a.pool[idx] = x;
-    uint32_t s = home(x.k0, x.k1);
-    while (a.table[s]) s = (s + 1) & mask;
-    a.table[s] = idx + 1;
-    a.queue[qt++] = LatTouch{x.seq, idx, 0u};
-    ++live;
-  };
-  // the front valid item (skipping stale records), or ~0
-  auto front = [&]() -> uint32_t {
-    while (qh < qt) {
-      const LatTouch r = a.queue[qh];
-      if (a.pool[r.idx].seq == r.seq) return r.idx;
-      ++qh;
-    }
-    return ~0u;
-  };
-  for (uint64_t k = 0; k < pend; ++k) {  // carried items, least recently touched first
-    const LatEvent c = a.ev[a.carry_order[k]];
-    insert(LatEntry{c.k0, c.k1, c.clock, c.seq, c.nanos, (c.bits >> 2) & 1u});
-  }
-  for (uint64_t pos = pend; pos < n; ++pos) {
-    const LatEvent e = a.ev[pos];
-    for (uint32_t f = front(); f != ~0u && e.clock > a.pool[f].expires; f = front()) {
-      erase((uint32_t)find(a.pool[f].k0, a.pool[f].k1));  // expired before this record
-      ++qh;
-      if (enabled & 4u) st[kLatNoResponse] += 1;
-    }
-    const int64_t s = find(e.k0, e.k1);
-    if ((e.bits & 3u) == kRoleReq) {
-      if (s >= 0) {  // Get hit: touched
-        const uint32_t idx = a.table[s] - 1;
-        a.pool[idx].expires = e.clock + kLatTtlNs;
-        a.pool[idx].seq = e.seq;
-        a.queue[qt++] = LatTouch{e.seq, idx, 0u};
-        continue;
-      }
-      if (live >= a.limit) {  // Set at capacity: the LRU back goes, uncounted
-        const uint32_t f = front();
-        erase((uint32_t)find(a.pool[f].k0, a.pool[f].k1));
-        ++qh;
-        st[kLatCapEvictions] += 1;
-      }
-      insert(LatEntry{e.k0, e.k1, e.clock + kLatTtlNs, e.seq, e.nanos, (e.bits >> 2) & 1u});
-    } else if (s >= 0) {  // reply: latency, then Delete
-      const LatEntry x = a.pool[a.table[s] - 1];
-      const int64_t d = (int64_t)e.nanos - (int64_t)x.nanos;
-      const int64_t ad = d < 0 ? -d : d;
-      const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
-      const uint32_t bk = lat_bucket(lat);
-      if (enabled & 1u) {
-        st[kLatHist + bk] += 1;
-        st[kLatHist + 11] += 1;
-        st[kLatHist + 12] += (unsigned long long)lat;
-      }
-      if ((enabled & 2u) && x.syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
-        st[kLatHandshake + bk] += 1;
-        st[kLatHandshake + 11] += 1;
-        st[kLatHandshake + 12] += (unsigned long long)lat;
-      }
-      erase((uint32_t)s);
-    }
-  }
-  // batch end: expired items count, the rest carry over in LRU order
-  const unsigned long long clk_end = st[kLatClockEnd];
-  uint64_t out = 0;
-  for (uint32_t f = front(); f != ~0u; f = front()) {
-    const LatEntry x = a.pool[f];
-    if (clk_end > x.expires) {
-      if (enabled & 4u) st[kLatNoResponse] += 1;
-    } else {
-      a.carry_out[out++] = LatEvent{x.k0, x.k1, x.expires, x.seq, x.nanos, kRoleCarry | (x.syn ? 4u : 0u)};
-    }
-    a.pool[f].seq = ~0ULL;
-    ++qh;
-  }
-  st[kLatCarryOut] = out;
-  st[kLatCapBatches] += 1;
-}
-
 __global__ void lat_finish_kernel(unsigned long long *st, const int32_t *max_live, uint64_t limit) {
   st[kLatSeqBase] += st[kLatEvents] - st[kLatPending];
   st[kLatClock] = st[kLatClockEnd];
@@ -496,8 +375,8 @@ hipError_t latency_carry_order(const LatEvent *carry, size_t n, unsigned long lo
   return rocprim::radix_sort_pairs(tmp, tb, keys, keys + n, vals, vals + n, n, 0, 64, st);
 }
 
-hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
-                               uint32_t enabled, hipStream_t st) {
+hipError_t launch_latency_check(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
+                                uint32_t enabled, hipStream_t st) {
   hipError_t e;
   if (n_events) {
     size_t tb = tmp_bytes;
@@ -517,9 +396,18 @@ hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, siz
     if ((e = rocprim::reduce(tmp, tb, a.live, a.max_live, (int32_t)0, n_events + 1, rocprim::maximum<int32_t>(),
                              st)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(lat_walk_kernel<1>, grid, dim3(kLatThreads), 0, st, a, enabled);
-    hipLaunchKernelGGL(lat_serial_kernel, dim3(1), dim3(1024), 0, st, a, enabled);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_latency_walk(const LatArgs &a, size_t n_events, uint32_t enabled, hipStream_t st) {
+  if (!n_events) return hipSuccess;
+  hipLaunchKernelGGL(lat_walk_kernel<1>, dim3((uint32_t)((n_events + kLatThreads - 1) / kLatThreads)),
+                     dim3(kLatThreads), 0, st, a, enabled);
+  return hipGetLastError();
+}
+
+hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, hipStream_t st) {
   hipLaunchKernelGGL(lat_finish_kernel, dim3(1), dim3(1), 0, st, a.state, n_events ? a.max_live : nullptr,
                      a.limit);
   return hipGetLastError();

@@ -165,12 +165,14 @@ constexpr uint64_t kLatTtlNs = 500000000ULL;  // latency.go:34
 enum : uint32_t {
   kLatClock = 0, kLatPending = 1, kLatCarryOut = 2, kLatClockEnd = 3, kLatEvents = 4,
   kLatSeqBase = 5,     // events numbered so far (LatEvent.seq of this batch's first event)
-  kLatPeakLive = 6,    // most live requests at any event (the batch's max of the live count)
-  kLatCapBatches = 7,  // batches the capacity bound (run by the sequential pass)
   kLatHist = 8,        // 11 buckets (le 0, 0.5 .. 4.5, +Inf), count, sum (i64)
   kLatHandshake = 24,  // same layout
   kLatNoResponse = 40,
   kLatCapEvictions = 41,  // requests evicted by the capacity (EvictionReasonCapacityReached)
+  kLatCapBatches = 42,    // batches the capacity bound (run by the sequential pass)
+  // Words [kLatHist, kLatPeakLive) restart at an epoch reset and are summed by a merge;
+  // [kLatPeakLive, kLatStateWords) restart too and are max-merged.
+  kLatPeakLive = 43,   // most live requests at any event (the batch's max of the live count)
   kLatStateWords = 48
 };
 struct LatArgs {
@@ -196,19 +198,20 @@ struct LatArgs {
   int32_t *delta, *live;            // [n_events + 1]: +1 / -1 per entry life, its prefix sums
   int32_t *max_live;                // max of live[] (device scalar)
   const uint32_t *carry_order;      // carried entries' positions in LRU (seq) order
-  LatEntry *pool;                   // [limit] ttlcache items
-  uint32_t *table;                  // [table_mask + 1] pool index + 1 (0: empty), linear probing
-  uint32_t table_mask;
-  uint32_t *free_idx;               // [limit] free-list stack
-  LatTouch *queue;                  // [n_events] touches in LRU order
 };
 hipError_t launch_latency_front(const LatArgs &a, hipStream_t st);
 hipError_t latency_sort_bytes(size_t n, size_t *bytes);
 // The carried entries' LRU order (by last touch): keys / values [2][n] each.
 hipError_t latency_carry_order(const LatEvent *carry, size_t n, unsigned long long *keys, uint32_t *vals,
                                void *tmp, size_t tmp_bytes, hipStream_t st);
-hipError_t launch_latency_back(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
-                               uint32_t enabled, hipStream_t st);
+// The capacity check (sort by key hash, entry lives, live-count scan and its maximum into
+// *a.max_live), then -- the host having read that maximum -- the parallel walk's effects
+// (limit not reached) or the host's sequential replay (gpuagg_runtime.cpp
+// lat_serial_host), then the state update.
+hipError_t launch_latency_check(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
+                                uint32_t enabled, hipStream_t st);
+hipError_t launch_latency_walk(const LatArgs &a, size_t n_events, uint32_t enabled, hipStream_t st);
+hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, hipStream_t st);
 
 // Sketch pass (count-min by window partition + HLL), after the metric kernels.
 struct SketchArgs {

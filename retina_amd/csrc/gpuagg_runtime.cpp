@@ -246,7 +246,7 @@ struct gpuagg_result {
   // gpuagg_result_render_text's output, rendered once (callers size, then fill)
   mutable std::unique_ptr<char[]> text;  // text_len bytes + NUL, text_cap allocated
   mutable size_t text_len = 0, text_cap = 0;
-  mutable bool text_done = false;
+  mutable std::once_flag text_once;  // render_text runs once, whichever reader comes first
 };
 
 struct gpuagg_ctx {
@@ -350,11 +350,6 @@ struct gpuagg_ctx {
   // capacity (ttlcache LIMIT): live-count check buffers and the sequential pass's ttlcache
   int32_t *d_lat_delta = nullptr;   // [2][lat_ev_alloc + 1]: entry lives, live counts
   int32_t *d_lat_max_live = nullptr;
-  LatEntry *d_lat_pool = nullptr;   // [limit]
-  uint32_t *d_lat_table = nullptr;  // [lat_table_mask + 1]
-  uint32_t lat_table_mask = 0;
-  uint32_t *d_lat_free = nullptr;   // [limit]
-  LatTouch *d_lat_queue = nullptr;  // [lat_ev_alloc]
   unsigned long long *d_lat_okeys = nullptr;  // carried entries' LRU sort: [2][lat_carry_alloc]
   uint32_t *d_lat_ovals = nullptr;
   size_t lat_order_alloc = 0;
@@ -1134,6 +1129,158 @@ int lat_reset(gpuagg_ctx *c, bool full) {
   return GPUAGG_OK;
 }
 
+// The batch in event order when the capacity binds: the ttlcache itself (every event
+// depends on the live set the earlier ones left), replayed on the host, where the item
+// table (2x LIMIT slots) and the pool stay in cache -- on the GPU this was one thread
+// chasing global memory, 1.7 s per 2^20-record batch (profiles/round5/r5l_lat_serial.jsonl).
+// Items live in a pool, a linear-probing table maps keys to them (backward-shift
+// deletion), and a queue of touches in order is the LRU list (a record is stale once its
+// item is touched again or freed): its front valid item is the least recently touched,
+// which is also the first to expire.  Reads the events (carried entries at [0, pend), in
+// LRU order by a.carry_order) and the state words, writes back the state and the
+// carry-out (lat_finish_kernel then advances the clock and the pending count).
+int lat_serial_host(gpuagg_ctx *c, const LatArgs &a, uint64_t n, uint64_t pend) {
+  std::vector<LatEvent> ev(n);
+  std::vector<uint32_t> order(pend);
+  unsigned long long st[kLatStateWords];
+  HIPCHK(c, x_copy_async(c, ev.data(), a.ev, n * sizeof(LatEvent), hipMemcpyDeviceToHost, c->stream));
+  if (pend)
+    HIPCHK(c, x_copy_async(c, order.data(), a.carry_order, pend * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, x_copy_async(c, st, a.state, sizeof st, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, x_sync(c, c->stream));
+  const uint32_t enabled = c->lat_enabled;
+  uint32_t tsize = 1024;
+  while (tsize < 2 * a.limit) tsize <<= 1;
+  const uint32_t mask = tsize - 1;
+  std::vector<uint32_t> table(tsize, 0u);  // pool index + 1 (0: empty)
+  std::vector<LatEntry> pool;
+  pool.reserve(std::min<uint64_t>(a.limit, n));
+  std::vector<uint32_t> free_idx;
+  std::vector<LatTouch> queue;
+  queue.reserve(n);
+  size_t qh = 0;
+  uint64_t live = 0;
+  auto home = [&](uint64_t k0, uint64_t k1) { return (uint32_t)fmix64(k0 ^ fmix64(k1 ^ 0x6A09E667F3BCC909ULL)) & mask; };
+  auto find = [&](uint64_t k0, uint64_t k1) -> int64_t {  // table slot, or -1
+    for (uint32_t s = home(k0, k1);; s = (s + 1) & mask) {
+      const uint32_t v = table[s];
+      if (!v) return -1;
+      const LatEntry &x = pool[v - 1];
+      if (x.k0 == k0 && x.k1 == k1) return s;
+    }
+  };
+  auto erase = [&](uint32_t s) {  // backward-shift deletion, frees the item
+    const uint32_t idx = table[s] - 1;
+    pool[idx].seq = ~0ULL;
+    free_idx.push_back(idx);
+    for (uint32_t t = (s + 1) & mask;; t = (t + 1) & mask) {
+      const uint32_t v = table[t];
+      if (!v) break;
+      const uint32_t hm = home(pool[v - 1].k0, pool[v - 1].k1);
+      // the item at t may move to s unless its home lies cyclically in (s, t]
+      const bool stay = s <= t ? (hm > s && hm <= t) : (hm > s || hm <= t);
+      if (!stay) {
+        table[s] = v;
+        s = t;
+      }
+    }
+    table[s] = 0u;
+    --live;
+  };
+  auto insert = [&](const LatEntry &x) {
+    uint32_t idx;
+    if (!free_idx.empty()) {
+      idx = free_idx.back();
+      free_idx.pop_back();
+      pool[idx] = x;
+    } else {
+      idx = (uint32_t)pool.size();
+      pool.push_back(x);
+    }
+    uint32_t s = home(x.k0, x.k1);
+    while (table[s]) s = (s + 1) & mask;
+    table[s] = idx + 1;
+    queue.push_back(LatTouch{x.seq, idx, 0u});
+    ++live;
+  };
+  auto front = [&]() -> uint32_t {  // the front valid item (skipping stale records), or ~0
+    while (qh < queue.size()) {
+      const LatTouch r = queue[qh];
+      if (pool[r.idx].seq == r.seq) return r.idx;
+      ++qh;
+    }
+    return ~0u;
+  };
+  auto bucket = [](int64_t v) -> uint32_t { return v <= 0 ? 0u : v >= 5 ? 10u : (uint32_t)(2 * v); };
+  for (uint64_t k = 0; k < pend; ++k) {  // carried items, least recently touched first
+    const LatEvent &e = ev[order[k]];
+    insert(LatEntry{e.k0, e.k1, e.clock, e.seq, e.nanos, (e.bits >> 2) & 1u});
+  }
+  for (uint64_t pos = pend; pos < n; ++pos) {
+    const LatEvent e = ev[pos];
+    for (uint32_t f = front(); f != ~0u && e.clock > pool[f].expires; f = front()) {
+      erase((uint32_t)find(pool[f].k0, pool[f].k1));  // expired before this record
+      ++qh;
+      if (enabled & 4u) st[kLatNoResponse] += 1;
+    }
+    const int64_t s = find(e.k0, e.k1);
+    if ((e.bits & 3u) == 1u) {  // request
+      if (s >= 0) {  // Get hit: touched
+        const uint32_t idx = table[s] - 1;
+        pool[idx].expires = e.clock + kLatTtlNs;
+        pool[idx].seq = e.seq;
+        queue.push_back(LatTouch{e.seq, idx, 0u});
+        continue;
+      }
+      if (live >= a.limit) {  // Set at capacity: the LRU back goes, uncounted
+        const uint32_t f = front();
+        erase((uint32_t)find(pool[f].k0, pool[f].k1));
+        ++qh;
+        st[kLatCapEvictions] += 1;
+      }
+      insert(LatEntry{e.k0, e.k1, e.clock + kLatTtlNs, e.seq, e.nanos, (e.bits >> 2) & 1u});
+    } else if (s >= 0) {  // reply: latency, then Delete
+      const LatEntry x = pool[table[s] - 1];
+      const int64_t d = (int64_t)e.nanos - (int64_t)x.nanos;
+      const int64_t ad = d < 0 ? -d : d;
+      const int64_t lat = (d < 0 ? -1 : 1) * ((ad + 500000) / 1000000);  // math.Round
+      const uint32_t bk = bucket(lat);
+      if (enabled & 1u) {
+        st[kLatHist + bk] += 1;
+        st[kLatHist + 11] += 1;
+        st[kLatHist + 12] += (unsigned long long)lat;
+      }
+      if ((enabled & 2u) && x.syn && ((e.bits >> 2) & 1u) && ((e.bits >> 3) & 1u)) {
+        st[kLatHandshake + bk] += 1;
+        st[kLatHandshake + 11] += 1;
+        st[kLatHandshake + 12] += (unsigned long long)lat;
+      }
+      erase((uint32_t)s);
+    }
+  }
+  // batch end: expired items count, the rest carry over in LRU order
+  const unsigned long long clk_end = st[kLatClockEnd];
+  std::vector<LatEvent> out;
+  for (uint32_t f = front(); f != ~0u; f = front()) {
+    const LatEntry x = pool[f];
+    if (clk_end > x.expires) {
+      if (enabled & 4u) st[kLatNoResponse] += 1;
+    } else {
+      out.push_back(LatEvent{x.k0, x.k1, x.expires, x.seq, x.nanos, 3u | (x.syn ? 4u : 0u)});
+    }
+    pool[f].seq = ~0ULL;
+    ++qh;
+  }
+  st[kLatCarryOut] = out.size();
+  st[kLatCapBatches] += 1;
+  if (!out.empty())
+    HIPCHK(c, x_copy_async(c, a.carry_out, out.data(), out.size() * sizeof(LatEvent), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, x_copy_async(c, a.state, st, sizeof st, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, x_sync(c, c->stream));  // the host buffers go out of scope
+  return GPUAGG_OK;
+}
+
 // The TTL join over one batch (see gpuagg_latency.hip); waits for the event count.
 int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   int rc;
@@ -1197,32 +1344,17 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     dev_free(c, c->d_lat_hash);
     dev_free(c, c->d_lat_idx);
     dev_free(c, c->d_lat_delta);
-    dev_free(c, c->d_lat_queue);
     c->lat_ev_alloc = 0;
     if ((rc = dev_alloc(c, &c->d_lat_ev, cap)) || (rc = dev_alloc(c, &c->d_lat_hash, 2 * cap)) ||
-        (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)) || (rc = dev_alloc(c, &c->d_lat_delta, 2 * (cap + 1))) ||
-        (rc = dev_alloc(c, &c->d_lat_queue, cap)))
+        (rc = dev_alloc(c, &c->d_lat_idx, 2 * cap)) || (rc = dev_alloc(c, &c->d_lat_delta, 2 * (cap + 1))))
       return rc;
     c->lat_ev_alloc = cap;
   }
-  // the sequential pass's ttlcache: `limit` items, a table at most half full
   a.limit = c->cfg.latency_limit ? c->cfg.latency_limit : kLatLimit;
-  if (!c->d_lat_pool) {
-    uint32_t tsize = 1024;
-    while (tsize < 2 * a.limit) tsize <<= 1;
-    if ((rc = dev_alloc(c, &c->d_lat_pool, a.limit)) || (rc = dev_alloc(c, &c->d_lat_table, tsize)) ||
-        (rc = dev_alloc(c, &c->d_lat_free, a.limit)) || (rc = dev_alloc(c, &c->d_lat_max_live, 1)))
-      return rc;
-    c->lat_table_mask = tsize - 1;
-  }
+  if (!c->d_lat_max_live && (rc = dev_alloc(c, &c->d_lat_max_live, 1))) return rc;
   a.delta = c->d_lat_delta;
   a.live = c->d_lat_delta + c->lat_ev_alloc + 1;
   a.max_live = c->d_lat_max_live;
-  a.pool = c->d_lat_pool;
-  a.table = c->d_lat_table;
-  a.table_mask = c->lat_table_mask;
-  a.free_idx = c->d_lat_free;
-  a.queue = c->d_lat_queue;
   a.ev = c->d_lat_ev;
   a.hash_in = c->d_lat_hash;
   a.hash_out = c->d_lat_hash + c->lat_ev_alloc;
@@ -1274,7 +1406,18 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
                                   c->stream));
     a.carry_order = c->d_lat_ovals + pend;
   }
-  HIPCHK(c, launch_latency_back(a, ne, c->d_lat_tmp, c->lat_tmp_alloc, c->lat_enabled, c->stream));
+  HIPCHK(c, launch_latency_check(a, ne, c->d_lat_tmp, c->lat_tmp_alloc, c->lat_enabled, c->stream));
+  int32_t max_live = 0;
+  if (ne) {  // the one decision the host takes: does the capacity bind in this batch?
+    HIPCHK(c, x_copy_async(c, &max_live, c->d_lat_max_live, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, x_sync(c, c->stream));
+  }
+  if ((uint64_t)max_live > a.limit) {
+    if ((rc = lat_serial_host(c, a, ne, pend))) return rc;
+  } else {
+    HIPCHK(c, launch_latency_walk(a, ne, c->lat_enabled, c->stream));
+  }
+  HIPCHK(c, launch_latency_finish(a, ne, c->stream));
   c->lat_carry_cur ^= 1;
   c->lat_carry_bound = ne;
   return GPUAGG_OK;
@@ -1807,11 +1950,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c, c->d_lat_hash);
   dev_free(c, c->d_lat_idx);
   dev_free(c, c->d_lat_delta);
-  dev_free(c, c->d_lat_queue);
   dev_free(c, c->d_lat_max_live);
-  dev_free(c, c->d_lat_pool);
-  dev_free(c, c->d_lat_table);
-  dev_free(c, c->d_lat_free);
   dev_free(c, c->d_lat_okeys);
   dev_free(c, c->d_lat_ovals);
   dev_free(c, c->d_lat_carry[0]);
@@ -3901,13 +4040,12 @@ void render_text(const gpuagg_result *r) {
       }
     });
   }
-  r->text_done = true;
 }
 }  // namespace
 
 int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, size_t *len) {
   if (!r || !len) return GPUAGG_EINVAL;
-  if (!r->text_done) render_text(r);
+  std::call_once(r->text_once, [r] { render_text(r); });  // two /metrics readers may race here
   *len = r->text_len;
   if (!buf) return GPUAGG_OK;
   if (cap < r->text_len + 1) return GPUAGG_ECAPACITY;
@@ -3917,7 +4055,7 @@ int gpuagg_result_render_text(const gpuagg_result *r, char *buf, size_t cap, siz
 
 int gpuagg_result_text(const gpuagg_result *r, const char **text, size_t *len) {
   if (!r || !text || !len) return GPUAGG_EINVAL;
-  if (!r->text_done) render_text(r);
+  std::call_once(r->text_once, [r] { render_text(r); });
   *text = r->text.get();
   *len = r->text_len;
   return GPUAGG_OK;
@@ -4162,7 +4300,10 @@ int merge_rccl(gpuagg_ctx *const *ctxs, size_t n, const std::vector<int> &devs) 
     reduce(ci->d_dense_byt, c0->dense_len, ncclUint64, ncclSum);
     reduce(ci->d_cms, c0->cms_len, ncclUint32, ncclSum);
     reduce(ci->d_hll, c0->hll_len, ncclUint8, ncclMax);
-    if (lat) reduce(ci->d_lat + kLatHist, kLatStateWords - kLatHist, ncclUint64, ncclSum);
+    if (lat) {
+      reduce(ci->d_lat + kLatHist, kLatPeakLive - kLatHist, ncclUint64, ncclSum);
+      reduce(ci->d_lat + kLatPeakLive, kLatStateWords - kLatPeakLive, ncclUint64, ncclMax);
+    }
     if (i > 0 && m[i] && r == ncclSuccess)
       r = ncclSend(ci->d_export, m[i] * kSparseEntryWords, ncclUint64, 0, comm[i], ci->stream);
   }
@@ -4332,7 +4473,7 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
       HIPCHK(ci, x_copy(ci, ai, ci->d_lat, sizeof ai, hipMemcpyDeviceToHost));
       if ((rc = bind(c0))) break;
       HIPCHK(c0, x_copy(c0, a0, c0->d_lat, sizeof a0, hipMemcpyDeviceToHost));
-      for (uint32_t w = kLatHist; w < kLatStateWords; ++w) a0[w] += ai[w];
+      for (uint32_t w = kLatHist; w < kLatStateWords; ++w) a0[w] = w < kLatPeakLive ? a0[w] + ai[w] : std::max(a0[w], ai[w]);
       HIPCHK(c0, x_copy(c0, c0->d_lat, a0, sizeof a0, hipMemcpyHostToDevice));
     }
     if ((rc = gpuagg_reset(ci))) break;

@@ -21,6 +21,8 @@ from typing import List, Optional
 
 import numpy as np
 
+from . import _abi
+
 _U64 = np.uint64
 _M1, _M2 = _U64(0xff51afd7ed558ccd), _U64(0xc4ceb9fe1a85ec53)
 SHARD_SEED = _U64(0x1F2E3D4C5B6A7988)
@@ -157,8 +159,10 @@ def merge_engine(engine, group=None, dst: int = 0) -> None:
         reduce(st.hll, st.hll_len, "|u1", dist.ReduceOp.MAX)
     # node-apiserver latency histograms / counts / sums and no_response: summed like the
     # counters (the pending requests stay on their shard: each shard runs its own clock)
-    if st.latency_len:
-        reduce(st.latency, st.latency_len, "<i8", dist.ReduceOp.SUM)
+    if st.latency_len:  # words [0, LAT_SUM_WORDS) summed, the rest (peak live) max-merged
+        reduce(st.latency, _abi.LAT_SUM_WORDS, "<i8", dist.ReduceOp.SUM)
+        reduce(st.latency + 8 * _abi.LAT_SUM_WORDS, st.latency_len - _abi.LAT_SUM_WORDS, "<i8",
+               dist.ReduceOp.MAX)
     # sparse table: every rank's compact entries gathered on dst and inserted-and-added
     cap = int(st.sparse_len)
     local = torch.empty((max(cap, 1), 5), dtype=torch.int64, device=device)

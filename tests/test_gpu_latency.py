@@ -247,3 +247,37 @@ def test_touch_without_capacity(gpu_device):
         g.close()
     assert {k: st[k] for k in want} == want
     assert st["capacity_batches"] == 0
+
+
+@pytest.mark.parametrize("cpu", [False, True], ids=["gpu", "cpu-backend"])
+def test_merge_capacity_counters(gpu_device, cpu):
+    """gpuagg_merge combines the capacity diagnostics the way a single context would report
+    them: capacity_evictions and capacity_batches summed, peak_live the max over
+    the contexts; the merged-from context restarts them with its histograms."""
+    from retina_amd import _abi
+    from retina_amd import dist as D
+    from retina_amd import GpuAgg
+    pods = W.make_pods(100, seed=51)
+    recs = W.gen_latency_records(900, pods, API, seed=52, background=500)
+    kw = dict(latency_limit=20)
+    if cpu:
+        kw["flags"] = _abi.FLAG_CPU_BACKEND
+    parts = [make_engine(pods, SPEC, False, gpu_device, **kw) for _ in range(2)]
+    try:
+        for r, g in enumerate(parts):
+            g.set_apiserver_ips(API)
+            sh = D.shard_records(recs, 2, r)
+            hb = g.alloc_batch(len(sh.src_ip))
+            hb.fill(sh)
+            g.submit(hb, len(sh.src_ip))
+        before = [g.latency_state() for g in parts]
+        assert all(b["capacity_batches"] > 0 and b["capacity_evictions"] > 0 for b in before)
+        parts[0].merge_from(parts[1:])
+        after, rest = parts[0].latency_state(), parts[1].latency_state()
+    finally:
+        for g in parts:
+            g.close()
+    assert after["capacity_evictions"] == sum(b["capacity_evictions"] for b in before)
+    assert after["capacity_batches"] == sum(b["capacity_batches"] for b in before)
+    assert after["peak_live"] == max(b["peak_live"] for b in before)
+    assert rest["capacity_evictions"] == rest["capacity_batches"] == rest["peak_live"] == 0
