@@ -50,6 +50,10 @@ def run(name, spec, pods, cols, n, remote=False, steps=5, flags=0, api_ips=None,
     dc = GpuAgg.device_columns(*cols)
     g.submit_device(dc, n)
     g.sync()
+    t_settle = time.perf_counter()  # clocks settle (profiles/round5/r5k_ramp.jsonl)
+    while time.perf_counter() - t_settle < float(os.environ.get("ABLATE_SETTLE_S", "0.04")):
+        g.submit_device(dc, n)
+        g.sync()
     g.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(steps):
