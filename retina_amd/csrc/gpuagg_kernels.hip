@@ -1100,26 +1100,28 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
     }
     atomicAdd(s.dropped, 1ULL);
   };
-  // Lists are short (tens of keys), so a lane owns a whole list: a wave loads 64 counts
-  // at once and then 8 keys per lane per round trip (cap is even: 16-byte pairs).
-  const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
-  for (uint32_t l0 = (threadIdx.x >> 6) * 64u; l0 < n_lists; l0 += nwaves * 64u) {
-    const uint32_t l = l0 + lane;
-    const uint32_t cnt = l < n_lists ? counts[(size_t)l * nwin + w] : 0u;
-    const ulonglong2 *e2 = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap);
-    uint32_t mx = cnt;
+  // lpl lanes per list (a power of two <= 64: the workgroup's lanes spread over the
+  // lists), each taking every lpl-th key with 8 loads in flight before its inserts.  A
+  // lane used to own a whole list: with one list per aggregation workgroup (256) only 4 of
+  // the 16 waves worked, and after the deferred launches a list holds hundreds of keys
+  // inserted one LDS round trip after another (C5: the fold grew by ~0.07 ms per launch).
+  uint32_t lpl = 1;
+  while (lpl < 64 && lpl * 2 * n_lists <= blockDim.x) lpl *= 2;
+  const uint32_t lists_per_round = blockDim.x / lpl, sub = threadIdx.x & (lpl - 1);
+  for (uint32_t l0 = 0; l0 < n_lists; l0 += lists_per_round) {
+    const uint32_t l = l0 + threadIdx.x / lpl;
+    if (l >= n_lists) continue;
+    const uint32_t cnt = counts[(size_t)l * nwin + w];
+    const unsigned long long *e = lists + ((size_t)l * nwin + w) * cap;
+    uint32_t k = sub;
+    for (; k + 7 * lpl < cnt; k += 8 * lpl) {
+      unsigned long long v[8];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    for (uint32_t k = 0; k < mx; k += 8) {
-      ulonglong2 v[4];
+      for (int q = 0; q < 8; ++q) v[q] = e[k + q * lpl];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = k + 2 * q < cnt ? e2[k / 2 + q] : make_ulonglong2(0ULL, 0ULL);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (k + 2 * q < cnt) insert(v[q].x);
-        if (k + 2 * q + 1 < cnt) insert(v[q].y);
-      }
+      for (int q = 0; q < 8; ++q) insert(v[q]);
     }
+    for (; k < cnt; k += lpl) insert(e[k]);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) g[i] = ((const ulonglong2 *)seg)[i];
