@@ -179,9 +179,10 @@ def pmc_traffic(cfg_name: str, kernel: str, build_id: str):
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 
 
-# The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go: batchCapacity = 1 << 20
-# records per pinned batch, submitted when full or every flushInterval = 100 ms).
-GO_BATCH = 1 << 20
+# The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go: batchCapacity = 1 << 22
+# records per pinned batch / feed staging, submitted when full or every flushInterval =
+# 100 ms; 2^20 until round 5).
+GO_BATCH = 1 << 22
 
 
 def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
@@ -208,11 +209,11 @@ def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
             "note": "pinned host batches through gpuagg_submit (PCIe H2D included; not `value`)"}
 
 
-def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 48, batch: int = GO_BATCH):
+def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 12, batch: int = GO_BATCH):
     """The Go plugin's raw path (gpuagg_linux.go Start -> submitRaw): raw 72-byte
     packetparser samples (conntrack.c:34-49) handed to the library feed in 2^16-sample
     pieces (rawPiece) -- gpuagg_raw_feed_put: the feed's host threads shard by the 5-tuple
-    and write into one of the device's two pinned 2^20-record stagings; a full staging's
+    and write into one of the device's two pinned GO_BATCH-record stagings; a full staging's
     H2D DMA starts without a wait while the other fills -- then a flush and sync.
     `value`: the feed's defaults -- samples copied as they are (72 B per record over PCIe)
     and decoded on the GPU (GPUAGG_FEED_RAW_DMA), 4 feed threads; `modes` times both modes
@@ -226,8 +227,8 @@ def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 48, batch: int = 
     raw = W.gen_raw_packets(batch, pods, seed=seed)  # one Go batch of samples, resubmitted
     piece = 1 << 16
 
-    def run(engines, mode, threads, nb):
-        feed = RawFeed(engines, _abi.RAW_PACKET, capacity=batch, threads=threads, mode=mode)
+    def run(engines, mode, threads, nb, cap=batch):
+        feed = RawFeed(engines, _abi.RAW_PACKET, capacity=cap, threads=threads, mode=mode)
         try:
             for a in range(0, batch, piece):  # warm-up: stagings, device buffers, pool threads
                 feed.put(raw[a * 72:(a + piece) * 72])
@@ -256,7 +257,8 @@ def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 48, batch: int = 
         for e in extra:
             e.reconcile(spec)
             e.load_endpoints(pods.endpoints)
-        shard8 = {name: {str(t): run([g] + extra, mode, t, batches // 2) for t in (4, 8, 16)}
+        # (stagings of batch / 4 records here: 8 contexts x 2 stagings of 72-byte samples)
+        shard8 = {name: {str(t): run([g] + extra, mode, t, batches // 2, batch // 4) for t in (4, 8, 16)}
                   for name, mode in (("host_decode", _abi.FEED_HOST_DECODE), ("raw_dma", _abi.FEED_RAW_DMA))}
     finally:
         for e in extra:
@@ -273,7 +275,7 @@ def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 48, batch: int = 
             "piece_records": piece, "record_bytes": 72, "feed_threads": 4, "feed_mode": "raw_dma", "modes": modes,
             "best": {"mode": best[0], "threads": int(best[1]), "value": modes[best[0]][best[1]]},
             "shard8": shard8, "shard_rate_8_devices": shard_rate,
-            "note": "raw packetparser samples through gpuagg_raw_feed_put in 2^16-sample pieces, 2 pinned 2^20-record "
+            "note": "raw packetparser samples through gpuagg_raw_feed_put in 2^16-sample pieces, 2 pinned 2^22-record "
                     "stagings per context, async H2D -- the Go plugin's real raw path; PCIe included, not `value`. "
                     "value = the feed's defaults (raw_dma, 4 threads); modes = records/s by mode and feed threads; shard8 = "
                     "one feed over 8 contexts of this GPU; shard_rate_8_devices = gpuagg_shard_raw (threaded) samples/s"}
@@ -433,7 +435,7 @@ def main():
         g.dns_intern(p.rcode, p.qtypes, p.query, p.ips, p.num_answers)
     dcols = GpuAgg.device_columns(*cols)
 
-    if args.production_only:  # diagnostic (rocprof of the 2^20-record launches)
+    if args.production_only:  # diagnostic (rocprof of the GO_BATCH-record launches)
         print(json.dumps({"production": production_geometry(g, cols, n, bpr, 0.0)}), flush=True)
         g.close()
         return

@@ -59,7 +59,7 @@ import (
 
 const (
 	name          = "gpuagg"
-	batchCapacity = 1 << 20
+	batchCapacity = 1 << 22 // records per pinned batch / feed staging: a launch's fixed cost (LDS image fill, staged bins) over 4M records
 	rawPiece      = 1 << 16 // samples / records buffered in Go before each hand-over to Start
 	flushInterval = 100 * time.Millisecond
 	scrapeEpoch   = 5 * time.Second

@@ -1425,6 +1425,9 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 
 // Launches whose list folds may wait for one fold_pending (see Pending).
 constexpr uint64_t kDeferLaunches = 64;
+// Spill-only plans defer their folds at launches of at most this many records per workgroup
+// (the Go plugin's 2^22-record batches: 2^14; full-size launches fold per batch, see launch()).
+constexpr uint64_t kSmallLaunchChunk = 1ull << 16;
 // Default device memory for the wide-key segment lists of one ctx (32-byte entries;
 // gpuagg_config.wide_list_mib overrides it): 32 GiB (1024 entries per workgroup and segment at 2^24
 // slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
@@ -1688,7 +1691,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     // records): there the spill fold's fixed pass over the windows cost more than the
     // tier-1 kernel itself; at full-size launches appending past earlier launches' entries
     // measured ~2 % slower in the tier-1 kernel (profiles/round2/r4f_*), so they fold per batch.
-    const bool small_spill = c->dense_len > a.lds_bins && a.chunk * kDeferLaunches <= kMaxRecordsPerBlock;
+    const bool small_spill = c->dense_len > a.lds_bins && a.chunk <= kSmallLaunchChunk;
     const bool lists = sp_lists || small_spill;
     const bool defer = c->defer_folds && lists;
     // Wide lists (192-bit keys) are folded when the device says so: every launch's fold
