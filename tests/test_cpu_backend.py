@@ -379,3 +379,38 @@ def test_scrape_buffers_reused_across_results():
         g.close()
     assert text(d) == want  # the context is gone; the result's buffers are its own
     g.lib.gpuagg_result_free(d)
+
+
+def test_result_text_concurrent_readers():
+    """Two /metrics handlers reading one result: gpuagg_result_text renders once
+    (std::call_once) and both readers get the same buffer and length."""
+    import ctypes as C
+    import threading
+    pods = W.make_pods(300, seed=71)
+    sp = [{"metric_name": m, "source_labels": ["namespace", "podname"]}
+          for m in ("forward_count", "forward_bytes", "drop_count", "drop_bytes")]
+    recs = W.gen_records(50_000, pods, seed=72, drop_frac=0.2)
+    g = make_engine(pods, sp, False, flags=128)
+    try:
+        hb = g.alloc_batch(len(recs.src_ip))
+        hb.fill(recs)
+        g.submit(hb, len(recs.src_ip))
+        for _ in range(5):
+            r = C.c_void_p()
+            assert g.lib.gpuagg_snapshot(g.h, C.byref(r)) == 0
+            out = []
+
+            def read():
+                p, n = C.c_void_p(), C.c_size_t()
+                assert g.lib.gpuagg_result_text(r, C.byref(p), C.byref(n)) == 0
+                out.append((p.value, n.value, C.string_at(p, n.value)))
+            th = [threading.Thread(target=read) for _ in range(4)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            g.lib.gpuagg_result_free(r)
+            assert len(out) == 4 and len({(a, b) for a, b, _ in out}) == 1 and len({t for _, _, t in out}) == 1
+            assert out[0][1] > 0
+    finally:
+        g.close()
