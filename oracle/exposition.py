@@ -7,7 +7,8 @@ forward.go:18-26,47-64, drops.go:18-23,42-60, tcpflags.go:18-24,43-51,
 tcpretrans.go:18-24,43-51 (GaugeVec) and dns.go:21-30,50-66 (CounterVec), namespace
 "networkobservability" (prometheusexporter.go:11).  The text layout is client_golang
 v1.21.1's (go.mod:8; not in this image, so the layout rules below are restated from its
-published text format 0.0.4 and are *parity unpinned* by reference tests): families
+published text format 0.0.4, and pinned by the scrape the reference's docs print,
+docs/06-Troubleshooting/basic-metrics.md:86-124 -> reference_kat.json exposition_sample): families
 sorted by name, "# HELP" (backslash and newline escaped) and "# TYPE" lines, a metric's
 label pairs sorted by label name, metrics of a family sorted by their label values,
 label values escaped (backslash, double quote, newline), sample values formatted as
@@ -56,13 +57,16 @@ def _esc(s: str, quote: bool) -> str:
     return s.replace('"', '\\"') if quote else s
 
 
-def render(series: Dict[Tuple[str, Tuple[Tuple[str, str], ...]], int]) -> str:
+def render(series: Dict[Tuple[str, Tuple[Tuple[str, str], ...]], int], families=None) -> str:
+    """families: {name: (type, help)}, default the advanced metrics' FAMILIES (the basic
+    registry's sample in tests/golden/reference_kat.json passes its own)."""
+    families = FAMILIES if families is None else families
     fams: Dict[str, list] = {}
     for (metric, labels), v in series.items():
         fams.setdefault(metric, []).append((tuple(sorted(labels, key=lambda p: p[0])), v))
     out = []
     for metric in sorted(fams):
-        typ, help_ = FAMILIES[metric]
+        typ, help_ = families[metric]
         out.append("# HELP %s %s\n# TYPE %s %s\n" % (metric, _esc(help_, False), metric, typ))
         for pairs, v in sorted(fams[metric], key=lambda e: [val for _, val in e[0]]):
             lab = ",".join('%s="%s"' % (k, _esc(val, True)) for k, val in pairs)

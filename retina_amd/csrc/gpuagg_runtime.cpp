@@ -1429,8 +1429,8 @@ constexpr uint64_t kDeferLaunches = 64;
 // (the Go plugin's 2^22-record batches: 2^14; full-size launches fold per batch, see launch()).
 constexpr uint64_t kSmallLaunchChunk = 1ull << 16;
 // Default device memory for the wide-key segment lists of one ctx (32-byte entries;
-// gpuagg_config.wide_list_mib overrides it): 32 GiB (1024 entries per workgroup and segment at 2^24
-// slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
+// gpuagg_config.wide_list_mib overrides it): 32 GiB (512 entries per workgroup and segment at 2^24
+// slots = 8192 segments), at most 1/8 of the device.  A list that fills sends its updates to memory-side
 // atomics, and under C4's skew 8 GiB (256 entries) overflowed within one launch: 1.74 ->
 // 1.32 ms per 100M records (profiles/round3/exp/v2_wide_list_bytes.jsonl).
 constexpr uint64_t kWideListBytes = 32ull << 30;

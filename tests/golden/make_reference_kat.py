@@ -318,6 +318,92 @@ kat["reconcile"] = [
      "reference_error": False, "expect_no_calls": True},
 ]
 
+# docs/06-Troubleshooting/basic-metrics.md:86-124: a scrape of the agent's /metrics (the
+# basic registry: GaugeVecs through the same client_golang text encoder as the advanced
+# registry), as printed by the reference's docs -- families, Help strings, label pairs
+# and float64 values as data, and the exact text they render to
+_G = "gauge"
+kat["exposition_sample"] = {
+    "src": "docs/06-Troubleshooting/basic-metrics.md:86-124",
+    "families": {
+        "retina_forward_bytes": [_G, "Total forwarded bytes"],
+        "retina_forward_count": [_G, "Total forwarded packets"],
+        "retina_interface_stats": [_G, "Interface Statistics"],
+        "retina_ip_connection_stats": [_G, "IP connections Statistics"],
+        "retina_tcp_connection_remote": [_G, "number of active TCP connections by remote address"],
+        "retina_tcp_connection_stats": [_G, "TCP connections Statistics"],
+        "retina_tcp_state": [_G, "number of active TCP connections by state"],
+        "retina_udp_connection_stats": [_G, "UDP connections Statistics"],
+    },
+    # listed out of order on purpose: the encoder sorts families, metrics and label pairs
+    "series": [
+        ["retina_tcp_state", {"state": "TIME_WAIT"}, 89],
+        ["retina_forward_count", {"direction": "ingress"}, 37254085],
+        ["retina_forward_bytes", {"direction": "ingress"}, 23619602627],
+        ["retina_forward_bytes", {"direction": "egress"}, 19064666952],
+        ["retina_forward_count", {"direction": "egress"}, 43139614],
+        ["retina_interface_stats", {"statistic_name": "vf_rx_packets", "interface_name": "eth0"}, 12948929],
+        ["retina_interface_stats", {"statistic_name": "vf_rx_bytes", "interface_name": "eth0"}, 12679472174],
+        ["retina_ip_connection_stats", {"statistic_name": "OutOctets"}, 27768258214],
+        ["retina_ip_connection_stats", {"statistic_name": "InECT0Pkts"}, 34713],
+        ["retina_ip_connection_stats", {"statistic_name": "InOctets"}, 16718610902],
+        ["retina_ip_connection_stats", {"statistic_name": "InNoECTPkts"}, 38893357],
+        ["retina_tcp_connection_remote", {"port": "7070", "address": "10.224.0.105"}, 1],
+        ["retina_tcp_connection_remote", {"port": "0", "address": "0.0.0.0"}, 8],
+        ["retina_tcp_connection_remote", {"port": "443", "address": "10.0.0.1"}, 1],
+        ["retina_tcp_connection_stats", {"statistic_name": "DelayedACKLocked"}, 107],
+        ["retina_tcp_state", {"state": "SYN_SENT"}, 1],
+        ["retina_tcp_state", {"state": "CLOSE_WAIT"}, 1],
+        ["retina_tcp_state", {"state": "LISTEN"}, 8],
+        ["retina_tcp_state", {"state": "ESTABLISHED"}, 16],
+        ["retina_tcp_state", {"state": "FIN_WAIT2"}, 1],
+        ["retina_tcp_state", {"state": "FIN_WAIT1"}, 1],
+        ["retina_tcp_state", {"state": "LAST_ACK"}, 1],
+        ["retina_udp_connection_stats", {"statistic_name": "ACTIVE"}, 5],
+    ],
+    "text": [
+        '# HELP retina_forward_bytes Total forwarded bytes',
+        '# TYPE retina_forward_bytes gauge',
+        'retina_forward_bytes{direction="egress"} 1.9064666952e+10',
+        'retina_forward_bytes{direction="ingress"} 2.3619602627e+10',
+        '# HELP retina_forward_count Total forwarded packets',
+        '# TYPE retina_forward_count gauge',
+        'retina_forward_count{direction="egress"} 4.3139614e+07',
+        'retina_forward_count{direction="ingress"} 3.7254085e+07',
+        '# HELP retina_interface_stats Interface Statistics',
+        '# TYPE retina_interface_stats gauge',
+        'retina_interface_stats{interface_name="eth0",statistic_name="vf_rx_bytes"} 1.2679472174e+10',
+        'retina_interface_stats{interface_name="eth0",statistic_name="vf_rx_packets"} 1.2948929e+07',
+        '# HELP retina_ip_connection_stats IP connections Statistics',
+        '# TYPE retina_ip_connection_stats gauge',
+        'retina_ip_connection_stats{statistic_name="InECT0Pkts"} 34713',
+        'retina_ip_connection_stats{statistic_name="InNoECTPkts"} 3.8893357e+07',
+        'retina_ip_connection_stats{statistic_name="InOctets"} 1.6718610902e+10',
+        'retina_ip_connection_stats{statistic_name="OutOctets"} 2.7768258214e+10',
+        '# HELP retina_tcp_connection_remote number of active TCP connections by remote address',
+        '# TYPE retina_tcp_connection_remote gauge',
+        'retina_tcp_connection_remote{address="0.0.0.0",port="0"} 8',
+        'retina_tcp_connection_remote{address="10.0.0.1",port="443"} 1',
+        'retina_tcp_connection_remote{address="10.224.0.105",port="7070"} 1',
+        '# HELP retina_tcp_connection_stats TCP connections Statistics',
+        '# TYPE retina_tcp_connection_stats gauge',
+        'retina_tcp_connection_stats{statistic_name="DelayedACKLocked"} 107',
+        '# HELP retina_tcp_state number of active TCP connections by state',
+        '# TYPE retina_tcp_state gauge',
+        'retina_tcp_state{state="CLOSE_WAIT"} 1',
+        'retina_tcp_state{state="ESTABLISHED"} 16',
+        'retina_tcp_state{state="FIN_WAIT1"} 1',
+        'retina_tcp_state{state="FIN_WAIT2"} 1',
+        'retina_tcp_state{state="LAST_ACK"} 1',
+        'retina_tcp_state{state="LISTEN"} 8',
+        'retina_tcp_state{state="SYN_SENT"} 1',
+        'retina_tcp_state{state="TIME_WAIT"} 89',
+        '# HELP retina_udp_connection_stats UDP connections Statistics',
+        '# TYPE retina_udp_connection_stats gauge',
+        'retina_udp_connection_stats{statistic_name="ACTIVE"} 5',
+    ],
+}
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kat.json")
     with open(out, "w") as f:

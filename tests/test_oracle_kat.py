@@ -226,3 +226,15 @@ def test_reconcile_transitions(case):
         vecs = {n: m.registry[n].vec for n in m.registry}
         for n, v in vecs.items():  # Init creates a vector only for the exact *_count / *_bytes names
             assert (v is not None) == (n in ("drop_count", "drop_bytes", "forward_count", "forward_bytes")), n
+
+
+def test_exposition_layout_pinned_by_reference_sample():
+    """The text layout of oracle/exposition.py (which the engine's gpuagg_result_render_text
+    equals byte for byte, test_cpu_backend.py) against the scrape the reference's docs print
+    (docs/06-Troubleshooting/basic-metrics.md:86-124): family order, HELP / TYPE lines,
+    label-pair and metric order, Go FormatFloat('g', -1) values (1.9064666952e+10, 34713)."""
+    from oracle import exposition as X
+    ex = KAT["exposition_sample"]
+    fams = {k: (t, h) for k, (t, h) in ex["families"].items()}
+    series = {(m, tuple(lab.items())): v for m, lab, v in ex["series"]}
+    assert X.render(series, fams) == "".join(line + "\n" for line in ex["text"])
