@@ -22,8 +22,9 @@ matmerr/retina @ 2025-03-28 (paths relative to the reference root):
 Parity status: pinned by the reference's own known-answer tests (transcribed into
 ``tests/golden/reference_kat.json`` and checked by ``tests/test_oracle_kat.py``).
 Enum *names* that come from cilium's flow.proto (TrafficDirection) are not in the
-reference tree; they are hard-coded from cilium's published proto and marked
-"parity unpinned" where used.  Prometheus float64 accumulation is replaced by exact
+reference tree; they follow from the reference's Go identifiers (flow_utils.go:75-91:
+protoc-gen-go's <Enum>_<value name> constants, whose String() is the value name;
+reference_kat.json traffic_direction_identifiers).  Prometheus float64 accumulation is replaced by exact
 integer sums (identical while < 2**53).
 """
 
@@ -45,7 +46,8 @@ VERDICT_DROPPED = 2
 VERDICT_RETRANSMISSION = 15
 VERDICT_DNS = 16
 
-# cilium flow.TrafficDirection -- parity unpinned (cilium proto not in the reference tree).
+# cilium flow.TrafficDirection: names from the Go identifiers TrafficDirection_<name>
+# (pkg/utils/flow_utils.go:75-91); numbers are internal to this restatement.
 TRAFFIC_DIRECTION_NAMES = {0: "TRAFFIC_DIRECTION_UNKNOWN", 1: "INGRESS", 2: "EGRESS"}
 TD_UNKNOWN, TD_INGRESS, TD_EGRESS = 0, 1, 2
 

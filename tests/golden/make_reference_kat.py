@@ -404,6 +404,16 @@ kat["exposition_sample"] = {
     ],
 }
 
+# pkg/utils/flow_utils.go:75-91 and dns.go:222: the Go identifiers of cilium's
+# flow.TrafficDirection values.  protoc-gen-go names a constant <Enum>_<proto value name>,
+# and the enum's String() (the metrics' direction label, forward.go:116) returns that value
+# name, so the identifiers fix the label text
+kat["traffic_direction_identifiers"] = {
+    "src": "pkg/utils/flow_utils.go:75-91",
+    "identifiers": ["TrafficDirection_EGRESS", "TrafficDirection_INGRESS",
+                    "TrafficDirection_TRAFFIC_DIRECTION_UNKNOWN"],
+}
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kat.json")
     with open(out, "w") as f:

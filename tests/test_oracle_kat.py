@@ -238,3 +238,11 @@ def test_exposition_layout_pinned_by_reference_sample():
     fams = {k: (t, h) for k, (t, h) in ex["families"].items()}
     series = {(m, tuple(lab.items())): v for m, lab, v in ex["series"]}
     assert X.render(series, fams) == "".join(line + "\n" for line in ex["text"])
+
+
+def test_traffic_direction_names_from_reference_identifiers():
+    """The direction label values (TrafficDirection.String(), forward.go:116) are the proto
+    value names that the reference's Go identifiers carry (flow_utils.go:75-91):
+    protoc-gen-go names each constant <Enum>_<value name>."""
+    names = {i.split("_", 1)[1] for i in KAT["traffic_direction_identifiers"]["identifiers"]}
+    assert names == set(O.TRAFFIC_DIRECTION_NAMES.values())
