@@ -360,25 +360,16 @@ GA_HD uint64_t key_hash(uint64_t k0, uint64_t k1, uint64_t k2) {
 constexpr uint32_t kSparseMaxProbe = 1u << 16;
 // compact table segments: 2^13 (key, count) slots = 128 KiB, folded in LDS
 constexpr uint32_t kSparseSegLog2 = 13, kSparseMaxSegLists = 4096;
-// Wide-key table segments (192-bit keys): 2^11 slots of 40 bytes = 80 KiB of LDS, so two
-// fold workgroups share a CU and one's segment load / store overlaps the other's inserts.
-// Probing wraps inside the segment, so a segment is folded alone (sparse_fold_wide_kernel);
-// tables of up to 2^24 slots (8192 segments) take the per-segment lists, bigger ones probe
-// the whole table with memory-side atomics.
-constexpr uint32_t kWideSegLog2 = 11, kWideMaxSegLists = 8192, kWideMaxLog2 = kWideSegLog2 + 13;
-static_assert((1u << (kWideMaxLog2 - kWideSegLog2)) == kWideMaxSegLists, "lists cover the largest table");
+// Wide-key table segments (192-bit keys): 2^12 slots of 40 bytes = the 160 KiB LDS of one
+// fold workgroup.  Probing wraps inside the segment, so a segment is folded alone
+// (sparse_fold_wide_kernel); tables of up to 2^24 slots (4096 segments) take the
+// per-segment lists, bigger ones probe the whole table with memory-side atomics.
+constexpr uint32_t kWideSegLog2 = 12, kWideMaxLog2 = kWideSegLog2 + 12;
 // A wide list entry: k0 k1 k2 and home << 52 | count << 40 | bytes -- home = the key's slot
 // in its segment (key_hash & (2^kWideSegLog2 - 1)), so the fold does not hash the key again;
 // updates whose count or bytes do not fit the fields go to the table directly
 constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40, kWideHomeShift = 52;
-static_assert(kWideHomeShift + kWideSegLog2 <= 64, "home field fits the word");
-// Wide-list fill counters are u16 pairs in LDS (8192 lists in the 16 KiB that 4096 u32
-// counters took): a lane whose append finds the list full takes its increment back, so a
-// counter never exceeds the cap + one workgroup's lanes and the cap stays below this bound.
-constexpr uint32_t kWideCapMax = 65535u - 1024u;
-// LDS (u64 words) of a workgroup's segment-list fill counters: u32 per compact list, u16
-// per wide list
-GA_HD uint32_t sp_ctr_words(uint32_t nwin, bool compact) { return compact ? (nwin + 1) / 2 : (nwin + 3) / 4; }
+static_assert(kWideHomeShift + kWideSegLog2 == 64, "home field fills the word");
 constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------

@@ -316,9 +316,8 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
 __device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t kh, uint64_t k0, uint64_t k1, uint64_t k2,
                                             uint64_t c, uint64_t b) {
   if (c < (1ULL << (kWideHomeShift - kWideCountShift)) && b < (1ULL << kWideCountShift)) {
-    const uint32_t w = ((uint32_t)kh & s.mask) >> s.seg_log2, one = 1u << ((w & 1u) << 4);
-    // u16 fill counters, two per LDS word (kWideCapMax)
-    const uint32_t pos = (atomicAdd(&s.lctr[w >> 1], one) >> ((w & 1u) << 4)) & 0xFFFFu;
+    const uint32_t w = ((uint32_t)kh & s.mask) >> s.seg_log2;
+    const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
     if (pos < s.lcap) {
       const uint64_t home = (uint64_t)((uint32_t)kh & ((1u << s.seg_log2) - 1u));
       ulonglong2 *e = (ulonglong2 *)(s.lists + ((size_t)w * s.lcap + pos) * kWideEntryWords);
@@ -326,7 +325,6 @@ __device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t kh, uin
       e[1] = make_ulonglong2(k2, (home << kWideHomeShift) | (c << kWideCountShift) | b);
       return;
     }
-    atomicSub(&s.lctr[w >> 1], one);  // full: the counter returns to the cap
   }
   sparse_add(s, k0, k1, k2, c, b);
 }
@@ -888,31 +886,12 @@ __device__ __forceinline__ void dense_flush(const KArgs &a, const DenseSink &ds)
   spill_counts_out(a, ds.ctr);
 }
 
-// Loads this workgroup's segment-list fills (continuing lists: accum) into LDS: u32 per
-// compact list, u16 pairs for wide lists (sp_ctr_words).
-__device__ __forceinline__ void sp_counts_in(const KArgs &a, uint32_t *sctr) {
-  const uint32_t *in = a.sp_counts + (size_t)blockIdx.x * a.sp_nwin;
-  if (a.s.compact) {
-    for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
-      const uint32_t c0 = a.accum ? in[i] : 0u;
-      sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
-    }
-    return;
-  }
-  for (uint32_t i = threadIdx.x; i < (a.sp_nwin + 1) / 2; i += blockDim.x) {
-    const uint32_t c0 = a.accum ? in[2 * i] : 0u, c1 = a.accum && 2 * i + 1 < a.sp_nwin ? in[2 * i + 1] : 0u;
-    sctr[i] = (c0 < a.sp_cap ? c0 : a.sp_cap) | (c1 < a.sp_cap ? c1 : a.sp_cap) << 16;
-  }
-}
-
 // Stores this workgroup's segment-list fills and, for device-conditional folds, adds
 // its fullest list to the launch's flag (one atomic max per workgroup).
 __device__ __forceinline__ void sp_counts_out(const KArgs &a, const uint32_t *sctr) {
   uint32_t mx = 0;
-  const bool wide = !a.s.compact;  // u16 counter pairs (wide_append)
   for (uint32_t w = threadIdx.x; w < a.sp_nwin; w += blockDim.x) {
-    const uint32_t v = wide ? (sctr[w >> 1] >> ((w & 1u) << 4)) & 0xFFFFu : sctr[w];
-    const uint32_t c = v < a.sp_cap ? v : a.sp_cap;
+    const uint32_t c = sctr[w] < a.sp_cap ? sctr[w] : a.sp_cap;
     a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + w] = c;
     mx = c > mx ? c : mx;
   }
@@ -928,9 +907,12 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
   // LDS: dense bins + extras, then the segment-list fill counters
   uint32_t *sctr = (uint32_t *)&lds[a.lds_bins + kLdsExtraWords];
-  sp_counts_in(a, sctr);
+  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
+    const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
+    sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
+  }
   // hot-key cache after the segment counters (8-byte aligned), then the doorkeeper bitmap
-  HotKey *hot = (HotKey *)&lds[a.lds_bins + kLdsExtraWords + sp_ctr_words(a.sp_nwin, a.s.compact)];
+  HotKey *hot = (HotKey *)&lds[a.lds_bins + kLdsExtraWords + (a.sp_nwin + 1) / 2];
   for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
   uint32_t *door = (uint32_t *)(hot + a.hot_n);
   const uint32_t door_words = a.door_log2 ? 1u << (a.door_log2 - 5) : 0u;
@@ -987,8 +969,11 @@ __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
   const uint32_t img_words = kIp >= 0 ? a.ipl_bytes / 8 : 0u;
   if (kIp >= 0) fill_lds_u4((uint4 *)lds, (const uint4 *)a.ipl, a.ipl_bytes / 16);
   uint32_t *sctr = (uint32_t *)(lds + img_words);
-  sp_counts_in(a, sctr);
-  HotKey *hot = (HotKey *)&lds[img_words + sp_ctr_words(a.sp_nwin, false)];
+  for (uint32_t i = threadIdx.x; i < a.sp_nwin; i += blockDim.x) {
+    const uint32_t c0 = a.accum ? a.sp_counts[(size_t)blockIdx.x * a.sp_nwin + i] : 0u;
+    sctr[i] = c0 < a.sp_cap ? c0 : a.sp_cap;
+  }
+  HotKey *hot = (HotKey *)&lds[img_words + (a.sp_nwin + 1) / 2];
   for (uint32_t i = threadIdx.x; i < a.hot_n; i += blockDim.x) hot[i].tag = 0ULL;
   uint32_t *door = (uint32_t *)(hot + a.hot_n);
   const uint32_t door_words = a.door_log2 ? 1u << (a.door_log2 - 5) : 0u;
@@ -1169,8 +1154,8 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   const uint32_t lists_per_round = blockDim.x / lpl, sub = threadIdx.x & (lpl - 1);
   uint32_t any = 0;
   for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) any |= counts[(size_t)l * nwin + w];
-  // (a flag word in the segment's LDS, so the kernel has no static LDS next to the 80 KiB
-  // segment that two workgroups per CU share)
+  // (a flag word in the segment's LDS: __syncthreads_or would take static LDS beyond the
+  // 160 KiB the segment may fill)
   if (threadIdx.x == 0) seg[0] = 0ULL;
   __syncthreads();
   if (any) seg[0] = 1ULL;
@@ -3084,7 +3069,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   k.p = a.plan;
   const bool sketch = a.cms_depth || a.hll_p;
   size_t lds = a.tier1 ? (size_t)a.ipl_bytes + (size_t)a.lds_bins * 4 + kL4ExtraBytes
-                       : ((size_t)a.lds_bins + kLdsExtraWords + sp_ctr_words(k.sp_nwin, a.sparse.compact)) * 8 +
+                       : ((size_t)a.lds_bins + kLdsExtraWords) * 8 + (size_t)k.sp_nwin * 4 +
                              (a.hot_n ? 4 + (size_t)a.hot_n * kHotKeyBytes : 0);
   // the hot-key cache's doorkeeper bitmap takes what LDS is left (2^13 .. 2^18 bits) on the
   // wide-key list path, where any key may otherwise claim an entry
@@ -3112,7 +3097,7 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
     // LDS: (remote context) the image of every pod IP when it fits next to a cache of
     // >= kWideIplMinHot entries and a 2^kWideIplMinDoor-bit doorkeeper (the cache halves
     // until it does), counters, cache, then the largest doorkeeper bitmap that fits
-    const size_t ctr = (size_t)sp_ctr_words(k.sp_nwin, false) * 8, img = remote && a.ipl ? ((size_t)a.ipl_bytes + 15) & ~15ull : 0;
+    const size_t ctr = (size_t)((k.sp_nwin + 1) / 2) * 8, img = remote && a.ipl ? ((size_t)a.ipl_bytes + 15) & ~15ull : 0;
     int kip = -1;
     if (img) {
       uint32_t hn = k.hot_n;

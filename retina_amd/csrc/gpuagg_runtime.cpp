@@ -1429,8 +1429,8 @@ constexpr uint64_t kDeferLaunches = 64;
 // (the Go plugin's 2^22-record batches: 2^14; full-size launches fold per batch, see launch()).
 constexpr uint64_t kSmallLaunchChunk = 1ull << 16;
 // Default device memory for the wide-key segment lists of one ctx (32-byte entries;
-// gpuagg_config.wide_list_mib overrides it): 32 GiB (512 entries per workgroup and segment at 2^24
-// slots = 8192 segments), at most 1/8 of the device.  A list that fills sends its updates to memory-side
+// gpuagg_config.wide_list_mib overrides it): 32 GiB (1024 entries per workgroup and segment at 2^24
+// slots), at most 1/8 of the device.  A list that fills sends its updates to memory-side
 // atomics, and under C4's skew 8 GiB (256 entries) overflowed within one launch: 1.74 ->
 // 1.32 ms per 100M records (profiles/round3/exp/v2_wide_list_bytes.jsonl).
 constexpr uint64_t kWideListBytes = 32ull << 30;
@@ -1522,18 +1522,17 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   // counters take LDS words from the dense window
   const bool generic = !a.dense_ng || a.dns_compact;  // kernels that take compact-key lists
   const uint64_t sp_nwin = c->sparse_slots ? c->sparse_slots >> c->sv.seg_log2 : 0;
-  // wide (192-bit) keys take per-segment lists too when the table has at most 8192
-  // segments of 2^11 slots (sparse_fold_wide_kernel folds one per workgroup)
+  // wide (192-bit) keys take per-segment lists too when the table has at most 4096
+  // segments of 2^12 slots (sparse_fold_wide_kernel folds one per workgroup)
   const bool wide_lists = !c->sv.compact && c->sparse_slots && c->sparse_slots <= (1ull << kWideMaxLog2) &&
                           !(c->cfg.flags & GPUAGG_FLAG_NO_WIDE_LISTS);
-  const bool sp_lists = generic && (c->sv.compact || wide_lists) && sp_nwin &&
-                        sp_nwin <= (c->sv.compact ? kSparseMaxSegLists : kWideMaxSegLists) &&
+  const bool sp_lists = generic && (c->sv.compact || wide_lists) && sp_nwin && sp_nwin <= kSparseMaxSegLists &&
                         !(c->cfg.flags & GPUAGG_FLAG_DIRECT_SKETCH);
   // plans with HBM-table keys (remote context, ip / port options): an LDS cache of the
   // hot keys per workgroup in front of the table (hot_add in gpuagg_kernels.hip)
   const bool hot = generic && c->sparse_slots && !c->sv.compact && !(c->cfg.flags & GPUAGG_FLAG_NO_HOT_KEYS);
   a.hot_n = hot ? kHotKeys : 0u;
-  a.lds_bins = prefix(kLdsMaxBins - (sp_lists ? sp_ctr_words((uint32_t)sp_nwin, c->sv.compact) : 0u) -
+  a.lds_bins = prefix(kLdsMaxBins - (sp_lists ? (uint32_t)(sp_nwin + 1) / 2 : 0u) -
                       (hot ? kHotKeys * kHotKeyBytes / 8 + 1 : 0u));
   // tier-1: the LDS IP image plus u32 bins, when at least the hottest group fits
   a.tier1 = false;
@@ -1663,8 +1662,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         g.sp_nwin = (uint32_t)sp_nwin;
         uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
         if (!c->sv.compact)  // 32-byte entries: wide_list_bytes of lists per ctx
-          cap = std::min<uint64_t>(kWideCapMax, std::max<uint64_t>(16, c->wide_list_bytes / (8 * kWideEntryWords) /
-                                                                          ((uint64_t)a.blocks * sp_nwin))) &
+          cap = std::max<uint64_t>(16, c->wide_list_bytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin)) &
                 ~1ULL;
         g.sp_cap = (uint32_t)cap;
       }
@@ -2234,7 +2232,7 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
       compact &= (groups[g].family == FAM_DNS_REQ || groups[g].family == FAM_DNS_RESP) &&
                  !(groups[g].src_opts & (OPT_IP | OPT_PORT));
   c->sv.compact = compact ? 1u : 0u;
-  if (c->sparse_slots) {  // probe / fold segments: compact 2^13 slots; wide 2^11 (or the table)
+  if (c->sparse_slots) {  // probe / fold segments: compact 2^13 slots; wide 2^12 (or the table)
     const uint32_t lg = (uint32_t)__builtin_ctzll(c->sparse_slots);
     c->sv.seg_log2 = compact ? std::min<uint32_t>(lg, kSparseSegLog2)
                              : (lg <= kWideMaxLog2 ? std::min<uint32_t>(lg, kWideSegLog2) : lg);

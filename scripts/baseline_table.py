@@ -16,6 +16,10 @@ LABEL = {
 }
 
 
+def pow2(n: int) -> str:
+    return "2^%d" % (n.bit_length() - 1) if n and not n & (n - 1) else str(n)
+
+
 def rows(path):
     d = json.load(open(path))
     cfg = path.rsplit("_bench_", 1)[-1].replace(".json", "")
@@ -34,12 +38,12 @@ def rows(path):
         traffic))
     pr = d.get("production")
     if pr:
-        out.append("| %s | HIP, device-resident 2^20-record launches (Go batch) | 1 GPU | %.3g | — | %.1f %% kernel | — |" % (
-            LABEL[cfg], pr["records_per_s"], 100 * pr["kernel_frac"]))
+        out.append("| %s | HIP, device-resident %s-record launches (Go batch) | 1 GPU | %.3g | — | %.1f %% kernel | — |" % (
+            LABEL[cfg], pow2(pr.get("batch_records", 1 << 20)), pr["records_per_s"], 100 * pr["kernel_frac"]))
     hf = d.get("host_fed")
     if hf:
-        out.append("| %s | HIP, host-fed 2^20-record pinned batches (PCIe H2D incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
-            LABEL[cfg], hf["value"]))
+        out.append("| %s | HIP, host-fed %s-record pinned batches (PCIe H2D incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
+            LABEL[cfg], pow2(hf.get("batch_records", 1 << 20)), hf["value"]))
     hr = d.get("host_fed_raw")
     if hr:
         out.append("| %s | HIP, raw 72-B samples via gpuagg_raw_feed_put (PCIe incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (

@@ -26,7 +26,7 @@ def row(path):
 
 if __name__ == "__main__":
     print("| config | records / step | records/s | ms/step | dominant kernel | kernel ms (HIP events) "
-          "| kernel % of 8 TB/s | step % | HBM B/rec (PMC) | 2^20-record launches, records/s "
+          "| kernel % of 8 TB/s | step % | HBM B/rec (PMC) | Go-batch launches (2^22), records/s "
           "| scrape ms (snapshot + render) | CPU tuned, 16 thr |")
     print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for p in sys.argv[1:]:
