@@ -445,11 +445,14 @@ def main():
     # ~10 launches and settles after ~25 (0.409 -> 0.425 -> 0.404 ms at C2, the same after
     # 2 s idle: profiles/round5/r5k_ramp.jsonl), so the driver's 5 warm-up steps left the
     # timed region in the hump.  Reported as `settle`; the timed region is unchanged.
+    # Launches go back to back in groups of 8 (a sync after each one left the GPU idle for a
+    # host round trip per launch, which at C1's 56 us launches showed in rocprof's averages).
     settle_n, t_settle = 0, time.perf_counter()
     while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        g.submit_device(dcols, n)
+        for _ in range(8):
+            g.submit_device(dcols, n)
         g.sync()
-        settle_n += 1
+        settle_n += 8
     settle_s = time.perf_counter() - t_settle
     for _ in range(args.warmup):
         g.submit_device(dcols, n)

@@ -46,8 +46,12 @@ def rows(path):
             LABEL[cfg], pow2(hf.get("batch_records", 1 << 20)), hf["value"]))
     hr = d.get("host_fed_raw")
     if hr:
-        out.append("| %s | HIP, raw 72-B samples via gpuagg_raw_feed_put (PCIe incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
-            LABEL[cfg], hr["value"]))
+        out.append("| %s | HIP, raw 72-B samples via gpuagg_raw_feed_put, %s %d threads (PCIe incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
+            LABEL[cfg], hr.get("feed_mode", "raw_dma"), hr.get("feed_threads", 1), hr["value"]))
+        best = hr.get("best")
+        if best and best["value"] > hr["value"]:
+            out.append("| %s | HIP, raw samples via gpuagg_raw_feed_put, %s %d threads (PCIe incl.) | 1 GPU | %.3g | — | PCIe-bound | — |" % (
+                LABEL[cfg], best["mode"], best["threads"], best["value"]))
     return out
 
 
