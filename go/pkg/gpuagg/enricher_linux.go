@@ -238,6 +238,12 @@ func (e *Enricher) flowToRecord(f *flow.Flow) (Record, bool) {
 		obs = 3
 	}
 	verdict := uint32(f.GetVerdict()) & 0xff
+	// rows the raw decode leaves out as well (PacketRecord / DropRecord: verdict 255, which no
+	// metric consumes): a traffic direction the meta word cannot carry, a drop type past
+	// the enum
+	if uint32(f.GetTrafficDirection()) > 3 || (f.GetVerdict() == flow.Verdict_DROPPED && uint32(meta.GetDropReason()) > 7) {
+		verdict = 255
+	}
 	r := Record{
 		SrcIP: src, DstIP: dst, Bytes: meta.GetBytes(),
 		Meta: proto | verdict<<8 | (uint32(f.GetTrafficDirection())&3)<<16 | (uint32(meta.GetDropReason())&7)<<18 |
