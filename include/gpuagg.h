@@ -524,6 +524,9 @@ typedef struct gpuagg_stats {
 #define GPUAGG_KERNEL_DENSE_LDS_IP 3u  /* dense_lds_kernel: IP table + u32 bins in LDS */
 #define GPUAGG_KERNEL_CPU 4u           /* the CPU backend's host threads               */
 
+/* The timed counters (kernel / fold / sketch / decode ms and launches) are summed from the
+ * launches' HIP events when the stats are read (after gpuagg_sync: at once; with launches
+ * in flight the call waits for the timed ones), not in gpuagg_sync. */
 int gpuagg_get_stats(gpuagg_ctx *ctx, gpuagg_stats *out);
 /* Enables HIP-event timing of the aggregation kernel on the ctx's stream; disabling zeroes
  * the timed counters (kernel / fold / sketch / decode ms and launches). */

@@ -474,6 +474,7 @@ struct gpuagg_ctx {
   // node-wide feeds over this context (gpuagg_feed.cpp): detached by gpuagg_destroy
   std::vector<gpuagg_raw_feed *> feeds;
   uint64_t host_decode_oor = 0;  // out-of-range rows the feeds decoded on the host
+  uint64_t *h_sync_words = nullptr;  // pinned: gpuagg_sync's counter readback [decode oor, sparse dropped]
 };
 
 // ------------------------------------------------------------------------------------
@@ -1960,6 +1961,7 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   dev_free(c, c->d_lat_carry[1]);
   if (c->d_lat_tmp) hipFree(c->d_lat_tmp);
   x_host_free(c, c->h_lat_n);
+  x_host_free(c, c->h_sync_words);
   dev_free(c, c->d_dense_cnt);
   dev_free(c, c->d_dense_byt);
   dev_free(c, c->sv.k0);  // k1, k2, cnt, byt point into the same array
@@ -2856,15 +2858,19 @@ int gpuagg_sync(gpuagg_ctx *c) {
   int rc = bind(c);
   if (rc) return rc;
   if ((rc = fold_pending(c))) return rc;
+  // the counters come back on the stream, ahead of its one synchronisation (no blocking
+  // copy per counter); the timing events are read when the stats are (gpuagg_get_stats)
+  if (!c->h_sync_words) HIPCHK(c, x_host_alloc(c, (void **)&c->h_sync_words, 16));
+  uint64_t *w = c->h_sync_words;
+  w[0] = w[1] = 0;
+  if (c->d_decode_oor) HIPCHK(c, x_copy_async(c, &w[0], c->d_decode_oor, 8, hipMemcpyDeviceToHost, c->stream));
+  if (c->sparse_slots) HIPCHK(c, x_copy_async(c, &w[1], c->sv.dropped, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, x_sync(c, c->stream));
-  drain_timing(c);
-  if (c->d_decode_oor)
-    HIPCHK(c, x_copy(c, &c->stats.decode_out_of_range, c->d_decode_oor, 8, hipMemcpyDeviceToHost));
-  else
-    c->stats.decode_out_of_range = 0;
-  c->stats.decode_out_of_range += c->host_decode_oor;
-  if (c->sparse_slots)
-    HIPCHK(c, x_copy(c, &c->stats.sparse_dropped, c->sv.dropped, 8, hipMemcpyDeviceToHost));
+  c->stats.decode_out_of_range = w[0] + c->host_decode_oor;
+  if (c->sparse_slots) c->stats.sparse_dropped = w[1];
+  // an agent that keeps timing on but never reads the stats: bound the pending events
+  if (c->pending_events.size() + c->pending_sketch.size() + c->pending_decode.size() + c->pending_fold.size() > 4096)
+    drain_timing(c);
   return GPUAGG_OK;
 }
 
@@ -4617,12 +4623,20 @@ int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
 
 int gpuagg_get_stats(gpuagg_ctx *c, gpuagg_stats *out) {
   if (!c || !out) return GPUAGG_EINVAL;
+  if (!c->cpu) {
+    if (int rc = bind(c)) return rc;
+    drain_timing(c);  // the timed launches since the last read (their events complete by now or soon)
+  }
   *out = c->stats;
   return GPUAGG_OK;
 }
 
 int gpuagg_set_timing(gpuagg_ctx *c, int enabled) {
   if (!c) return GPUAGG_EINVAL;
+  if (!c->cpu) {  // events of launches before this call count before it
+    if (int rc = bind(c)) return rc;
+    drain_timing(c);
+  }
   if (c->cpu) c->host_timing = enabled != 0;  // host wall time of the launches (no HIP events)
   else c->timing = enabled != 0;
   c->tm_chain = false;
