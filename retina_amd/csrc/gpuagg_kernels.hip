@@ -3233,9 +3233,16 @@ hipError_t launch_aggregate(const LaunchArgs &a, hipStream_t st, hipEvent_t betw
   return launch_folds(a, st);
 }
 
-hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
+hipError_t launch_folds(const LaunchArgs &a, hipStream_t st, const ForkJoin *fj) {
   hipError_t e;
   const DevDense dd{(unsigned long long *)a.dense_cnt, (unsigned long long *)a.dense_byt};
+  // the spill fold + reduce stream: beside the segment fold when both are due
+  const bool fork = fj && a.sp_lists && a.sparse.compact && a.spill;
+  const hipStream_t sst = fork ? fj->st2 : st;
+  if (fork) {
+    if ((e = hipEventRecord(fj->fork, st)) != hipSuccess || (e = hipStreamWaitEvent(fj->st2, fj->fork, 0)) != hipSuccess)
+      return e;
+  }
   // the tier-1 copies are summed by stage_reduce_kernel after the fold (one launch for
   // both reductions); without a fold they get it alone
   const uint32_t ra_x = (a.lds_bins + 255) / 256, ra_y = 8;
@@ -3244,7 +3251,7 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
     const uint32_t na = a.stage_a ? ra_x * ra_y : 0u;
     const uint32_t nb = with_b ? (a.nwin * W + 255) / 256 : 0u;
     if (na + nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(stage_reduce_kernel, dim3(na + nb), dim3(256), 0, st, a.stage_a, a.blocks, a.stage_a_stride,
+    hipLaunchKernelGGL(stage_reduce_kernel, dim3(na + nb), dim3(256), 0, sst, a.stage_a, a.blocks, a.stage_a_stride,
                        a.lds_bins, ra_x, ra_y, a.plan, (const unsigned long long *)a.stage_b, a.nwin,
                        with_b ? a.win_blocks / a.nwin : 0u, W, a.spill_lo, a.dense_len, dd);
     return hipGetLastError();
@@ -3272,11 +3279,16 @@ hipError_t launch_folds(const LaunchArgs &a, hipStream_t st) {
   e = hipFuncSetAttribute((const void *)spill_window_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, st,
+  hipLaunchKernelGGL(spill_window_kernel, dim3(a.win_blocks), dim3(1024), (size_t)8 * W, sst,
                      (const uint32_t *)a.spill, a.spill_count, a.blocks, a.spill_cap,
                      a.spill_lo, a.dense_len, W, a.nwin, dd, (unsigned long long *)a.stage_b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return reduce(a.stage_b != nullptr);
+  if ((e = reduce(a.stage_b != nullptr)) != hipSuccess) return e;
+  if (fork) {  // st continues once both folds are done
+    if ((e = hipEventRecord(fj->join, sst)) != hipSuccess) return e;
+    return hipStreamWaitEvent(st, fj->join, 0);
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_sparse_init(const SparseView &v, size_t slots, hipStream_t st) {

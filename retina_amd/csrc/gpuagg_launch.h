@@ -89,9 +89,16 @@ struct LaunchArgs {
   bool fold_cond;
   uint32_t hot_n;  // aggregate_kernel's LDS hot-key cache entries (0: none)
 };
+// A second stream for launch_folds: with both compact-key lists and spill lists (C5's
+// plan) the spill-window fold and its reduction run on st2 beside the segment fold on st
+// (they touch disjoint state), forked after `fork` and joined back through `join`.
+struct ForkJoin {
+  hipStream_t st2;
+  hipEvent_t fork, join;
+};
 // The list folds of (possibly several deferred) launches with geometry a: the compact
 // segment fold, the spill-window fold and its partial reduction.
-hipError_t launch_folds(const LaunchArgs &a, hipStream_t st);
+hipError_t launch_folds(const LaunchArgs &a, hipStream_t st, const ForkJoin *fj = nullptr);
 
 // Raw perf-record decode (gpuagg_decode.hip); kinds match GPUAGG_RAW_* of gpuagg.h.
 enum RawKind : int { kRawPacket = 1, kRawDrop = 2 };

@@ -401,6 +401,9 @@ struct gpuagg_ctx {
   size_t staging_cap = 0;
   int next_stg = 0;
   hipStream_t copy_stream = nullptr;
+  // deferred folds: the spill-window fold beside the segment fold (launch_folds' ForkJoin)
+  hipStream_t fold_stream = nullptr;
+  hipEvent_t fold_fork = nullptr, fold_join = nullptr;
   std::vector<gpuagg_batch *> batches;
   std::string kernel_name;  // aggregation kernel of the last launch (rocprofv3 spelling)
   std::string sketch_kernel_name;  // kernels of the last sketch pass, joined by "+"
@@ -713,7 +716,13 @@ int fold_pending_dense(gpuagg_ctx *c) {
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
   ENQ(c);
-  HIPCHK(c, launch_folds(f, c->stream));
+  if (f.sp_lists && f.sparse.compact && f.spill && !c->fold_stream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->fold_fork, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->fold_join, hipEventDisableTiming));
+  }
+  const ForkJoin fj{c->fold_stream, c->fold_fork, c->fold_join};
+  HIPCHK(c, launch_folds(f, c->stream, c->fold_stream ? &fj : nullptr));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->pending_fold.push_back(ev);
@@ -1996,6 +2005,12 @@ void gpuagg_destroy(gpuagg_ctx *c) {
   }
   for (ncclComm_t cm : c->rccl_comms) ncclCommDestroy(cm);
   c->rccl_comms.clear();
+  if (c->fold_stream) {
+    hipStreamSynchronize(c->fold_stream);
+    hipStreamDestroy(c->fold_stream);
+  }
+  if (c->fold_fork) hipEventDestroy(c->fold_fork);
+  if (c->fold_join) hipEventDestroy(c->fold_join);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
