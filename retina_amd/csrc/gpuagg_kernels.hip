@@ -2503,7 +2503,7 @@ __global__ __launch_bounds__(1024) void cms_fold_kernel(SketchK k, uint32_t n_li
   }
 }
 
-hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels) {
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels, const ForkJoin *fj) {
   const bool scatter = a.passes != kSketchFolds, folds = a.passes != kSketchScatter;
   if (a.n == 0 && scatter) return hipSuccess;
   std::string names;
@@ -2623,6 +2623,14 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
     if (kernels) *kernels = names;
     return hipSuccess;
   }
+  // the count-min fold beside the HLL chain when both are due (-2 % per C3 step,
+  // profiles/round5/exp/r5c3f_*)
+  const bool fork = fj && a.nwin && a.cms_depth && a.hll_nsup && a.hll_p;
+  const hipStream_t cst = fork ? fj->st2 : st;
+  if (fork) {
+    if ((e = hipEventRecord(fj->fork, st)) != hipSuccess || (e = hipStreamWaitEvent(fj->st2, fj->fork, 0)) != hipSuccess)
+      return e;
+  }
   if (a.nwin && a.cms_depth) {
     names += names.empty() ? "cms_fold_kernel" : "+cms_fold_kernel";
     const size_t lds = (size_t)4 << a.win_shift;
@@ -2630,7 +2638,7 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
         (e = hipFuncSetAttribute((const void *)cms_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, st, k, a.blocks);
+    hipLaunchKernelGGL(cms_fold_kernel, dim3(a.fold_blocks), dim3(1024), lds, cst, k, a.blocks);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (a.hll_nsup && a.hll_p) {
@@ -2659,6 +2667,10 @@ hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kerne
       return e;
     hipLaunchKernelGGL(hll_fold_kernel, dim3(a.hll_nwin), dim3(1024), lds, st, k);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (fork) {
+    if ((e = hipEventRecord(fj->join, fj->st2)) != hipSuccess || (e = hipStreamWaitEvent(st, fj->join, 0)) != hipSuccess)
+      return e;
   }
   if (kernels) *kernels = names;
   return hipSuccess;

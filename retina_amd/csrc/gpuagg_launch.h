@@ -256,8 +256,11 @@ struct SketchArgs {
   bool accum;
 };
 constexpr uint32_t kSketchBoth = 0, kSketchScatter = 1, kSketchFolds = 2;
-// *kernels: the pass's kernels in rocprofv3 spelling joined by "+"
-hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels);
+struct ForkJoin;
+// *kernels: the pass's kernels in rocprofv3 spelling joined by "+"; fj (may be null): the
+// folds' count-min pass on fj->st2 beside the HLL split + fold on st (disjoint state),
+// joined back into st
+hipError_t launch_sketch(const SketchArgs &a, hipStream_t st, std::string *kernels, const ForkJoin *fj = nullptr);
 
 // `between` (may be null) is recorded after aggregate_kernel, before the spill fold.
 // *kernel (may be null) receives the aggregation kernel's signature as rocprofv3 prints it

@@ -700,6 +700,17 @@ constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 // snapshot), state export, merge, slot retirement and dense re-layout.
 int fold_pending_sketch(gpuagg_ctx *c);
 
+// The ctx's second stream for folds that run side by side (launch_folds, launch_sketch).
+int fold_fork_join(gpuagg_ctx *c, ForkJoin *fj) {
+  if (!c->fold_stream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->fold_fork, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->fold_join, hipEventDisableTiming));
+  }
+  *fj = ForkJoin{c->fold_stream, c->fold_fork, c->fold_join};
+  return GPUAGG_OK;
+}
+
 // The aggregation launches' deferred lists only (their own budget ran out: the sketch
 // lists keep theirs).
 int fold_pending_dense(gpuagg_ctx *c) {
@@ -716,13 +727,11 @@ int fold_pending_dense(gpuagg_ctx *c) {
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
   ENQ(c);
-  if (f.sp_lists && f.sparse.compact && f.spill && !c->fold_stream) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreateWithFlags(&c->fold_fork, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->fold_join, hipEventDisableTiming));
-  }
-  const ForkJoin fj{c->fold_stream, c->fold_fork, c->fold_join};
-  HIPCHK(c, launch_folds(f, c->stream, c->fold_stream ? &fj : nullptr));
+  ForkJoin fj{};
+  const bool fork = f.sp_lists && f.sparse.compact && f.spill;
+  if (fork)
+    if (int rc = fold_fork_join(c, &fj)) return rc;
+  HIPCHK(c, launch_folds(f, c->stream, fork ? &fj : nullptr));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->pending_fold.push_back(ev);
@@ -957,7 +966,9 @@ int fold_pending_sketch(gpuagg_ctx *c) {
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
   }
   ENQ(c);
-  HIPCHK(c, launch_sketch(s, c->stream, nullptr));
+  ForkJoin fj{};
+  if (!c->cpu && (rc = fold_fork_join(c, &fj))) return rc;
+  HIPCHK(c, launch_sketch(s, c->stream, nullptr, c->cpu ? nullptr : &fj));
   if (c->timing) {
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->pending_fold.push_back(ev);
