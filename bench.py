@@ -374,9 +374,106 @@ def scrape_cost(g, reps: int = 3):
                     "scrape epoch, outside `value`" % reps}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N rank processes of this
+    script under torch.distributed.run (one per GPU, 127.0.0.1 rendezvous) as a CHILD and
+    return its exit code.  Called before anything in this process touches the GPU (no exec
+    from a process with a HIP context); every rank then binds its device before joining the
+    process group (rank_device / main)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd + list(argv), env=env)
+
+
+def rank_device(local_rank: int, local_world: int, backend: str, ndev: int) -> int:
+    """The GPU of a rank: one per rank (RCCL needs distinct devices).  Under gloo, ranks may
+    share devices round-robin (the one-GPU rehearsal of the multi-rank path)."""
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible (use --cpu-backend for the host engine)")
+    if local_world > ndev:
+        if backend == "nccl":
+            raise SystemExit("bench.py: %d ranks on %d visible GPUs: RCCL needs one GPU per rank "
+                             "(--backend gloo shares devices)" % (local_world, ndev))
+        return local_rank % ndev
+    return local_rank
+
+
+def host_columns(arrs):
+    """_abi.Columns over host numpy arrays (the CPU backend's "device" memory)."""
+    from retina_amd import _abi
+    return _abi.Columns(*[a.ctypes.data_as(_abi.u32p) for a in arrs], None, None)
+
+
+def gen_host_records(n: int, pods, seed: int, gen_kw, chunk: int = 8_000_000):
+    """gen_device_records for the CPU backend: the same columns, kept in host memory."""
+    from retina_amd import workloads as W
+    cols = [np.empty(n, np.uint32) for _ in range(6)]
+    start, k, r = 0, 0, None
+    while start < n:
+        m = min(chunk, n - start)
+        r = W.gen_records(m, pods, seed * 1000 + k, **gen_kw)
+        for t, a in zip(cols, (r.src_ip, r.dst_ip, r.bytes, r.meta, r.ports, r.dns_id)):
+            t[start:start + m] = a
+        start += m
+        k += 1
+    return cols, r
+
+
+def merge_check(args, cfg, spec, sketch, remote, n, world, g, gen, cols_of, pods, gen_kw, chunk, capacity):
+    """--check-merge: rank 0's merged state after the timed region against ONE engine fed
+    every rank's batch `steps` times (the engine was reset after the warm-up, so the merged
+    state holds exactly the timed steps of every rank).  Counters and count-min are sums and
+    HLL registers a max, so the two must be equal bit for bit."""
+    from retina_amd import GpuAgg
+    ref = GpuAgg(device=g.device, remote_context=remote, max_slots=cfg["pods"] + 16,
+                 max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=capacity, flags=g.cfg.flags, **sketch)
+    try:
+        ref.reconcile(spec)
+        ref.load_endpoints(pods.endpoints)
+        for r in range(world):
+            cols, _ = gen(n, pods, cfg["seed"] + 7919 * r, gen_kw, chunk)
+            dc = cols_of(cols)
+            for _ in range(args.steps):
+                ref.submit_device(dc, n)
+            ref.sync()
+        want, got = ref.snapshot(), g.snapshot()
+        out = {"series": len(got), "series_equal": got == want, "records_each_rank": n, "ranks": world}
+        if sketch:
+            out["cms_equal"] = bool(np.array_equal(g.cms_array(), ref.cms_array()))
+            out["hll_equal"] = bool(np.array_equal(g.hll_array(), ref.hll_array()))
+        out["equal"] = all(v for k, v in out.items() if k.endswith("_equal"))
+        return out
+    finally:
+        ref.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="GPUs (ranks) of this node; default: WORLD_SIZE, or 1.  Without a launcher, "
+                         "N > 1 starts N ranks under torch.distributed.run")
+    ap.add_argument("--backend", default=os.environ.get("GPUAGG_BENCH_BACKEND", "nccl"),
+                    choices=("nccl", "gloo"),
+                    help="collective backend of the per-epoch merge: nccl = RCCL over xGMI; gloo stages "
+                         "through host memory and lets ranks share one GPU")
+    ap.add_argument("--cpu-backend", action="store_true",
+                    help="run the engine's CPU backend (GPUAGG_FLAG_CPU_BACKEND, host memory) instead of "
+                         "a GPU: rehearses the multi-rank path on a machine without one (not a bench line)")
+    ap.add_argument("--check-merge", action="store_true",
+                    help="reset the engines after the warm-up, and after the timed region check rank 0's "
+                         "merged state against one engine fed every rank's batch")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
@@ -394,19 +491,42 @@ def main():
                     help="skip the Go-batch-size (1M-record) device-resident launches")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # nothing has touched the GPU yet (torch is not even imported): start the ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.gpus and args.gpus != world:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.cpu_backend and args.backend != "gloo":
+        raise SystemExit("bench.py: --cpu-backend merges over gloo (pass --backend gloo)")
+    if args.check_merge and args.config == "c5":
+        # DNS ids index each rank's own generated payload dictionary; the merge of DNS keys
+        # needs one dictionary interned alike on every rank (as the Go plugin does per context)
+        raise SystemExit("bench.py: --check-merge does not cover c5 (per-rank DNS dictionaries)")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+
     import torch
     import torch.distributed as dist
-    from retina_amd import GpuAgg
+    from retina_amd import GpuAgg, _abi
     from retina_amd import workloads as W
     from retina_amd.dist import merge_engine
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = args.cpu_backend
+    if cpu:
+        dev_index, device = 0, torch.device("cpu")
+    else:
+        # bind this rank's GPU BEFORE the process group exists (RCCL communicators are made
+        # on the current device)
+        dev_index = rank_device(local_rank, local_world, args.backend, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+        dist.init_process_group(args.backend)
+        if dist.get_world_size() != world:
+            raise SystemExit("bench.py: process group has %d ranks, WORLD_SIZE %d" % (dist.get_world_size(), world))
+    cuda_sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     cfg = W.CONFIGS[args.config]
     n = args.records or cfg["records"]
@@ -419,21 +539,33 @@ def main():
     t0 = time.time()
     # DNS ids index one generated dictionary: C5 is generated as a single chunk
     chunk = n if args.config == "c5" else 8_000_000
-    cols, last = gen_device_records(n, pods, cfg["seed"] + 7919 * rank, device, gen_kw, chunk=chunk,
-                                    cache_key=args.config)
-    torch.cuda.synchronize()
-    log("rank %d: %d records resident in HBM (%.1f s)" % (rank, n, time.time() - t0))
+    if cpu:
+        def gen(nn, pp, seed, kw, ch):
+            return gen_host_records(nn, pp, seed, kw, chunk=ch)
+        cols_of = host_columns
+    else:
+        def gen(nn, pp, seed, kw, ch):
+            return gen_device_records(nn, pp, seed, device, kw, chunk=ch)
+        cols_of = lambda c: GpuAgg.device_columns(*c)  # noqa: E731
+    if cpu or world > 1:
+        cols, last = gen(n, pods, cfg["seed"] + 7919 * rank, gen_kw, chunk)
+    else:
+        cols, last = gen_device_records(n, pods, cfg["seed"], device, gen_kw, chunk=chunk, cache_key=args.config)
+    cuda_sync()
+    log("rank %d: %d records resident in %s (%.1f s)" % (rank, n, "host memory" if cpu else "HBM of cuda:%d" % dev_index,
+                                                        time.time() - t0))
 
     # C5's DNS series are sparse keys (one per query payload and side): a 2^24-slot table
     remote = args.config in REMOTE_CONFIGS
-    g = GpuAgg(device=local_rank, remote_context=remote, max_slots=cfg["pods"] + 16,
-               max_ips=2 * cfg["pods"] + 16,
-               sparse_capacity_log2={"c1": 21, "c5": 23, "c4-remote": 24}.get(args.config, 16), **sketch)
+    capacity = {"c1": 21, "c5": 23, "c4-remote": 24}.get(args.config, 16)
+    g = GpuAgg(device=dev_index, remote_context=remote, max_slots=cfg["pods"] + 16,
+               max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=capacity,
+               flags=_abi.FLAG_CPU_BACKEND if cpu else 0, **sketch)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     for p in last.dns:
         g.dns_intern(p.rcode, p.qtypes, p.query, p.ips, p.num_answers)
-    dcols = GpuAgg.device_columns(*cols)
+    dcols = cols_of(cols)
 
     if args.production_only:  # diagnostic (rocprof of the GO_BATCH-record launches)
         print(json.dumps({"production": production_geometry(g, cols, n, bpr, 0.0)}), flush=True)
@@ -457,33 +589,39 @@ def main():
     for _ in range(args.warmup):
         g.submit_device(dcols, n)
     g.sync()
+    if args.check_merge:  # the state then holds exactly the timed steps
+        g.reset()
 
     # ---- timed region --------------------------------------------------------------
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    cuda_sync()
     g.set_timing(False)
     g.set_timing(True)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         g.submit_device(dcols, n)
     g.sync()
+    t_merge = time.perf_counter()
     if world > 1:  # per-epoch merge over RCCL/xGMI: dense + count-min sum, HLL max, sparse table
         merge_engine(g)
-    torch.cuda.synchronize()
+    cuda_sync()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    t_end = time.perf_counter()
+    elapsed, merge_s = t_end - t_start, t_end - t_merge
     stats = g.stats()
     kernel = g.kernel_name()
     sketch_kernels = g.sketch_kernel_name()
     g.set_timing(False)
     if stats["sparse_dropped"]:
         raise RuntimeError("group-by table overflowed (%d updates lost)" % stats["sparse_dropped"])
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    # max over ranks (a gloo group reduces host tensors)
+    t = torch.tensor([elapsed, merge_s], dtype=torch.float64,
+                     device=device if (world > 1 and args.backend == "nccl") else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, merge_s = (float(x) for x in t.tolist())
 
     # roofline of the dominant kernel: the aggregation kernel, or (C3) the sketch pass
     agg_ms = stats["kernel_ms"] / max(1, stats["kernel_launches"])
@@ -518,7 +656,11 @@ def main():
             "pods": cfg["pods"],
             "metrics": [s["metric_name"] for s in spec],
             "parallelism": "dp%d (records sharded, state merged once per timed region)" % world,
+            "backend": "cpu engine (GPUAGG_FLAG_CPU_BACKEND; rehearsal, not a GPU measurement)" if cpu
+            else ("gfx950; merge over %s" % ("RCCL" if args.backend == "nccl" else "gloo") if world > 1
+                  else "gfx950"),
         },
+        "merge_ms": merge_s * 1e3 if world > 1 else None,
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -538,14 +680,19 @@ def main():
                    "note": "untimed passes of the step before the warm-up steps, so the timed region runs at "
                            "steady-state clocks (profiles/round5/r5k_ramp.jsonl)"},
     }
+    if cpu:  # the host engine: no kernel, no HBM roofline
+        result["roofline"] = None
+    if args.check_merge and rank == 0:
+        result["merge_check"] = merge_check(args, cfg, spec, sketch, remote, n, world, g, gen, cols_of, pods,
+                                            gen_kw, chunk, capacity)
     if rank == 0 and not args.no_scrape:
         result["scrape"] = scrape_cost(g)
-    if rank == 0 and world == 1 and not args.no_production and n > GO_BATCH:
+    if rank == 0 and world == 1 and not cpu and not args.no_production and n > GO_BATCH:
         result["production"] = production_geometry(g, cols, n, bpr, stats["kernel_ms"] / max(1, stats["kernel_launches"]))
-    if rank == 0 and world == 1 and not args.no_host_fed:
+    if rank == 0 and world == 1 and not cpu and not args.no_host_fed:
         result["host_fed"] = host_fed_rate(g, cols, n, args.steps)
         result["host_fed_raw"] = host_fed_raw_rate(g, pods, spec, cfg["seed"] + 17)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not cpu and not args.no_cpu_baseline:
         go_s, tu_s = (400_000, 4_000_000) if args.config == "c5" else (args.cpu_sample // 8, args.cpu_sample)
         result["cpu_baseline"] = cpu_baseline(args.config, pods, spec, cfg["seed"], gen_kw, go_s, tu_s,
                                               remote=remote)

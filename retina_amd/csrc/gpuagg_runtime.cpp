@@ -4000,8 +4000,11 @@ void render_text(const gpuagg_result *r) {
     for (unsigned t = 0; t < j.T; ++t) part[t + 1] += part[t];
     run_par(j.T, [&](unsigned t) {  // offsets
       uint64_t o = part[t];
-      for (size_t q = n * t / j.T; q < n * (t + 1) / j.T; ++q) {
-        const uint64_t len = j.at[q + 1];
+      const size_t hi = n * (t + 1) / j.T;
+      for (size_t q = n * t / j.T; q < hi; ++q) {
+        // the chunk's last length is not needed, and its word j.at[hi] is the next
+        // chunk's first offset, which that chunk's thread writes (TSan, round 6)
+        const uint64_t len = q + 1 < hi ? j.at[q + 1] : 0;
         j.at[q] = o;
         o += len;
       }

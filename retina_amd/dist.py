@@ -124,6 +124,18 @@ def device_view(ptr: int, n: int, typestr: str, device):
     return torch.as_tensor(_CAI(ptr, n, typestr), device=device)
 
 
+_HOST_CTYPES = {"<i8": np.int64, "<i4": np.int32, "|u1": np.uint8}
+
+
+def host_view(ptr: int, n: int, typestr: str):
+    """torch tensor aliasing engine-owned HOST memory (the CPU backend's state; no copy)."""
+    import ctypes
+    import torch
+    dt = np.dtype(_HOST_CTYPES[typestr])
+    buf = (ctypes.c_uint8 * (n * dt.itemsize)).from_address(ptr)
+    return torch.from_numpy(np.frombuffer(buf, dtype=dt, count=n))
+
+
 def merge_engine(engine, group=None, dst: int = 0) -> None:
     """Per-epoch merge of a GpuAgg's state across ranks: rank `dst` ends with the node
     total, every other rank is reset (gpuagg_reset) so the next epoch counts only new
@@ -131,16 +143,25 @@ def merge_engine(engine, group=None, dst: int = 0) -> None:
 
     Backend "nccl" (RCCL over xGMI) reduces the engine's device memory in place through
     __cuda_array_interface__ views.  Backend "gloo" (CPU tests, and several ranks sharing
-    one GPU) stages each array through host memory: copy out, reduce, copy back."""
+    one GPU) stages each array through host memory: copy out, reduce, copy back.  An
+    engine on the CPU backend (GPUAGG_FLAG_CPU_BACKEND) keeps its state in host memory,
+    which gloo reduces in place."""
     import torch
     import torch.distributed as dist
-    device = torch.device("cuda", engine.device)
+    on_cpu = bool(engine.cfg.flags & _abi.FLAG_CPU_BACKEND)
+    device = torch.device("cpu") if on_cpu else torch.device("cuda", engine.device)
     on_host = dist.get_backend(group) == "gloo"
+    if on_cpu and not on_host:
+        raise ValueError("merge_engine: a CPU-backend engine merges over gloo")
+    dev_sync = (lambda: None) if on_cpu else (lambda: torch.cuda.synchronize(device))
     engine.sync()
     st = engine.state()
     me = dist.get_rank(group)
 
     def reduce(ptr, n, typestr, op):
+        if on_cpu:
+            dist.reduce(host_view(ptr, n, typestr), dst, op=op, group=group)
+            return
         view = device_view(ptr, n, typestr, device)
         if not on_host:
             dist.reduce(view, dst, op=op, group=group)
@@ -168,17 +189,17 @@ def merge_engine(engine, group=None, dst: int = 0) -> None:
     local = torch.empty((max(cap, 1), 5), dtype=torch.int64, device=device)
     # the engine writes on its own stream: nothing of torch's may still be pending on
     # this memory (a zero-fill racing the export was seen to wipe exported rows)
-    torch.cuda.synchronize(device)
+    dev_sync()
     n = engine.sparse_export(local.data_ptr(), cap) if cap else 0
-    torch.cuda.synchronize(device)
+    dev_sync()
     blocks = gather_entries(local.cpu() if on_host else local, n, dst, group)
     if blocks is not None:
         for r, b in enumerate(blocks):
             if r != me and b.shape[0]:
                 b = b.to(device).contiguous()
-                torch.cuda.synchronize(device)
+                dev_sync()
                 engine.sparse_import(b.data_ptr(), int(b.shape[0]))
     engine.sync()
-    torch.cuda.synchronize(device)
+    dev_sync()
     if me != dst:
         engine.reset()

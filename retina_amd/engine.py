@@ -325,7 +325,10 @@ class GpuAgg:
 
     # -- raw perf records (gpuagg_decode.hip) ----------------------------------------
     def _torch_sync(self) -> None:
-        """Device memory handed over as raw pointers may have torch work pending on it."""
+        """Device memory handed over as raw pointers may have torch work pending on it
+        (the CPU backend's buffers are host memory: nothing to wait for)."""
+        if self.cfg.flags & _abi.FLAG_CPU_BACKEND:
+            return
         import torch
         torch.cuda.synchronize(self.device)
 
