@@ -473,7 +473,8 @@ struct gpuagg_ctx {
   size_t hll_lists2_alloc = 0;
   uint32_t *d_hll_counts2 = nullptr;
   size_t hll_counts2_alloc = 0;
-  std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch pass start, end
+  std::vector<std::array<hipEvent_t, 2>> pending_sketch;  // sketch scatter launch start, end
+  uint64_t pending_sketch_submits = 0;  // submits those launches belong to (sketch_launches)
   // node-wide feeds over this context (gpuagg_feed.cpp): detached by gpuagg_destroy
   std::vector<gpuagg_raw_feed *> feeds;
   uint64_t host_decode_oor = 0;  // out-of-range rows the feeds decoded on the host
@@ -908,12 +909,12 @@ void drain_timing(gpuagg_ctx *c) {
   c->pending_decode.clear();
   for (auto &ev : c->pending_sketch) {
     float ms = 0.f;
-    if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) {
+    if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess)
       c->stats.sketch_ms += ms;
-      c->stats.sketch_launches += 1;
-    }
     for (hipEvent_t e : ev) hipEventDestroy(e);
   }
+  c->stats.sketch_launches += c->pending_sketch_submits;
+  c->pending_sketch_submits = 0;
   c->pending_sketch.clear();
   for (auto &ev : c->pending_fold) {
     float ms = 0.f;
@@ -1061,11 +1062,20 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     return GPUAGG_OK;
   };
-  std::array<hipEvent_t, 2> ev{};
-  if (c->timing) {
+  // Timing (gpuagg_set_timing): sketch_ms spans the scatter launches only -- the kernel
+  // bench.py names -- and the folds count in fold_ms (fold_pending_sketch, or the pair
+  // around a full-size launch's folds below); sketch_launches counts submits.
+  auto t_open = [&](std::array<hipEvent_t, 2> &ev) -> int {
     for (auto &e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, kTimingEventFlags));
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
-  }
+    return GPUAGG_OK;
+  };
+  auto t_close = [&](std::array<hipEvent_t, 2> &ev, std::vector<std::array<hipEvent_t, 2>> &to) -> int {
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    to.push_back(ev);
+    return GPUAGG_OK;
+  };
+  if (c->timing) ++c->pending_sketch_submits;
   // Deferred folds (small launches, e.g. the Go plugin's 2^20 records: chunk 4096): the
   // folds' fixed passes -- every count-min row and the whole HLL register array (164 MB at
   // C3's 10k pods, p = 14) are read and rewritten -- cost ~20x the scatter of such a launch,
@@ -1109,7 +1119,10 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
       s.passes = kSketchScatter;
       s.accum = accum;
       ENQ(c);
+      std::array<hipEvent_t, 2> ev{};
+      if (c->timing && (rc = t_open(ev))) return rc;
       HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
+      if (c->timing && (rc = t_close(ev, c->pending_sketch))) return rc;
       c->sk_pend.rpb = (accum ? c->sk_pend.rpb : 0) + s.chunk;
       c->sk_pend.budget = kSketchDeferRecords;
       c->sk_pend.s = s;
@@ -1118,14 +1131,18 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     }
     if ((rc = size_lists(s, s.chunk))) return rc;
     if (hnsup && (rc = size_hll_level2(c, s, m))) return rc;
-    s.passes = kSketchBoth;
+    // the scatter, then its folds (kSketchBoth as two calls, so each is timed on its own)
     s.accum = false;
     ENQ(c);
+    std::array<hipEvent_t, 2> ev{}, evf{};
+    s.passes = kSketchScatter;
+    if (c->timing && (rc = t_open(ev))) return rc;
     HIPCHK(c, launch_sketch(s, c->stream, &c->sketch_kernel_name));
-  }
-  if (c->timing) {
-    HIPCHK(c, hipEventRecord(ev[1], c->stream));
-    c->pending_sketch.push_back(ev);
+    if (c->timing && (rc = t_close(ev, c->pending_sketch))) return rc;
+    s.passes = kSketchFolds;
+    if (c->timing && (rc = t_open(evf))) return rc;
+    HIPCHK(c, launch_sketch(s, c->stream, nullptr));
+    if (c->timing && (rc = t_close(evf, c->pending_fold))) return rc;
   }
   return GPUAGG_OK;
 }
