@@ -87,7 +87,25 @@ func NewEnricher(ctx context.Context, g *gpuAgg) *Enricher {
 	for i := range e.in {
 		e.in[i] = make(chan *v1.Event, channelDepth)
 	}
+	g.onDNSRetire(e.dropDNS)
 	return e
+}
+
+// dropDNS forgets cached payloads whose dns_id the engine retired (gpuagg_dns_retire at a
+// publish): the next record with such a payload interns it again.  Called with the
+// plugin's lock held; dnsID never holds dnsMu while it takes that lock.
+func (e *Enricher) dropDNS(ids []uint32) {
+	dead := make(map[uint32]struct{}, len(ids))
+	for _, id := range ids {
+		dead[id] = struct{}{}
+	}
+	e.dnsMu.Lock()
+	for k, id := range e.dnsIDs {
+		if _, ok := dead[id]; ok {
+			delete(e.dnsIDs, k)
+		}
+	}
+	e.dnsMu.Unlock()
 }
 
 // Run starts the conversion workers and the export loop (enricher.go:69-98 starts one

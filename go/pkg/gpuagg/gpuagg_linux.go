@@ -133,11 +133,12 @@ type gpuAgg struct {
 	// enriched-flow emission (SetupChannel): the consumer channel, the cache's endpoint
 	// per slot (what getEndpoint copies, enricher.go:142-183), the DNS payload per dns_id
 	// (AddDNSInfo's arguments) and the per-batch endpoint slots from gpuagg_submit_enrich
-	external  chan *v1.Event
-	slotEP    map[int32]*common.RetinaEndpoint
-	dnsByID   map[uint32]dnsPayload
-	enrichSrc []int32
-	enrichDst []int32
+	external   chan *v1.Event
+	slotEP     map[int32]*common.RetinaEndpoint
+	dnsByID    map[uint32]dnsPayload
+	dnsRetired []func([]uint32) // producer caches told about retired ids (Enricher.dropDNS)
+	enrichSrc  []int32
+	enrichDst  []int32
 
 	// producer side: single Write()s collect in recIn (recMu also orders them against
 	// WriteBatch slices), raw samples in a batcher per kind; full pieces go to Start
@@ -952,9 +953,57 @@ func (g *gpuAgg) publish() error {
 			}
 		}
 	}
-	// the epoch is published: slots no IP maps to any more are freed (their series keep
-	// the last published value, as the reference's gauges of a deleted pod do)
+	// the epoch is published: DNS ids no series references any more (at this publish and
+	// the previous one) are retired, and slots no IP maps to any more are freed (their
+	// series keep the last published value, as the reference's gauges of a deleted pod do)
+	if err := g.retireDNSLocked(); err != nil {
+		return err
+	}
 	return g.each("gpuagg_retire_slots", func(c *C.gpuagg_ctx) C.int { return C.gpuagg_retire_slots(c, nil) })
+}
+
+// retireDNSLocked retires, on every device at once, the dns_ids no group-by key has
+// referenced at this call and the previous one (gpuagg_dns_retire's two phases), drops
+// them from dnsByID and hands them to the producer caches, so the dictionary is bounded
+// by the live series (as the reference's AdvancedRegistry holds its DNS series) instead
+// of growing with every payload ever seen.
+func (g *gpuAgg) retireDNSLocked() error {
+	if len(g.devs) == 0 || len(g.dnsByID) == 0 {
+		return nil
+	}
+	ctxs := make([]*C.gpuagg_ctx, len(g.devs))
+	for i, d := range g.devs {
+		ctxs[i] = d.ctx
+	}
+	// every id in use was handed out by InternDNS, so it is a key of dnsByID
+	ids := make([]C.uint32_t, len(g.dnsByID))
+	var n C.size_t
+	if err := check(ctxs[0], C.gpuagg_dns_retire(&ctxs[0], C.size_t(len(ctxs)), &ids[0], C.size_t(len(ids)), &n),
+		"gpuagg_dns_retire"); err != nil {
+		return err
+	}
+	if int(n) > len(ids) {
+		n = C.size_t(len(ids))
+	}
+	if n == 0 {
+		return nil
+	}
+	dead := make([]uint32, int(n))
+	for i := range dead {
+		dead[i] = uint32(ids[i])
+		delete(g.dnsByID, dead[i])
+	}
+	for _, h := range g.dnsRetired {
+		h(dead)
+	}
+	return nil
+}
+
+// onDNSRetire registers a producer cache to drop retired dns_ids from.
+func (g *gpuAgg) onDNSRetire(h func([]uint32)) {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	g.dnsRetired = append(g.dnsRetired, h)
 }
 
 // Stop stops Start (it waits for it) and releases the contexts.

@@ -172,6 +172,21 @@ int gpuagg_dns_intern(gpuagg_ctx *ctx, uint32_t rcode, const char *qtypes_joined
                       const char *query, const char *ips_joined, uint32_t num_answers,
                       uint32_t *dns_id);
 
+/* DNS id lifecycle (the dictionary would otherwise only grow under rotating answers).
+ * Over the n contexts of a node (one dictionary interned alike on each, as the Go
+ * plugin does; else GPUAGG_EINVAL): aggregates every submitted batch, then finds the DNS
+ * ids no DNS group-by key of any of them references -- after an epoch reset
+ * (gpuagg_reset, or the non-target side of a merge) that is every id.  Two phases: such
+ * an id turns idle; an id still idle at the NEXT call (unreferenced at both, and not
+ * handed out again by gpuagg_dns_intern in between) is retired.  Retired ids are reused
+ * by later interns, so the caller drops them from its own payload -> id cache: the first
+ * min(n_retired, cap) are written to ids.  A record converted with an id before one call
+ * and submitted after the next may name a retired id: its group-by entries are then not
+ * rendered and count as lost updates (gpuagg_result_dropped).  The reference keeps a DNS
+ * series' labels until the metric object is re-created (dns.go:240-242 Clean on
+ * reconcile, metrics_module.go:204-214). */
+int gpuagg_dns_retire(gpuagg_ctx *const *ctxs, size_t n, uint32_t *ids, size_t cap, size_t *n_retired);
+
 /* ------------------------------------------------------------------------------
  * Records: one decoded flow per row, struct-of-arrays, all uint32.
  *

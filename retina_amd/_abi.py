@@ -107,6 +107,8 @@ SIGNATURES = [
     ("gpuagg_set_endpoints", C.c_int, [C.c_void_p, u32p, C.POINTER(C.c_int32), C.c_size_t, C.c_uint64]),
     ("gpuagg_dns_intern", C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_char_p,
                                     C.c_uint32, u32p]),
+    ("gpuagg_dns_retire", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t, u32p, C.c_size_t,
+                                    C.POINTER(C.c_size_t)]),
     ("gpuagg_alloc_batch", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.POINTER(Batch))]),
     ("gpuagg_free_batch", None, [C.c_void_p, C.POINTER(Batch)]),
     ("gpuagg_submit", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_size_t]),

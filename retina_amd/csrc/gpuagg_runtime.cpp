@@ -82,6 +82,8 @@ struct SlotAttr {
 struct DnsAttr {
   uint32_t rcode, nresp;
   std::string qtypes, query, ips;
+  bool in_use = true;  // false once retired (gpuagg_dns_retire); the id is then reusable
+  bool idle = false;   // no key referenced it at the last gpuagg_dns_retire (retired at the next)
 };
 
 enum ValueKind { VK_COUNT, VK_BYTES };
@@ -288,6 +290,7 @@ struct gpuagg_ctx {
   std::unordered_map<uint32_t, std::string> ip_to_svc, ip_to_node;
   std::unordered_map<std::string, uint32_t> dns_ids;
   std::vector<DnsAttr> dns;
+  std::vector<uint32_t> free_dns;  // retired DNS ids, reused (lowest first) by gpuagg_dns_intern
   // label-canonical DNS payloads, kept at intern time: request series render (qtypes,
   // query), response series (rcode name, qtypes, query, ips, answers)
   std::unordered_map<std::string, uint32_t> dns_req_canon, dns_resp_canon;
@@ -2734,40 +2737,152 @@ int gpuagg_retire_slots(gpuagg_ctx *c, size_t *n_retired) {
   return GPUAGG_OK;
 }
 
-int gpuagg_dns_intern(gpuagg_ctx *c, uint32_t rcode, const char *qtypes, const char *query,
-                      const char *ips, uint32_t nresp, uint32_t *id) {
-  if (!c || !qtypes || !query || !ips || !id) return GPUAGG_EINVAL;
-  std::string key = std::to_string(rcode) + '\x1f' + qtypes + '\x1f' + query + '\x1f' + ips +
-                    '\x1f' + std::to_string(nresp);
-  auto it = c->dns_ids.find(key);
-  if (it != c->dns_ids.end()) {
-    *id = it->second;
-    return GPUAGG_OK;
-  }
-  if (c->dns.size() >= 0xFFFFFFFEull) return fail(c, GPUAGG_ECAPACITY, "DNS dictionary full");
-  const uint32_t nid = (uint32_t)c->dns.size();
-  c->dns.push_back(DnsAttr{rcode, nresp, qtypes, query, ips});
-  c->dns_ids.emplace(std::move(key), nid);
-  const std::string q = std::string(qtypes) + '\0' + query;
+static std::string dns_key(uint32_t rcode, const std::string &qtypes, const std::string &query,
+                           const std::string &ips, uint32_t nresp) {
+  return std::to_string(rcode) + '\x1f' + qtypes + '\x1f' + query + '\x1f' + ips + '\x1f' + std::to_string(nresp);
+}
+
+// The label-canonical forms of DNS id `id` (request: qtypes, query; response: rcode name,
+// qtypes, query, ips, answers): equal label tuples share one canonical id, whose label
+// values are rendered once into the *_blk tables.
+static void dns_canon_add(gpuagg_ctx *c, uint32_t id) {
+  const DnsAttr &a = c->dns[id];
+  if (c->dns_req_id.size() <= id) c->dns_req_id.resize(id + 1, 0);
+  if (c->dns_resp_id.size() <= id) c->dns_resp_id.resize(id + 1, 0);
+  const std::string q = a.qtypes + '\0' + a.query;
   auto i1 = c->dns_req_canon.emplace(q, (uint32_t)c->dns_req_rep.size());
   if (i1.second) {
-    c->dns_req_rep.push_back(nid);
+    c->dns_req_rep.push_back(id);
     c->dns_req_blk.insert(c->dns_req_blk.end(), q.begin(), q.end());
     c->dns_req_blk.push_back('\0');
     c->dns_req_boff.push_back(c->dns_req_blk.size());
   }
-  c->dns_req_id.push_back(i1.first->second);
-  const std::string full = std::string(rcode < 6 ? kRcodeNames[rcode] : "") + '\0' + q + '\0' + ips + '\0' +
-                           std::to_string(nresp);
+  c->dns_req_id[id] = i1.first->second;
+  const std::string full = std::string(a.rcode < 6 ? kRcodeNames[a.rcode] : "") + '\0' + q + '\0' + a.ips + '\0' +
+                           std::to_string(a.nresp);
   auto i2 = c->dns_resp_canon.emplace(full, (uint32_t)c->dns_resp_rep.size());
   if (i2.second) {
-    c->dns_resp_rep.push_back(nid);
+    c->dns_resp_rep.push_back(id);
     c->dns_resp_blk.insert(c->dns_resp_blk.end(), full.begin(), full.end());
     c->dns_resp_blk.push_back('\0');
     c->dns_resp_boff.push_back(c->dns_resp_blk.size());
   }
-  c->dns_resp_id.push_back(i2.first->second);
+  c->dns_resp_id[id] = i2.first->second;
+}
+
+// The canonical tables of the ids in use, from scratch (after a retire).
+static void dns_canon_rebuild(gpuagg_ctx *c) {
+  c->dns_req_canon.clear();
+  c->dns_resp_canon.clear();
+  c->dns_req_rep.clear();
+  c->dns_resp_rep.clear();
+  c->dns_req_blk.clear();
+  c->dns_resp_blk.clear();
+  c->dns_req_boff.assign(1, 0);
+  c->dns_resp_boff.assign(1, 0);
+  c->dns_req_rec.clear();  // the render's sort tokens: recomputed at the next snapshot
+  c->dns_resp_rec.clear();
+  c->dns_req_id.assign(c->dns.size(), 0);
+  c->dns_resp_id.assign(c->dns.size(), 0);
+  for (uint32_t id = 0; id < c->dns.size(); ++id)
+    if (c->dns[id].in_use) dns_canon_add(c, id);
+}
+
+int gpuagg_dns_intern(gpuagg_ctx *c, uint32_t rcode, const char *qtypes, const char *query,
+                      const char *ips, uint32_t nresp, uint32_t *id) {
+  if (!c || !qtypes || !query || !ips || !id) return GPUAGG_EINVAL;
+  std::string key = dns_key(rcode, qtypes, query, ips, nresp);
+  auto it = c->dns_ids.find(key);
+  if (it != c->dns_ids.end()) {
+    c->dns[it->second].idle = false;  // handed out again: not retired at the next call
+    *id = it->second;
+    return GPUAGG_OK;
+  }
+  uint32_t nid;
+  if (!c->free_dns.empty()) {  // a retired id (no group-by key references it)
+    nid = c->free_dns.back();
+    c->free_dns.pop_back();
+    c->dns[nid] = DnsAttr{rcode, nresp, qtypes, query, ips};
+  } else {
+    if (c->dns.size() >= 0xFFFFFFFEull) return fail(c, GPUAGG_ECAPACITY, "DNS dictionary full");
+    nid = (uint32_t)c->dns.size();
+    c->dns.push_back(DnsAttr{rcode, nresp, qtypes, query, ips});
+  }
+  c->dns_ids.emplace(std::move(key), nid);
+  dns_canon_add(c, nid);
   *id = nid;
+  return GPUAGG_OK;
+}
+
+int gpuagg_dns_retire(gpuagg_ctx *const *ctxs, size_t n, uint32_t *ids, size_t cap, size_t *n_retired) {
+  if (!ctxs || !n || !ctxs[0] || (cap && !ids)) return GPUAGG_EINVAL;
+  gpuagg_ctx *c0 = ctxs[0];
+  for (size_t i = 1; i < n; ++i) {  // one dictionary on every ctx (the producer interns alike)
+    const gpuagg_ctx *ci = ctxs[i];
+    if (!ci) return GPUAGG_EINVAL;
+    bool same = ci->dns.size() == c0->dns.size();
+    for (size_t k = 0; same && k < c0->dns.size(); ++k)
+      same = ci->dns[k].in_use == c0->dns[k].in_use && ci->dns[k].rcode == c0->dns[k].rcode &&
+             ci->dns[k].nresp == c0->dns[k].nresp && ci->dns[k].qtypes == c0->dns[k].qtypes &&
+             ci->dns[k].query == c0->dns[k].query && ci->dns[k].ips == c0->dns[k].ips;
+    if (!same) return fail(c0, GPUAGG_EINVAL, "dns_retire: ctx %zu has another DNS dictionary", i);
+  }
+  // ids referenced by a group-by key of a DNS family, on any ctx (after every submitted
+  // batch is aggregated and every deferred list folded)
+  std::vector<char> live(c0->dns.size(), 0);
+  for (size_t i = 0; i < n; ++i) {
+    gpuagg_ctx *c = ctxs[i];
+    int rc = gpuagg_sync(c);
+    if (rc) return rc;
+    bool any_dns = false;
+    for (const Group &g : c->groups) any_dns |= g.sparse && (g.family == FAM_DNS_REQ || g.family == FAM_DNS_RESP);
+    if (!any_dns || !c->sparse_slots) continue;
+    if (c->export_cap < c->sparse_slots) {
+      dev_free(c, c->d_export);
+      c->export_cap = 0;
+      if ((rc = dev_alloc(c, &c->d_export, c->sparse_slots * kSparseEntryWords))) return rc;
+      c->export_cap = c->sparse_slots;
+    }
+    size_t nent = 0;
+    if ((rc = gpuagg_sparse_export(c, c->d_export, c->export_cap, &nent))) return rc;
+    std::vector<uint64_t> ent(nent * kSparseEntryWords);
+    if (nent) HIPCHK(c, x_copy(c, ent.data(), c->d_export, ent.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t e = 0; e < nent; ++e) {
+      const uint64_t *w = &ent[e * kSparseEntryWords];
+      const uint32_t grp = key_group(w[0]);
+      if (grp >= c->groups.size()) continue;
+      const uint8_t fam = c->groups[grp].family;
+      if (fam != FAM_DNS_REQ && fam != FAM_DNS_RESP) continue;
+      const uint32_t id = key_dns(w[2]);
+      if (id < live.size()) live[id] = 1;
+    }
+  }
+  // two phases: an id unreferenced now turns idle; one still unreferenced (and not handed
+  // out again) at the next call is retired -- a record converted with it before this call
+  // and submitted after it still finds its payload
+  std::vector<uint32_t> dead, idle;
+  for (uint32_t id = 0; id < c0->dns.size(); ++id) {
+    if (!c0->dns[id].in_use || live[id]) continue;
+    (c0->dns[id].idle ? dead : idle).push_back(id);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    gpuagg_ctx *c = ctxs[i];
+    if (i && c == c0) continue;
+    for (uint32_t id = 0; id < c->dns.size(); ++id) c->dns[id].idle = false;
+    for (uint32_t id : idle) c->dns[id].idle = true;
+    for (uint32_t id : dead) {
+      DnsAttr &a = c->dns[id];
+      c->dns_ids.erase(dns_key(a.rcode, a.qtypes, a.query, a.ips, a.nresp));
+      a = DnsAttr{};
+      a.in_use = false;
+      c->free_dns.push_back(id);
+    }
+    std::sort(c->free_dns.begin(), c->free_dns.end(), std::greater<uint32_t>());  // lowest id first
+    c->free_dns.erase(std::unique(c->free_dns.begin(), c->free_dns.end()), c->free_dns.end());
+    if (!dead.empty()) dns_canon_rebuild(c);
+  }
+  for (size_t k = 0; k < dead.size() && k < cap; ++k) ids[k] = dead[k];
+  if (n_retired) *n_retired = dead.size();
   return GPUAGG_OK;
 }
 
@@ -3379,6 +3494,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
     for (unsigned q = 0; q < T; ++q) parts[t][q].clear();
   }
   std::vector<int> err(T, GPUAGG_OK);
+  std::vector<uint64_t> dead_dns(T, 0);  // entries of retired DNS ids: not rendered, counted as lost
   auto run = [&](auto &&fn) {  // fn(t) on T threads
     if (T == 1) {
       fn(0u);
@@ -3411,6 +3527,10 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
         case FAM_DNS_REQ:
         case FAM_DNS_RESP: {
           const uint32_t id = key_dns(w[2]);
+          if (id < c->dns.size() && !c->dns[id].in_use) {  // a retired id in a late record
+            ++dead_dns[t];
+            continue;
+          }
           if (id >= c->dns.size()) {
             err[t] = GPUAGG_EINVAL;
             return;
@@ -3461,6 +3581,7 @@ int render_series(gpuagg_ctx *c, const std::vector<uint64_t> &dc, const std::vec
   });
   for (int e : err)
     if (e) return fail(c, e, "snapshot: a group-by key names a dns_id that was not interned");
+  for (uint64_t d : dead_dns) r->dropped += d;
   // per partition: sum equal keys, then render each distinct key's series into the
   // partition's arena
   auto &out = c->agg_scratch.out;
@@ -4418,7 +4539,8 @@ int gpuagg_merge(gpuagg_ctx *const *ctxs, size_t n) {
              ci->slots[k].wk_kind == c0->slots[k].wk_kind && ci->slots[k].wk_name == c0->slots[k].wk_name &&
              ci->slots[k].has_owner == c0->slots[k].has_owner && ci->slots[k].in_use == c0->slots[k].in_use;
     for (size_t k = 0; same && k < c0->dns.size(); ++k)
-      same = ci->dns[k].rcode == c0->dns[k].rcode && ci->dns[k].nresp == c0->dns[k].nresp &&
+      same = ci->dns[k].in_use == c0->dns[k].in_use && ci->dns[k].rcode == c0->dns[k].rcode &&
+             ci->dns[k].nresp == c0->dns[k].nresp &&
              ci->dns[k].qtypes == c0->dns[k].qtypes && ci->dns[k].query == c0->dns[k].query &&
              ci->dns[k].ips == c0->dns[k].ips;
     if (!same)

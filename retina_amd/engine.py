@@ -220,9 +220,22 @@ class GpuAgg:
         self._check(self.lib.gpuagg_dns_intern(self.h, rcode, ",".join(qtypes).encode(),
                                                query.encode(), ",".join(ips).encode(),
                                                num_answers, C.byref(out)))
+        self._dns_hwm = max(getattr(self, "_dns_hwm", 0), out.value + 1)  # ids < hwm
         return out.value
 
+    def dns_retire(self, others: Sequence["GpuAgg"] = ()) -> List[int]:
+        """gpuagg_dns_retire over this engine and `others` (one dictionary interned alike on
+        each): the DNS ids no group-by key references any more, now free for reuse."""
+        ctxs = [self] + list(others)
+        arr = (C.c_void_p * len(ctxs))(*[e.h for e in ctxs])
+        cap = max(1, getattr(self, "_dns_hwm", 0))  # every id ever handed out is below it
+        ids = (C.c_uint32 * cap)()
+        n = C.c_size_t()
+        self._check(self.lib.gpuagg_dns_retire(arr, len(ctxs), ids, cap, C.byref(n)))
+        return list(ids[:n.value])
+
     # -- records -----------------------------------------------------------------------
+
     def alloc_batch(self, capacity: int) -> HostBatch:
         p = C.POINTER(_abi.Batch)()
         self._check(self.lib.gpuagg_alloc_batch(self.h, capacity, C.byref(p)))
