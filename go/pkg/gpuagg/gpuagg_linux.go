@@ -33,6 +33,8 @@ import (
 	"io"
 	"math/bits"
 	"net"
+	"os"
+	"strconv"
 	"strings"
 	"sync"
 	"time"
@@ -59,7 +61,14 @@ import (
 
 const (
 	name          = "gpuagg"
-	batchCapacity = 1 << 22 // records per pinned batch / feed staging: a launch's fixed cost (LDS image fill, staged bins) over 4M records
+	// Pinned host memory per device (INTEGRATION.md "Memory and threads"): each feed keeps
+	// two stagings per device.  The packetparser feed carries the traffic: its stagings of
+	// 2^22 samples spread a launch's fixed cost (LDS image fill, staged bins) over 4M
+	// records; drops, decoded records and the enriched-flow batch are far rarer and get
+	// 2^20.  Per device: 2 x 2^22 x 72 B + 2 x 2^20 x 32 B + 2 x 2^20 x 36 B + 2^20 x 36 B
+	// = 0.78 GB (RETINA_GPUAGG_PACKET_STAGING_LOG2 = 20 brings it to 0.29 GB).
+	packetCapacity = 1 << 22 // raw packetparser samples per staging (default)
+	batchCapacity  = 1 << 20 // drop samples / decoded records per staging; enriched-flow batch
 	rawPiece      = 1 << 16 // samples / records buffered in Go before each hand-over to Start
 	flushInterval = 100 * time.Millisecond
 	scrapeEpoch   = 5 * time.Second
@@ -110,6 +119,15 @@ type device struct {
 	n     int
 	cols  [7][]uint32 // src, dst, bytes, meta, ports, dns_id, tcp_id
 	times []uint64
+}
+
+// packetStaging is the packetparser feed's staging size in samples: packetCapacity, or
+// 2^RETINA_GPUAGG_PACKET_STAGING_LOG2 (16..22) for agents under a tight memory limit.
+func packetStaging() int {
+	if v, err := strconv.Atoi(os.Getenv("RETINA_GPUAGG_PACKET_STAGING_LOG2")); err == nil && v >= 16 && v <= 22 {
+		return 1 << v
+	}
+	return packetCapacity
 }
 
 type gpuAgg struct {
@@ -389,8 +407,12 @@ func (g *gpuAgg) Init() error {
 	g.feeds = map[int]*C.gpuagg_raw_feed{}
 	for kind := range rawSize {
 		var f *C.gpuagg_raw_feed
+		capacity := C.size_t(batchCapacity)
+		if kind == RawPacket {
+			capacity = C.size_t(packetStaging())
+		}
 		if err := check(ctxs[0], C.gpuagg_raw_feed_create(&ctxs[0], C.size_t(len(ctxs)), C.int(kind),
-			batchCapacity, &f), "gpuagg_raw_feed_create"); err != nil {
+			capacity, &f), "gpuagg_raw_feed_create"); err != nil {
 			g.destroyLocked()
 			return err
 		}

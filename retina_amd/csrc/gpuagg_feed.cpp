@@ -25,6 +25,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -68,6 +69,9 @@ class Pool {
       f(0u);
       return;
     }
+    // feeds share pools (shared_pool): one job at a time (uncontended under the ABI's
+    // one-thread-per-ctx rule, since the plugin's feeds span the same contexts)
+    std::lock_guard<std::mutex> job(run_mu_);
     fn_ = [](void *p, unsigned t) { (*static_cast<F *>(p))(t); };
     arg_ = &f;
     left_.store(n_ - 1, std::memory_order_relaxed);
@@ -106,11 +110,26 @@ class Pool {
   std::atomic<uint64_t> gen_{0};
   std::atomic<unsigned> left_{0};
   std::atomic<bool> stop_{false};
-  std::mutex m_;
+  std::mutex m_, run_mu_;
   std::condition_variable cv_;
   void (*fn_)(void *, unsigned) = nullptr;
   void *arg_ = nullptr;
 };
+
+// One pool per thread count for the whole process: the Go plugin's packet, drop and record
+// feeds (and any feeds of other plugins) share one set of host threads instead of starting
+// up to 16 spinning threads each.  The last feed that lets go of a pool joins it.
+std::shared_ptr<Pool> shared_pool(unsigned n) {
+  static std::mutex mu;
+  static std::map<unsigned, std::weak_ptr<Pool>> pools;
+  std::lock_guard<std::mutex> g(mu);
+  std::shared_ptr<Pool> p = pools[n].lock();
+  if (!p) {
+    p = std::make_shared<Pool>(n);
+    pools[n] = p;
+  }
+  return p;
+}
 
 inline void split(size_t n, unsigned parts, unsigned t, size_t &lo, size_t &hi) {
   lo = n * t / parts;
@@ -157,7 +176,7 @@ struct gpuagg_raw_feed {
   int mode = GPUAGG_FEED_RAW_DMA;
   size_t rec = 0, cap = 0;  // bytes per input record, records per staging
   std::vector<Dev> dev;
-  std::unique_ptr<Pool> pool;
+  std::shared_ptr<Pool> pool;
   std::vector<uint16_t> shard;  // device of each record of a piece (several devices)
   std::vector<size_t> cnt;      // [thread][device]: records, then write positions
   std::vector<std::unique_ptr<Tile>> tiles;  // [thread][device]
@@ -221,7 +240,7 @@ void free_all(Feed *f) {
 
 void set_threads(Feed *f, unsigned t) {
   t = std::max(1u, std::min(t, kMaxFeedThreads));
-  if (!f->pool || f->pool->size() != t) f->pool.reset(new Pool(t));
+  if (!f->pool || f->pool->size() != t) f->pool = shared_pool(t);
   f->cnt.assign((size_t)t * f->dev.size(), 0);
   f->tiles.resize((size_t)t * f->dev.size());
   for (auto &p : f->tiles)
@@ -235,10 +254,10 @@ int submit_stage(Feed *f, Feed::Dev &D, size_t n) {
   if (!n) return GPUAGG_OK;
   const int rc = f->soa() ? gx_submit_batch_async(D.c, s.bat, n, s.done)
                           : gx_submit_raw_async(D.c, f->kind, s.raw, n, s.done);
-  if (rc == GPUAGG_OK) {
-    D.submitted += n;
-    s.pending = !gx_is_cpu(D.c);
-  }
+  if (rc == GPUAGG_OK) D.submitted += n;
+  // even when the launch failed, the H2D copies out of this staging may be enqueued (and
+  // s.done recorded behind them): it is not refilled or freed before that event
+  s.pending = !gx_is_cpu(D.c);
   return rc;
 }
 
@@ -451,7 +470,10 @@ int gpuagg_raw_feed_configure(gpuagg_raw_feed *f, uint32_t threads, int mode) {
   if (f->kind != GPUAGG_RECORD && mode != f->mode) {
     free_all(f);
     f->mode = mode;
-    if (int rc = alloc_all(f)) return rc;
+    if (int rc = alloc_all(f)) {
+      f->dead = true;  // partial stagings: later puts / flushes return GPUAGG_ESTATE
+      return rc;
+    }
   }
   return GPUAGG_OK;
 }

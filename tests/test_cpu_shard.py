@@ -220,3 +220,29 @@ def test_record_feed_scatter(lib, world, cap):
         feed.close()
         for g in engines:
             g.close()
+
+
+def test_feeds_share_one_thread_pool(lib):
+    """The plugin's packet, drop and record feeds over the same contexts share one pool of
+    host threads (three pools of up to 16 spinning threads each before), and the
+    shared pool still scatters every feed's records exactly."""
+    import os
+    from retina_amd import RawFeed, _abi
+    from .helpers import make_engine
+    pods = W.make_pods(80, seed=47)
+    sp = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+    engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(2)]
+    threads = lambda: len(os.listdir("/proc/self/task"))  # noqa: E731
+    before = threads()
+    feeds = [RawFeed(engines, kind, capacity=2_048, threads=6)
+             for kind in (_abi.RAW_PACKET, _abi.RAW_DROP, _abi.RECORD)]
+    assert threads() - before == 5  # one pool of 6: the caller's thread + 5 workers
+    raw = W.gen_raw_packets(5_000, pods, seed=48)
+    feeds[0].put(raw)
+    feeds[0].flush()
+    assert sum(feeds[0].submitted()) == 5_000
+    for f in feeds:
+        f.close()
+    assert threads() == before  # the last feed joined the pool's workers
+    for e in engines:
+        e.close()
