@@ -179,14 +179,16 @@ def pmc_traffic(cfg_name: str, kernel: str, build_id: str):
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 
 
-# The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go: batchCapacity = 1 << 22
-# records per pinned batch / feed staging, submitted when full or every flushInterval =
-# 100 ms; 2^20 until round 5).
+# The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go): the packetparser feed's
+# stagings hold packetCapacity = 2^22 raw samples (the traffic path; submitted when full or
+# every flushInterval = 100 ms), decoded records and drops batchCapacity = 2^20 (round 6;
+# every feed took 2^22 in round 5, 2^20 before).
 GO_BATCH = 1 << 22
+RECORD_BATCH = 1 << 20
 
 
-def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = GO_BATCH):
-    """Host-fed throughput at the Go plugin's batch size: two pinned batches (pre-filled
+def host_fed_rate(g, cols, n_total: int, steps: int, batch: int = RECORD_BATCH):
+    """Host-fed throughput at the Go plugin's decoded-record batch size: two pinned batches (pre-filled
     from the workload) submitted alternately through gpuagg_submit, the H2D copy of one
     overlapping the other's aggregation."""
     import torch
@@ -260,6 +262,12 @@ def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 12, batch: int = 
         # (stagings of batch / 4 records here: 8 contexts x 2 stagings of 72-byte samples)
         shard8 = {name: {str(t): run([g] + extra, mode, t, batches // 2, batch // 4) for t in (4, 8, 16)}
                   for name, mode in (("host_decode", _abi.FEED_HOST_DECODE), ("raw_dma", _abi.FEED_RAW_DMA))}
+        # the host side alone (FEED_DRY_RUN: stagings counted, never copied or aggregated):
+        # what the node's CPU can shard + scatter (+ decode) into 8 devices' pinned stagings
+        # when every device has its own PCIe link
+        shard8_host = {name: {str(t): run([g] + extra, mode | _abi.FEED_DRY_RUN, t, batches // 2, batch // 4)
+                              for t in (1, 4, 8, 16)}
+                       for name, mode in (("host_decode", _abi.FEED_HOST_DECODE), ("raw_dma", _abi.FEED_RAW_DMA))}
     finally:
         for e in extra:
             e.close()
@@ -274,11 +282,13 @@ def host_fed_raw_rate(g, pods, spec, seed: int, batches: int = 12, batch: int = 
     return {"value": modes["raw_dma"]["4"], "unit": "records/s", "batch_records": batch, "batches": batches,
             "piece_records": piece, "record_bytes": 72, "feed_threads": 4, "feed_mode": "raw_dma", "modes": modes,
             "best": {"mode": best[0], "threads": int(best[1]), "value": modes[best[0]][best[1]]},
-            "shard8": shard8, "shard_rate_8_devices": shard_rate,
+            "shard8": shard8, "shard8_host_only": shard8_host, "shard_rate_8_devices": shard_rate,
             "note": "raw packetparser samples through gpuagg_raw_feed_put in 2^16-sample pieces, 2 pinned 2^22-record "
                     "stagings per context, async H2D -- the Go plugin's real raw path; PCIe included, not `value`. "
                     "value = the feed's defaults (raw_dma, 4 threads); modes = records/s by mode and feed threads; shard8 = "
-                    "one feed over 8 contexts of this GPU; shard_rate_8_devices = gpuagg_shard_raw (threaded) samples/s"}
+                    "one feed over 8 contexts of this GPU; shard8_host_only = the same with the DMA and aggregation out of the "
+                    "loop (GPUAGG_FEED_DRY_RUN: the host's shard + scatter + decode ceiling for an 8-GPU node); "
+                    "shard_rate_8_devices = gpuagg_shard_raw (threaded) samples/s"}
 
 
 def production_geometry(g, cols, n_total: int, bpr: int, full_kernel_ms: float, launches: int = 100,

@@ -321,6 +321,10 @@ typedef struct gpuagg_record {
 typedef struct gpuagg_raw_feed gpuagg_raw_feed;
 #define GPUAGG_FEED_HOST_DECODE 0
 #define GPUAGG_FEED_RAW_DMA 1
+/* or'ed into a mode (diagnostics): full stagings are counted as submitted but never copied
+ * or aggregated -- the host side alone (shard, scatter, host decode into pinned memory),
+ * for the node-level host ceiling with the DMA out of the loop */
+#define GPUAGG_FEED_DRY_RUN 0x100
 /* kind: GPUAGG_RAW_PACKET / GPUAGG_RAW_DROP (perf samples) or GPUAGG_RECORD (gpuagg_record) */
 int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size_t capacity,
                            gpuagg_raw_feed **out);

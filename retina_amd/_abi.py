@@ -90,6 +90,7 @@ RAW_PACKET, RAW_DROP = 1, 2          # GPUAGG_RAW_* (include/gpuagg.h)
 RECORD = 3  # GPUAGG_RECORD: decoded records, struct gpuagg_record (40 bytes)
 RAW_SIZE = {RAW_PACKET: 72, RAW_DROP: 32, RECORD: 40}
 FEED_HOST_DECODE, FEED_RAW_DMA = 0, 1  # GPUAGG_FEED_* (gpuagg_raw_feed_configure)
+FEED_DRY_RUN = 0x100  # or'ed into a mode: stagings counted, never submitted (diagnostics)
 LAT_SUM_WORDS = 35  # gpuagg_state_desc.latency: words [0, 35) sum, the rest max (gpuagg.h)
 
 

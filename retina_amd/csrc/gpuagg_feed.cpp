@@ -174,6 +174,7 @@ struct gpuagg_raw_feed {
   };
   int kind = 0;
   int mode = GPUAGG_FEED_RAW_DMA;
+  bool dry = false;  // GPUAGG_FEED_DRY_RUN: stagings counted, never submitted (diagnostics)
   size_t rec = 0, cap = 0;  // bytes per input record, records per staging
   std::vector<Dev> dev;
   std::shared_ptr<Pool> pool;
@@ -252,6 +253,10 @@ int submit_stage(Feed *f, Feed::Dev &D, size_t n) {
   Feed::Stage &s = D.st[D.cur];
   D.cur ^= 1;
   if (!n) return GPUAGG_OK;
+  if (f->dry) {
+    D.submitted += n;
+    return GPUAGG_OK;
+  }
   const int rc = f->soa() ? gx_submit_batch_async(D.c, s.bat, n, s.done)
                           : gx_submit_raw_async(D.c, f->kind, s.raw, n, s.done);
   if (rc == GPUAGG_OK) D.submitted += n;
@@ -462,11 +467,14 @@ int gpuagg_raw_feed_create(gpuagg_ctx *const *ctxs, size_t n_ctx, int kind, size
 }
 
 int gpuagg_raw_feed_configure(gpuagg_raw_feed *f, uint32_t threads, int mode) {
+  const bool dry = mode & GPUAGG_FEED_DRY_RUN;
+  mode &= ~GPUAGG_FEED_DRY_RUN;
   if (!f || (mode != GPUAGG_FEED_HOST_DECODE && mode != GPUAGG_FEED_RAW_DMA)) return GPUAGG_EINVAL;
   if (f->dead) return GPUAGG_ESTATE;
   for (auto &D : f->dev)
     if (D.fill) return gx_fail(D.c, GPUAGG_ESTATE, "gpuagg_raw_feed_configure: flush the feed first");
   if (threads) set_threads(f, threads);
+  f->dry = dry;
   if (f->kind != GPUAGG_RECORD && mode != f->mode) {
     free_all(f);
     f->mode = mode;

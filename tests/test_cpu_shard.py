@@ -246,3 +246,28 @@ def test_feeds_share_one_thread_pool(lib):
     assert threads() == before  # the last feed joined the pool's workers
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_raw_feed_dry_run_counts_only(lib, mode):
+    """GPUAGG_FEED_DRY_RUN (the bench's host-only ceiling): every record is sharded and
+    counted as submitted, nothing is aggregated; a later configure without it feeds again."""
+    from retina_amd import RawFeed, _abi
+    from .helpers import make_engine
+    pods = W.make_pods(60, seed=49)
+    sp = [{"metric_name": "forward_count", "source_labels": ["namespace", "podname"]}]
+    engines = [make_engine(pods, sp, False, flags=_abi.FLAG_CPU_BACKEND) for _ in range(3)]
+    raw = W.gen_raw_packets(9_000, pods, seed=50)
+    feed = RawFeed(engines, _abi.RAW_PACKET, capacity=1_024, threads=3, mode=mode | _abi.FEED_DRY_RUN)
+    feed.put(raw)
+    feed.flush()
+    assert sum(feed.submitted()) == 9_000
+    assert all(e.snapshot() == {} for e in engines)
+    feed.configure(3, mode)
+    feed.put(raw)
+    feed.flush()
+    assert sum(feed.submitted()) == 18_000
+    assert any(e.snapshot() for e in engines)
+    feed.close()
+    for e in engines:
+        e.close()
