@@ -179,6 +179,48 @@ def pmc_traffic(cfg_name: str, kernel: str, build_id: str):
     return pmc.get("hbm_bytes_per_launch_corrected"), os.path.relpath(path, ROOT)
 
 
+# Secondary ceilings of MI355X measured by scripts/microbench_bounds.hip on the box
+# (profiles/round6/r6b_bounds.jsonl), for the kernels that are not HBM-streaming-bound:
+SECONDARY_PEAKS = {
+    # random u32 adds into a 64 KiB LDS array, one 1024-thread workgroup per CU (ds_add_u32)
+    "lds_atomic": {"peak": 4.46e12, "unit": "lane atomics/s"},
+    # random 4-byte loads from an L2-resident 1 MiB table (one L2 request each)
+    "l2_gather": {"peak": 2.73e11, "unit": "L2 requests/s"},
+    # the LDS array's cycles: SQ_LDS_IDX_ACTIVE over the CUs' cycles of the launch
+    "lds_array": {"peak": 1.0, "unit": "busy fraction"},
+}
+N_CU, N_XCD = 256, 8
+
+
+def secondary_bounds(pmc_path, kernel_ms: float):
+    """The dominant kernel's use of its non-HBM resources against SECONDARY_PEAKS, from the
+    same PMC file (and build) as `traffic`: LDS atomics (SQ_INSTS_LDS_ATOMIC x 64 lanes),
+    L2 requests (TCC_HIT + TCC_MISS) and LDS-array busy cycles (SQ_LDS_IDX_ACTIVE over
+    CUs x GRBM_GUI_ACTIVE / XCDs), per launch over the kernel's HIP-event time.  `bound` is
+    the resource with the largest fraction."""
+    try:
+        c = json.load(open(os.path.join(ROOT, pmc_path)))["counters_avg_per_dispatch"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    s = kernel_ms * 1e-3
+    out = {}
+    if "SQ_INSTS_LDS_ATOMIC" in c:
+        a = c["SQ_INSTS_LDS_ATOMIC"] * 64 / s
+        out["lds_atomic"] = {"achieved": a, "frac": a / SECONDARY_PEAKS["lds_atomic"]["peak"]}
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        a = (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]) / s
+        out["l2_gather"] = {"achieved": a, "frac": a / SECONDARY_PEAKS["l2_gather"]["peak"]}
+    if c.get("SQ_LDS_IDX_ACTIVE") and c.get("GRBM_GUI_ACTIVE"):
+        a = c["SQ_LDS_IDX_ACTIVE"] / (N_CU * c["GRBM_GUI_ACTIVE"] / N_XCD)
+        out["lds_array"] = {"achieved": a, "frac": a}
+    for k, v in out.items():
+        v.update(peak=SECONDARY_PEAKS[k]["peak"], unit=SECONDARY_PEAKS[k]["unit"])
+    if out:
+        out["bound"] = max((k for k in out), key=lambda k: out[k]["frac"])
+        out["source"] = "%s + profiles/round6/r6b_bounds.jsonl" % pmc_path
+    return out
+
+
 # The Go plugin's batch geometry (go/pkg/gpuagg/gpuagg_linux.go): the packetparser feed's
 # stagings hold packetCapacity = 2^22 raw samples (the traffic path; submitted when full or
 # every flushInterval = 100 ms), decoded records and drops batchCapacity = 2^20 (round 6;
@@ -684,6 +726,7 @@ def main():
             "other_kernels_ms": other_ms,
             "bytes_per_record": dom_bpr,
             "step_bytes_per_record": bpr,
+            "secondary": secondary_bounds(traffic_src, dom_ms) if traffic is not None else None,
         },
         "build_id": build_id,
         "settle": {"launches": settle_n, "s": settle_s,
