@@ -20,6 +20,10 @@ def rep(old, new, count=1):
 k0 = s.index("__global__ __launch_bounds__(1024) void dense_lds_kernel(KArgs a)")
 head, body = s[:k0], s[k0:]
 s = body
+if "noqflush" in what:  # records are queued, the full queue is dropped
+    rep("""        if (full) {
+          q_flush(true);""", """        if (full) {
+          if (a.n == 3) q_flush(true);""")
 if "nospill" in what:
     rep("      l4_records<NG, SIG, 4, 1>(G, l4, ds, by, me, ss, sd);\n",
         "      l4_records<NG, SIG, 4, 1>(G, l4, ds, by, me, ss, sd);\n      if (a.n) continue;\n")
@@ -31,6 +35,14 @@ if "nolookup" in what:
         "#pragma unroll\n      for (int q = 0; q < 8; ++q) sl[q] = act ? ((ip[q] * 2654435761u) >> 16) % 10000u : kIplNoSlot;")
 body = s
 s = head
+if "nostore" in what:  # spill_put reserves and returns without the store
+    rep("""      spill[mul_u24(w, spill_cap) + pos] = entry(bin, nbytes);
+      return;
+    }
+    atomicAdd(&d.cnt[bin], 1ULL);""", """      if (pos == 0xFFFFFFFFu) spill[mul_u24(w, spill_cap) + pos] = entry(bin, nbytes);
+      return;
+    }
+    atomicAdd(&d.cnt[bin], 1ULL);""")
 if "noatomic" in what:
     rep("          od[k] = atomicAdd(&l4.bins[vd[k] ? bd[k] : l4.dummy], add);\n"
         "          os[k] = atomicAdd(&l4.bins[vs[k] ? bs[k] : l4.dummy], add);",
