@@ -188,3 +188,50 @@ def test_two_rank_latency_merge(gpu_device):
     assert got["no_response"] + got["pending"] + rest["pending"] == want["no_response"] + want["pending"]
     assert rest["latency_count"] == 0 and rest["no_response"] == 0
     assert want["latency_count"] > 0
+
+
+def _nccl_worker(port, q):
+    """merge_engine over RCCL (backend "nccl") with one rank: the reduce / all-gather calls
+    run on the engine's device memory through __cuda_array_interface__ views, as on an
+    8-GPU node; with one rank the merged state must be the engine's own."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from retina_amd import dist as D
+    try:
+        torch.cuda.set_device(0)  # the device first, then the group (bench.py's order)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        pods, recs = _data()
+        out = []
+        for remote, spec, kw in ((False, LOCAL_SPEC, SKETCH), (True, W.C1_REMOTE, {})):
+            from retina_amd import GpuAgg
+            g = make_engine(pods, spec, remote, 0, recs, sparse_capacity_log2=21, **kw)
+            g.submit_device(GpuAgg.device_columns(*to_device(recs, 0)), len(recs))
+            g.sync()
+            before = (g.snapshot(), g.cms_array() if kw else None, g.hll_array() if kw else None)
+            D.merge_engine(g)
+            D.merge_engine(g)  # a second epoch merge: communicators reused
+            after = (g.snapshot(), g.cms_array() if kw else None, g.hll_array() if kw else None)
+            g.close()
+            out.append((before[0] == after[0] and len(before[0]) > 0,
+                        kw == {} or (np.array_equal(before[1], after[1]) and np.array_equal(before[2], after[2]))))
+        q.put(("ok", out))
+    except Exception as e:
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_merge_engine_over_rccl_single_rank(gpu_device):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    status, out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert status == "ok", out
+    assert p.exitcode == 0
+    assert all(a and b for a, b in out), out
