@@ -935,9 +935,13 @@ constexpr uint32_t kCmsWindowShift = 15, kCmsMaxWindows = 4096;
 // pod-in-window in 8 bits and the register index in 18, so p <= 17 and shift <= 8)
 constexpr uint32_t kHllWindowLog2Bytes = 17, kHllMaxWindows = 8192;
 
-// Records per scatter workgroup between deferred sketch folds (256 launches of the Go
-// plugin's 2^20-record batches over 256 workgroups; ~3.8 GB of lists at C3's geometry).
-constexpr uint64_t kSketchDeferRecords = 1ull << 20;
+// Records per scatter workgroup between deferred sketch folds: 8 full-size C3 launches
+// (2^27 records over 256 workgroups), 256 of the Go plugin's 2^22-record batches; ~15 GB of
+// lists at C3's geometry (d = 4, 256 workgroups), plus the HLL re-bucketing lists at the
+// fold.  Each fold rewrites the whole HLL register array and every count-min row, so fewer,
+// larger folds pay that once per 8 launches instead of once per 2: C3 step 2.41 -> 2.30 ms
+// (2^20 until round 6; 2^21: 2.37; profiles/round6/exp/r6k_c3_sketch_defer_budget_ab.jsonl).
+constexpr uint64_t kSketchDeferRecords = 1ull << 22;
 
 // HLL level-2 (split) lists for `records` scatter entries at most: m / (nsup * b2 * nfine)
 // per list, +25 % + 64 of headroom (a full list applies the update with the global CAS).

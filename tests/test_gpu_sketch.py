@@ -141,9 +141,9 @@ def test_c3_full_shape_bit_exact(gpu_device):
 @pytest.mark.parametrize("flags", [0, 8], ids=["deferred", "per-batch"])
 def test_deferred_sketch_folds_exact(gpu_device, flags):
     """Small launches (the Go plugin's batch geometry) defer their count-min / HLL folds:
-    the scatters append to one set of lists sized for 2^20 records per workgroup and
+    the scatters append to one set of lists sized for 2^22 records per workgroup and
     fold_pending folds them once.  Exact against the restatement across mid-stream reads
-    (cms_array / hll_array fold what waits), 258 launches of 2^20 records (the 256-launch
+    (cms_array / hll_array fold what waits), 1026 launches of 2^20 records (the 1024-launch
     budget overflows and folds; the batch is resubmitted, so count-min is linear in the
     repeats and HLL idempotent), ragged launches and a slot-table growth (relayout folds).
     FLAG_FOLD_PER_BATCH (8) keeps per-launch folds as the reference point."""
@@ -178,11 +178,11 @@ def test_deferred_sketch_folds_exact(gpu_device, flags):
         check("after 6 small launches")
         big = W.gen_records(1 << 20, pods, seed=5300, udp_frac=0.2)
         cols = GpuAgg.device_columns(*to_device(big, gpu_device))
-        for _ in range(258):
+        for _ in range(1026):
             g.submit_device(cols, 1 << 20)
-        expect(big, pods, 258)
-        total += 258 << 20
-        check("after 258 launches of 2^20")
+        expect(big, pods, 1026)
+        total += 1026 << 20
+        check("after 1026 launches of 2^20")
         g.load_endpoints(more.endpoints[len(pods.endpoints):], version=2)
         for k in range(3):
             r = W.gen_records(50_000, more, seed=5400 + k, udp_frac=0.2)
