@@ -323,7 +323,10 @@ __global__ __launch_bounds__(kLatThreads) void lat_walk_kernel(LatArgs a, uint32
   }
 }
 
-__global__ void lat_finish_kernel(unsigned long long *st, const int32_t *max_live, uint64_t limit) {
+__global__ void lat_finish_kernel(unsigned long long *st, const int32_t *max_live, uint64_t limit,
+                                  uint32_t guard) {
+  // guard: a capacity-bound batch is finished after its host replay (lat_resolve)
+  if (guard && max_live && *max_live > (int64_t)limit) return;
   st[kLatSeqBase] += st[kLatEvents] - st[kLatPending];
   st[kLatClock] = st[kLatClockEnd];
   st[kLatPending] = st[kLatCarryOut];
@@ -407,9 +410,9 @@ hipError_t launch_latency_walk(const LatArgs &a, size_t n_events, uint32_t enabl
   return hipGetLastError();
 }
 
-hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, hipStream_t st) {
+hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, bool guard, hipStream_t st) {
   hipLaunchKernelGGL(lat_finish_kernel, dim3(1), dim3(1), 0, st, a.state, n_events ? a.max_live : nullptr,
-                     a.limit);
+                     a.limit, guard ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -218,7 +218,9 @@ hipError_t latency_carry_order(const LatEvent *carry, size_t n, unsigned long lo
 hipError_t launch_latency_check(const LatArgs &a, size_t n_events, void *tmp, size_t tmp_bytes,
                                 uint32_t enabled, hipStream_t st);
 hipError_t launch_latency_walk(const LatArgs &a, size_t n_events, uint32_t enabled, hipStream_t st);
-hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, hipStream_t st);
+// guard: return at once when the batch's live-count maximum exceeds the limit (a bound
+// batch is finished after its host replay, lat_resolve)
+hipError_t launch_latency_finish(const LatArgs &a, size_t n_events, bool guard, hipStream_t st);
 
 // Sketch pass (count-min by window partition + HLL), after the metric kernels.
 struct SketchArgs {

@@ -357,6 +357,13 @@ struct gpuagg_ctx {
   uint32_t *d_lat_ovals = nullptr;
   size_t lat_order_alloc = 0;
   uint64_t *h_lat_n = nullptr;   // pinned: state words [kLatPending, kLatEvents] of the batch
+                                 // and, at [kLatReadWords], the batch's live-count maximum
+  // the last batch's capacity decision, read at the next synchronisation (lat_resolve)
+  struct LatPend {
+    bool active = false;
+    LatArgs a{};
+    uint64_t ne = 0, pend = 0;
+  } lat_pend;
   uint64_t lat_peak_pending = 0; // most requests carried into a batch since the reconcile
   int64_t time_offset = 0;       // ktime.MonotonicOffset added to decoded record times
   uint8_t *d_ipl_all = nullptr;  // every pod IP incl. the apiserver (sketch pass)
@@ -743,11 +750,14 @@ int fold_pending_dense(gpuagg_ctx *c) {
   return GPUAGG_OK;
 }
 
+int lat_resolve(gpuagg_ctx *c);
+
 int fold_pending(gpuagg_ctx *c) {
   if (c->cpu) {  // the host threads' accumulators into the ctx's counters and table
     c->cpu->flush();
     return GPUAGG_OK;
   }
+  if (int rc = lat_resolve(c)) return rc;
   if (int rc = fold_pending_sketch(c)) return rc;
   return fold_pending_dense(c);
 }
@@ -1158,6 +1168,11 @@ int launch_sketches(gpuagg_ctx *c, const ColsView &cv, size_t n) {
 // Latency state: `full` (reconcile) also drops the clock and the pending requests;
 // otherwise (epoch reset after a merge) only the histograms and no_response restart.
 int lat_reset(gpuagg_ctx *c, bool full) {
+  if (full) {
+    c->lat_pend.active = false;  // a new TTL cache: the last batch's decision no longer matters
+  } else if (int rc = lat_resolve(c)) {
+    return rc;
+  }
   if (!c->d_lat) {
     if (!c->lat_enabled) return GPUAGG_OK;
     if (int rc = dev_alloc(c, &c->d_lat, kLatStateWords)) return rc;
@@ -1332,6 +1347,7 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   if (!cv.ports || !cv.tcp_id || !cv.time_ns)
     return fail(c, GPUAGG_EINVAL, "node-apiserver latency metrics read the ports, tcp_id and time_ns columns");
   if (!c->d_lat && (rc = lat_reset(c, true))) return rc;
+  if ((rc = lat_resolve(c))) return rc;  // the previous batch first (its events are still in place)
   if (c->cpu) {  // the TTL join in record order on the host
     LatArgs a{};
     a.src = cv.src_ip;
@@ -1406,8 +1422,8 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
   a.idx_in = c->d_lat_idx;
   a.idx_out = c->d_lat_idx + c->lat_ev_alloc;
   constexpr size_t kLatReadWords = kLatEvents - kLatPending + 1;
-  if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8 * kLatReadWords, hipHostMallocDefault) != hipSuccess)
-    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", 8 * kLatReadWords);
+  if (!c->h_lat_n && hipHostMalloc((void **)&c->h_lat_n, 8 * (kLatReadWords + 1), hipHostMallocDefault) != hipSuccess)
+    return fail(c, GPUAGG_ENOMEM, "hipHostMalloc(%zu)", 8 * (kLatReadWords + 1));
   a.carry_in = c->d_lat_carry[c->lat_carry_cur];  // copied into the events by the front
   ENQ(c);
   HIPCHK(c, launch_latency_front(a, c->stream));
@@ -1452,19 +1468,43 @@ int launch_latency(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.carry_order = c->d_lat_ovals + pend;
   }
   HIPCHK(c, launch_latency_check(a, ne, c->d_lat_tmp, c->lat_tmp_alloc, c->lat_enabled, c->stream));
-  int32_t max_live = 0;
-  if (ne) {  // the one decision the host takes: does the capacity bind in this batch?
-    HIPCHK(c, x_copy_async(c, &max_live, c->d_lat_max_live, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, x_sync(c, c->stream));
-  }
-  if ((uint64_t)max_live > a.limit) {
-    if ((rc = lat_serial_host(c, a, ne, pend))) return rc;
-  } else {
+  // The one decision the host takes -- does the capacity bind in this batch? -- is not
+  // waited for here (a second blocking sync per batch undid the async submit).
+  // The parallel walk and the finish run guarded on the device (both return at once when
+  // the live-count maximum exceeds the limit), the maximum comes back into pinned memory
+  // behind them, and lat_resolve -- at the next batch, sync, state read, merge or epoch
+  // reset, before anything touches this batch's events -- replays a bound batch on the
+  // host (in event order, as the ttlcache) and finishes it then.
+  c->h_lat_n[kLatReadWords] = 0;
+  if (ne) {
     HIPCHK(c, launch_latency_walk(a, ne, c->lat_enabled, c->stream));
+    HIPCHK(c, x_copy_async(c, &c->h_lat_n[kLatReadWords], c->d_lat_max_live, 4, hipMemcpyDeviceToHost,
+                           c->stream));
   }
-  HIPCHK(c, launch_latency_finish(a, ne, c->stream));
+  HIPCHK(c, launch_latency_finish(a, ne, true, c->stream));
+  c->lat_pend.active = ne != 0;
+  c->lat_pend.a = a;
+  c->lat_pend.ne = ne;
+  c->lat_pend.pend = pend;
   c->lat_carry_cur ^= 1;
   c->lat_carry_bound = ne;
+  return GPUAGG_OK;
+}
+
+// The last latency batch's capacity decision (launch_latency): a batch whose live count
+// passed the limit is replayed on the host and finished.  Nothing between that batch and
+// this call wrote its events, order keys or state words (the next batch calls this first).
+int lat_resolve(gpuagg_ctx *c) {
+  if (!c->lat_pend.active) return GPUAGG_OK;
+  c->lat_pend.active = false;
+  constexpr size_t kLatReadWords = kLatEvents - kLatPending + 1;
+  HIPCHK(c, x_sync(c, c->stream));
+  const int32_t max_live = (int32_t)(uint32_t)c->h_lat_n[kLatReadWords];
+  const LatArgs &a = c->lat_pend.a;
+  if ((uint64_t)(int64_t)max_live <= a.limit) return GPUAGG_OK;  // walked and finished on the device
+  int rc = lat_serial_host(c, a, c->lat_pend.ne, c->lat_pend.pend);
+  if (rc) return rc;
+  HIPCHK(c, launch_latency_finish(a, c->lat_pend.ne, false, c->stream));
   return GPUAGG_OK;
 }
 
@@ -4346,6 +4386,10 @@ int gpuagg_hll_copy(gpuagg_ctx *c, uint8_t *out, size_t n) {
 // ---- multi-GPU merge hooks -----------------------------------------------------------
 int gpuagg_state(gpuagg_ctx *c, gpuagg_state_desc *o) {
   if (!c || !o) return GPUAGG_EINVAL;
+  if (c->lat_pend.active) {  // the latency words below are read by the caller
+    int rc = bind(c);
+    if (rc || (rc = lat_resolve(c))) return rc;
+  }
   if (c->pend.active || c->sk_pend.active) {  // the arrays below are read by the caller: fold what is waiting
     int rc = bind(c);
     if (rc || (rc = fold_pending(c))) return rc;
@@ -4772,6 +4816,7 @@ int gpuagg_latency_read(gpuagg_ctx *c, gpuagg_latency_state *out) {
   *out = gpuagg_latency_state{};
   out->enabled = c->lat_enabled;
   if (!c->d_lat) return GPUAGG_OK;
+  if ((rc = lat_resolve(c))) return rc;
   unsigned long long w[kLatStateWords];
   HIPCHK(c, x_sync(c, c->stream));
   HIPCHK(c, x_copy(c, w, c->d_lat, sizeof w, hipMemcpyDeviceToHost));
