@@ -370,6 +370,13 @@ constexpr uint32_t kWideSegLog2 = 12, kWideMaxLog2 = kWideSegLog2 + 12;
 // updates whose count or bytes do not fit the fields go to the table directly
 constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40, kWideHomeShift = 52;
 static_assert(kWideHomeShift + kWideSegLog2 == 64, "home field fills the word");
+// Narrow entries (plans with no port option and no DNS family, e.g. C1 / C4 remote): the
+// key's port fields (k1 bits 30-63) and DNS id (k2 bits 0-31) are zero, so k1 and k2 pack
+// into one word d_slot1 << 32 | d_ip -- 24 bytes an entry instead of 32
+constexpr uint32_t kWideNarrowWords = 3;
+GA_HD uint64_t wide_pack12(uint64_t k1, uint64_t k2) { return ((k1 >> 9) << 32) | (k2 >> 32); }
+GA_HD uint64_t wide_unpack1(uint64_t n) { return (n >> 32) << 9; }
+GA_HD uint64_t wide_unpack2(uint64_t n) { return (n & 0xFFFFFFFFULL) << 32; }
 constexpr int kSparseEntryWords = 5;  // k0 k1 k2 count bytes
 
 // ---- sketches ---------------------------------------------

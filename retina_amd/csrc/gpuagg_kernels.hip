@@ -75,6 +75,9 @@ struct DevSparse {
   // workgroup, so the keys seen once -- the long tail -- do not take the entries
   uint32_t *door;
   uint32_t door_log2;  // 0: no doorkeeper
+  // wide keys whose port and DNS fields are zero for every group of the plan (no port
+  // option, no DNS family): list entries drop the zero words (wide_entry_words)
+  uint32_t narrow;
 };
 
 // One cached key: tag 0 free, 1 being claimed, 2 published (key words final).
@@ -308,6 +311,11 @@ __device__ __forceinline__ void sparse_add(const DevSparse &s, uint64_t k0, uint
   atomicAdd(s.dropped, c);
 }
 
+// words per segment-list entry: compact key 1, wide 4, narrow wide 3
+__device__ __forceinline__ uint32_t list_entry_words(const DevSparse &s) {
+  return s.compact ? 1u : (s.narrow ? kWideNarrowWords : kWideEntryWords);
+}
+
 // Wide keys (192 bits) through per-segment lists: the update is appended to this
 // workgroup's list for the key's table segment (LDS fill counter, one 32-byte store) and
 // sparse_fold_wide_kernel later adds every list into its segment in LDS -- instead of a
@@ -320,9 +328,17 @@ __device__ __forceinline__ void wide_append(const DevSparse &s, uint64_t kh, uin
     const uint32_t pos = atomicAdd(&s.lctr[w], 1u);
     if (pos < s.lcap) {
       const uint64_t home = (uint64_t)((uint32_t)kh & ((1u << s.seg_log2) - 1u));
+      const uint64_t m = (home << kWideHomeShift) | (c << kWideCountShift) | b;
+      if (s.narrow) {
+        unsigned long long *e = s.lists + ((size_t)w * s.lcap + pos) * kWideNarrowWords;
+        e[0] = k0;
+        e[1] = wide_pack12(k1, k2);
+        e[2] = m;
+        return;
+      }
       ulonglong2 *e = (ulonglong2 *)(s.lists + ((size_t)w * s.lcap + pos) * kWideEntryWords);
       e[0] = make_ulonglong2(k0, k1);
-      e[1] = make_ulonglong2(k2, (home << kWideHomeShift) | (c << kWideCountShift) | b);
+      e[1] = make_ulonglong2(k2, m);
       return;
     }
   }
@@ -926,8 +942,8 @@ __global__ __launch_bounds__(1024) void aggregate_kernel(KArgs a) {
   s.hot_n = a.hot_n;
   s.door = door;
   s.door_log2 = a.door_log2;
-  if (a.sp_lists) {  // this workgroup's lists: compact u64 keys or wide 4-word entries
-    s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * (s.compact ? 1u : kWideEntryWords);
+  if (a.sp_lists) {  // this workgroup's lists: compact u64 keys or wide 4- / 3-word entries
+    s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * list_entry_words(s);
     s.lcap = a.sp_cap;
   }
   for_each_record<kVec>(a, a.p.need_ports || kSketch, a.p.need_dns,
@@ -985,7 +1001,7 @@ __global__ __launch_bounds__(1024) void wide_kernel(KArgs a) {
   s.hot_n = a.hot_n;
   s.door = door;
   s.door_log2 = a.door_log2;
-  s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * kWideEntryWords;
+  s.lists = a.sp_lists + (size_t)blockIdx.x * a.sp_nwin * a.sp_cap * list_entry_words(s);
   s.lcap = a.sp_cap;
   uint32_t fam[NG], sop[NG], dop[NG];
 #pragma unroll
@@ -1184,20 +1200,24 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   }
   __syncthreads();
   auto insert = [&](uint32_t h, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {  // h: home slot
-    {  // the key already sits published in its home slot (the common case under skew): one
-       // round trip of reads (K2 first: published after K1, LDS returns in order), then
-       // no-return adds -- no CAS, no dependent chain
-      const unsigned long long p2 = __hip_atomic_load(&K2[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const unsigned long long p0 = __hip_atomic_load(&K0[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const unsigned long long p1 = K1[h];
-      if (p2 == x2 && p0 == x0 && p1 == x1) {
-        __hip_atomic_fetch_add(&CN[h], (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (b) __hip_atomic_fetch_add(&BY[h], (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return;
-      }
-    }
+    // Every probe first reads the slot: K2, then K0 and K1, issued together (atomic loads
+    // keep their program order; LDS executes a wave's accesses in order and a claimer
+    // publishes K2 after K1, so a published K2 means the K0 / K1 read after it are final).  A key already in
+    // the segment -- every key once the same flows come back -- costs one LDS round trip
+    // per probe and no-return adds; only a free slot takes the CAS claim.  (The claim CAS
+    // on every probe, then two dependent reads, made each probe three round trips, and a
+    // wave waits for its longest probe run: profiles/round6/exp/r6q_*.)
     for (uint32_t probe = 0; probe < N; ++probe) {
       const uint32_t i = (h + probe) & smask;
+      const unsigned long long p2 = __hip_atomic_load(&K2[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned long long p0 = __hip_atomic_load(&K0[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned long long p1 = __hip_atomic_load(&K1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (p2 == x2 && p0 == x0 && p1 == x1) {
+        __hip_atomic_fetch_add(&CN[i], (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (b) __hip_atomic_fetch_add(&BY[i], (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+      }
+      if (p0 != 0ULL) continue;  // another key, or one still being published (it may take two slots)
       const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
       if (cur == 0ULL) {
         K1[i] = x1;
@@ -1228,6 +1248,24 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     const uint32_t l = l0 + threadIdx.x / lpl;
     if (l >= n_lists) continue;
     const uint32_t cnt = counts[(size_t)l * nwin + w];
+    if (s.narrow) {  // 3-word entries (k0, d_slot1 << 32 | d_ip, meta): three 8-byte loads
+      const unsigned long long *e = lists + ((size_t)l * nwin + w) * cap * kWideNarrowWords;
+      auto insn = [&](uint64_t x0, uint64_t n, uint64_t m) {
+        ins(make_ulonglong2(x0, wide_unpack1(n)), make_ulonglong2(wide_unpack2(n), m));
+      };
+      uint32_t k = sub;
+      for (; k + 3 * lpl < cnt; k += 4 * lpl) {
+        unsigned long long v[12];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[3 * q + j] = e[3 * (size_t)(k + q * lpl) + j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) insn(v[3 * q], v[3 * q + 1], v[3 * q + 2]);
+      }
+      for (; k < cnt; k += lpl) insn(e[3 * (size_t)k], e[3 * (size_t)k + 1], e[3 * (size_t)k + 2]);
+      continue;
+    }
     const ulonglong2 *e = (const ulonglong2 *)(lists + ((size_t)l * nwin + w) * cap * kWideEntryWords);
     uint32_t k = sub;
     for (; k + 3 * lpl < cnt; k += 4 * lpl) {
@@ -3009,7 +3047,7 @@ static DevSparse dev_sparse(const SparseView &v) {
   return DevSparse{(unsigned long long *)v.k0, (unsigned long long *)v.k1,
                    (unsigned long long *)v.k2, (unsigned long long *)v.cnt,
                    (unsigned long long *)v.byt, v.mask, (unsigned long long *)v.dropped, v.compact,
-                   v.seg_log2, nullptr, nullptr, 0u};
+                   v.seg_log2, nullptr, nullptr, 0u, nullptr, 0u, nullptr, 0u, v.narrow};
 }
 
 template <class K>

@@ -24,6 +24,7 @@ struct SparseView {
   uint64_t *dropped;
   uint32_t compact;  // 64-bit keys, 2 words (key, count) per slot at k0
   uint32_t seg_log2; // compact: a key probes only its 2^seg_log2-slot segment
+  uint32_t narrow;   // wide keys without port / DNS fields: 24-byte list entries
 };
 
 struct LaunchArgs {

@@ -1728,6 +1728,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
                sp_cap == o.sp_cap && win_shift == o.win_shift;
       }
     };
+    const uint32_t list_words = c->sv.compact ? 1u : (c->sv.narrow ? kWideNarrowWords : kWideEntryWords);
     auto geom = [&](uint64_t budget) {
       Geom g;
       if (c->dense_len > a.lds_bins) {
@@ -1746,8 +1747,8 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
         const uint64_t mean = budget / sp_nwin;
         g.sp_nwin = (uint32_t)sp_nwin;
         uint64_t cap = (mean + mean / 4 + 64 + 1) & ~1ULL;  // even: 16-byte key pairs
-        if (!c->sv.compact)  // 32-byte entries: wide_list_bytes of lists per ctx
-          cap = std::max<uint64_t>(16, c->wide_list_bytes / (8 * kWideEntryWords) / ((uint64_t)a.blocks * sp_nwin)) &
+        if (!c->sv.compact)  // 32- (narrow: 24-) byte entries: wide_list_bytes of lists per ctx
+          cap = std::max<uint64_t>(16, c->wide_list_bytes / (8 * list_words) / ((uint64_t)a.blocks * sp_nwin)) &
                 ~1ULL;
         g.sp_cap = (uint32_t)cap;
       }
@@ -1819,7 +1820,7 @@ int launch(gpuagg_ctx *c, const ColsView &cv, size_t n) {
     a.sp_nwin = 0;
     if (g.sp_nwin) {
       if ((rc = ensure_buf(c, &c->d_sp_lists, &c->sp_lists_alloc,
-                           (size_t)a.blocks * g.sp_nwin * g.sp_cap * (c->sv.compact ? 1u : kWideEntryWords))))
+                           (size_t)a.blocks * g.sp_nwin * g.sp_cap * list_words)))
         return rc;
       if ((rc = ensure_buf(c, &c->d_sp_counts, &c->sp_counts_alloc, (size_t)a.blocks * g.sp_nwin))) return rc;
       a.sp_lists = c->d_sp_lists;
@@ -2324,6 +2325,8 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
       compact &= (groups[g].family == FAM_DNS_REQ || groups[g].family == FAM_DNS_RESP) &&
                  !(groups[g].src_opts & (OPT_IP | OPT_PORT));
   c->sv.compact = compact ? 1u : 0u;
+  // wide keys with no port / DNS fields: 24-byte list entries (kWideNarrowWords)
+  c->sv.narrow = (!compact && !p.need_ports && !p.need_dns && !(c->cfg.flags & GPUAGG_FLAG_WIDE_ENTRIES)) ? 1u : 0u;
   if (c->sparse_slots) {  // probe / fold segments: compact 2^13 slots; wide 2^12 (or the table)
     const uint32_t lg = (uint32_t)__builtin_ctzll(c->sparse_slots);
     c->sv.seg_log2 = compact ? std::min<uint32_t>(lg, kSparseSegLog2)

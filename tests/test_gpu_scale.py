@@ -188,6 +188,11 @@ def test_hot_key_cache_exact(gpu_device, gen):
                                   sparse_capacity_log2=23,
                                   flags=_abi.FLAG_NO_HOT_KEYS | _abi.FLAG_NO_WIDE_LISTS))
     assert a == c, diff_series(a, c)
+    # C1_REMOTE has no port / DNS labels: its lists take 24-byte entries; the 32-byte form
+    # agrees
+    d = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
+                                  sparse_capacity_log2=23, flags=_abi.FLAG_WIDE_ENTRIES))
+    assert a == d, diff_series(a, d)
     r = RefCPU(W.C1_REMOTE, pods.endpoints, True, recs.dns)
     r.process(recs)
     want = r.series()
