@@ -86,8 +86,14 @@ struct HotKey {
 };
 static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp");
 
+// Candidate entries per key.  Entries are never evicted, so a hot key whose candidates are
+// all taken by the time it first comes misses for the rest of the launch and appends every
+// update: with two, C4-remote's workgroups each lost a few top-100 flows that way and some
+// list overflowed in every launch, so every launch folded (a third way: -2.5 % appends,
+// fullest list ~2681 -> ~440 in a 4-workgroup simulation of the bench stream)
+constexpr uint32_t kHotWays = 3;
 // Adds (c, b) to key (k0, k1, k2) (hash h) in this workgroup's LDS hot-key cache if the
-// key is there or a free entry can be claimed (two candidate entries); false: the caller
+// key is there or a free entry can be claimed (kHotWays candidate entries); false: the caller
 // adds to the lists / HBM table.  No lane ever waits: an entry being claimed by another
 // lane is skipped.  Under skew (C4's Zipf flows) the hot keys then cost LDS atomics
 // instead of memory-side atomics serialised on one table slot; the cache is added to the
@@ -96,7 +102,7 @@ static_assert(sizeof(HotKey) == kHotKeyBytes, "LDS sizing in gpuagg_runtime.cpp"
 __device__ __forceinline__ bool hot_add(const DevSparse &s, uint32_t h, uint64_t k0, uint64_t k1, uint64_t k2,
                                         uint64_t c, uint64_t b, bool may_claim) {
 #pragma unroll
-  for (uint32_t q = 0; q < 2; ++q) {
+  for (uint32_t q = 0; q < kHotWays; ++q) {
     HotKey *e = &s.hot[(h + q * 0x9E37u) & (s.hot_n - 1u)];
     unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (t == 0ULL) {
@@ -1101,7 +1107,9 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
   auto insert = [&](unsigned long long key) {
     const uint32_t h = compact_home(s, key);
     // the key already in its home slot (a key is published whole by its claiming CAS):
-    // one read, then the no-return add
+    // one read, then the no-return add.  (Reading every probe first, as the wide fold does,
+    // measured slower here: a compact probe's CAS is one round trip already --
+    // profiles/round6/exp/r6r_c5_*)
     if (__hip_atomic_load(&seg[2 * h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == key) {
       atomicAdd(&seg[2 * h + 1], 1ULL);
       return;
@@ -1150,6 +1158,7 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
 // (a lane that meets a key still being published moves on, so a key may take two slots;
 // the host sums them) -- and the segment is stored back.  Segments no list reaches are
 // not touched.
+constexpr uint32_t kFoldSegLoads = 10;  // 16-byte segment loads per lane in flight (5 * 2^12 / 2 / 1024)
 __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, const unsigned long long *lists,
                                                                 uint32_t *counts, uint32_t n_lists,
                                                                 uint32_t nwin, uint32_t cap, uint32_t *flag,
@@ -1160,7 +1169,9 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     // device-conditional fold: the next launch's flag starts at 0; while the fullest list
     // of the launches since the last fold is below thr, the lists keep growing (the next
     // aggregation launch appends after them).  Atomics: executed at memory, so no XCD's
-    // L2 can hold a stale copy of the flags.
+    // L2 can hold a stale copy of the flags.  (Folding only the segments whose own lists
+    // reached thr, and keeping the rest for later, measured slower at C4-remote: 0.82 ->
+    // 1.19 ms of folds per launch, profiles/round6/exp/r6w_*.)
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&flag[parity ^ 1u], 0u);
     if (thr && atomicOr(&flag[parity], 0u) < thr) return;  // the same value for every workgroup
   }
@@ -1181,22 +1192,29 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   if (!work) return;
   unsigned long long *K0 = seg, *K1 = seg + N, *K2 = seg + 2 * N, *CN = seg + 3 * N, *BY = seg + 4 * N;
   unsigned long long *g = s.k0 + (size_t)kSparseSlotWords * ((size_t)w << s.seg_log2);
-  // coalesced words, 4 loads in flight per lane before their LDS stores
-  const uint32_t nw5 = kSparseSlotWords * N;
-  uint32_t j0 = threadIdx.x;
-  for (; j0 + 3 * blockDim.x < nw5; j0 += 4 * blockDim.x) {
-    unsigned long long v[4];
+  // the segment in 16-byte words (N is even: 5 * N / 2 of them, 16-byte aligned), up to 10
+  // loads per lane in flight -- the whole 160 KiB segment in one round trip at 1024 lanes
+  // -- then scattered field-major into LDS
+  const uint32_t nv = kSparseSlotWords * N / 2;
+  auto field = [&](uint32_t word) -> unsigned long long & {
+    const uint32_t slot = word / kSparseSlotWords;
+    return seg[(word - slot * kSparseSlotWords) * N + slot];
+  };
+  for (uint32_t v0 = threadIdx.x; v0 < nv; v0 += kFoldSegLoads * blockDim.x) {
+    ulonglong2 v[kFoldSegLoads];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = g[j0 + q * blockDim.x];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t j = j0 + q * blockDim.x, slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
-      seg[f * N + slot] = v[q];
+    for (uint32_t q = 0; q < kFoldSegLoads; ++q) {
+      const uint32_t j = v0 + q * blockDim.x;
+      if (j < nv) v[q] = ((const ulonglong2 *)g)[j];
     }
-  }
-  for (; j0 < nw5; j0 += blockDim.x) {
-    const uint32_t slot = j0 / kSparseSlotWords, f = j0 - slot * kSparseSlotWords;
-    seg[f * N + slot] = g[j0];
+#pragma unroll
+    for (uint32_t q = 0; q < kFoldSegLoads; ++q) {
+      const uint32_t j = v0 + q * blockDim.x;
+      if (j < nv) {
+        field(2 * j) = v[q].x;
+        field(2 * j + 1) = v[q].y;
+      }
+    }
   }
   __syncthreads();
   auto insert = [&](uint32_t h, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t c, uint64_t b) {  // h: home slot
@@ -1281,10 +1299,8 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     for (; k < cnt; k += lpl) ins(e[2 * k], e[2 * k + 1]);
   }
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < kSparseSlotWords * N; j += blockDim.x) {
-    const uint32_t slot = j / kSparseSlotWords, f = j - slot * kSparseSlotWords;
-    g[j] = seg[f * N + slot];
-  }
+  for (uint32_t j = threadIdx.x; j < nv; j += blockDim.x)
+    ((ulonglong2 *)g)[j] = make_ulonglong2(field(2 * j), field(2 * j + 1));
   // this segment's lists are folded: empty them for the launches that append next
   for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) counts[(size_t)l * nwin + w] = 0u;
 }
