@@ -612,7 +612,8 @@ def main():
     capacity = {"c1": 21, "c5": 23, "c4-remote": 24}.get(args.config, 16)
     g = GpuAgg(device=dev_index, remote_context=remote, max_slots=cfg["pods"] + 16,
                max_ips=2 * cfg["pods"] + 16, sparse_capacity_log2=capacity,
-               flags=_abi.FLAG_CPU_BACKEND if cpu else 0, **sketch)
+               flags=(_abi.FLAG_CPU_BACKEND if cpu else 0) | int(os.environ.get("GPUAGG_BENCH_FLAGS", "0"), 0),
+               **sketch)  # (GPUAGG_BENCH_FLAGS: diagnostic gpuagg_config.flags for A/B runs)
     g.reconcile(spec)
     g.load_endpoints(pods.endpoints)
     for p in last.dns:
