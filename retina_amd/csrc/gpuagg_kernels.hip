@@ -498,14 +498,45 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {  // converged wave
 // meet in the LDS hot-key cache or append separately and are summed by the fold.  A key
 // may claim a free cache entry on its second sighting in the workgroup (doorkeeper
 // bitmap), so the long tail of keys seen once does not take the entries.
+// The cache is searched first and the doorkeeper asked only when one of the key's ways is
+// still free: a hit -- or a miss once its ways are taken, i.e. most misses after the first
+// records of a launch -- costs no doorkeeper atomic.  (Ways are never freed, so a key
+// cannot sit in a later way while an earlier one is free.)
 __device__ __forceinline__ void wide_insert(const DevSparse &s, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t b) {
   const uint64_t kh = key_hash(k0, k1, k2);
-  bool claim = true;
-  if (s.door_log2) {
-    const uint32_t bit = (uint32_t)(kh >> 40) & ((1u << s.door_log2) - 1u);
-    claim = (atomicOr(&s.door[bit >> 5], 1u << (bit & 31u)) >> (bit & 31u)) & 1u;
+  if (s.hot_n) {
+    const uint32_t h = (uint32_t)kh;
+    HotKey *fe = nullptr;
+#pragma unroll
+    for (uint32_t q = 0; q < kHotWays; ++q) {
+      HotKey *e = &s.hot[(h + q * 0x9E37u) & (s.hot_n - 1u)];
+      const unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (t == 2ULL && e->k0 == k0 && e->k1 == k1 && e->k2 == k2) {
+        atomicAdd(&e->cnt, 1ULL);
+        if (b) atomicAdd(&e->byt, (unsigned long long)b);
+        return;
+      }
+      if (t == 0ULL && !fe) fe = e;
+    }
+    if (fe) {
+      bool claim = true;
+      if (s.door_log2) {
+        const uint32_t bit = (uint32_t)(kh >> 40) & ((1u << s.door_log2) - 1u);
+        claim = (atomicOr(&s.door[bit >> 5], 1u << (bit & 31u)) >> (bit & 31u)) & 1u;
+      }
+      if (claim && atomicCAS(&fe->tag, 0ULL, 1ULL) == 0ULL) {  // claimed: key + first update, publish
+        fe->k0 = k0;
+        fe->k1 = k1;
+        fe->k2 = k2;
+        fe->cnt = 1ULL;
+        fe->byt = b;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&fe->tag, 2ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+      }
+    }
   }
-  if (!(s.hot_n && hot_add(s, (uint32_t)kh, k0, k1, k2, 1, b, claim))) wide_append(s, kh, k0, k1, k2, 1, b);
+  wide_append(s, kh, k0, k1, k2, 1, b);
 }
 
 // Wave-level key de-duplication before the global table (BASELINE.json north_star): the
