@@ -1189,6 +1189,10 @@ __global__ __launch_bounds__(1024) void sparse_fold_kernel(DevSparse s, const un
 // (a lane that meets a key still being published moves on, so a key may take two slots;
 // the host sums them) -- and the segment is stored back.  Segments no list reaches are
 // not touched.
+// re-reads of a slot whose key (same k0) is being published before probing on: a claimer
+// publishes within a few instructions, and the bound keeps every insert finite even if
+// the compiler defers the claimer's stores past the loop
+constexpr uint32_t kFoldSpin = 32;
 constexpr uint32_t kFoldSegLoads = 10;  // 16-byte segment loads per lane in flight (5 * 2^12 / 2 / 1024)
 __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, const unsigned long long *lists,
                                                                 uint32_t *counts, uint32_t n_lists,
@@ -1200,9 +1204,7 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     // device-conditional fold: the next launch's flag starts at 0; while the fullest list
     // of the launches since the last fold is below thr, the lists keep growing (the next
     // aggregation launch appends after them).  Atomics: executed at memory, so no XCD's
-    // L2 can hold a stale copy of the flags.  (Folding only the segments whose own lists
-    // reached thr, and keeping the rest for later, measured slower at C4-remote: 0.82 ->
-    // 1.19 ms of folds per launch, profiles/round6/exp/r6w_*.)
+    // L2 can hold a stale copy of the flags.
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&flag[parity ^ 1u], 0u);
     if (thr && atomicOr(&flag[parity], 0u) < thr) return;  // the same value for every workgroup
   }
@@ -1210,13 +1212,18 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
   uint32_t lpl = 1;
   while (lpl < 64 && lpl * 2 * n_lists <= blockDim.x) lpl *= 2;
   const uint32_t lists_per_round = blockDim.x / lpl, sub = threadIdx.x & (lpl - 1);
-  uint32_t any = 0;
-  for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) any |= counts[(size_t)l * nwin + w];
+  // Per-segment decision: a device-conditional fold (thr > 0) folds only the segments with
+  // a list at thr or beyond; the others keep their lists (and fill counters) for a later
+  // fold, so a segment's 160 KiB pass in and out is paid when its lists are long -- not in
+  // every launch for every segment because one workgroup's list of one segment filled
+  // (C4-remote: a few hot flows miss their cache ways in some workgroups every launch).
   // (a flag word in the segment's LDS: __syncthreads_or would take static LDS beyond the
   // 160 KiB the segment may fill)
+  uint32_t mx = 0;
+  for (uint32_t l = threadIdx.x; l < n_lists; l += blockDim.x) mx = max(mx, counts[(size_t)l * nwin + w]);
   if (threadIdx.x == 0) seg[0] = 0ULL;
   __syncthreads();
-  if (any) seg[0] = 1ULL;
+  if (thr ? mx >= thr : mx != 0u) seg[0] = 1ULL;
   __syncthreads();
   const bool work = seg[0] != 0ULL;
   __syncthreads();
@@ -1256,7 +1263,8 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
     // per probe and no-return adds; only a free slot takes the CAS claim.  (The claim CAS
     // on every probe, then two dependent reads, made each probe three round trips, and a
     // wave waits for its longest probe run: profiles/round6/exp/r6q_*.)
-    for (uint32_t probe = 0; probe < N; ++probe) {
+    uint32_t spin = 0;
+    for (uint32_t probe = 0; probe < N;) {
       const uint32_t i = (h + probe) & smask;
       const unsigned long long p2 = __hip_atomic_load(&K2[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const unsigned long long p0 = __hip_atomic_load(&K0[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1266,33 +1274,112 @@ __global__ __launch_bounds__(1024) void sparse_fold_wide_kernel(DevSparse s, con
         if (b) __hip_atomic_fetch_add(&BY[i], (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
       }
-      if (p0 != 0ULL) continue;  // another key, or one still being published (it may take two slots)
-      const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
-      if (cur == 0ULL) {
-        K1[i] = x1;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __hip_atomic_store(&K2[i], (unsigned long long)x2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // publish
-        atomicAdd(&CN[i], (unsigned long long)c);
-        if (b) atomicAdd(&BY[i], (unsigned long long)b);
-        return;
+      if (p0 == 0ULL) {
+        const unsigned long long cur = atomicCAS(&K0[i], 0ULL, (unsigned long long)x0);
+        if (cur == 0ULL) {
+          K1[i] = x1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&K2[i], (unsigned long long)x2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // publish
+          atomicAdd(&CN[i], (unsigned long long)c);
+          if (b) atomicAdd(&BY[i], (unsigned long long)b);
+          return;
+        }
+        // claimed this instant by a lane with the same k0: read the slot again
+        if (cur == x0 && spin < kFoldSpin) {
+          ++spin;
+          continue;
+        }
+      } else if (p0 == x0 && p2 == kKeyPending && spin < kFoldSpin) {
+        // a key with this k0 still being published: wait for it (bounded) rather than
+        // claiming a second slot -- many lanes meeting one new key used to take a slot each
+        ++spin;
+        continue;
       }
-      if (cur == x0 &&
-          __hip_atomic_load(&K2[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == x2 && K1[i] == x1) {
-        atomicAdd(&CN[i], (unsigned long long)c);
-        if (b) atomicAdd(&BY[i], (unsigned long long)b);
-        return;
-      }
+      ++probe;
     }
     atomicAdd(s.dropped, (unsigned long long)c);
   };
-  // lpl lanes per list, each taking every lpl-th entry (two 16-byte loads per entry); a
-  // lane loads 4 entries before inserting any, so the list reads are in flight together
-  // instead of one HBM round trip per entry
+  // (more than 256 lists: lpl lanes per list, each taking every lpl-th entry; a lane loads 4
+  // entries before inserting any, so the list reads are in flight together instead of one
+  // HBM round trip per entry)
   auto ins = [&](const ulonglong2 &a0, const ulonglong2 &a1) {
     insert((uint32_t)(a1.y >> kWideHomeShift) & smask, a0.x, a0.y, a1.x,
            (a1.y >> kWideCountShift) & ((1ULL << (kWideHomeShift - kWideCountShift)) - 1),
            a1.y & ((1ULL << kWideCountShift) - 1));
   };
+  const uint32_t ew = s.narrow ? kWideNarrowWords : kWideEntryWords;
+  if (n_lists <= 256) {
+    // Balanced: the segment's lists as one concatenated run of E entries, dealt out in
+    // 64-entry chunks round-robin over the waves (lane = offset in the chunk), so every
+    // lane inserts ~E / 1024 entries however uneven the lists are -- deferred lists are,
+    // and lanes fixed to a list waited on the longest -- and consecutive lanes read
+    // consecutive entries.  Each wave holds the lists' prefix sums in registers (4 lists a
+    // lane): inc[q] ends list 4 * lane + q inside the lane's run, which starts at B.  (Many
+    // lanes then meet one new hot key at once; the probe's bounded wait on a key being
+    // published keeps that key in one slot.)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t inc[4], tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t l = lane * 4u + (uint32_t)q;
+      const uint32_t c = l < n_lists ? counts[(size_t)l * nwin + w] : 0u;
+      tot += c < cap ? c : cap;
+      inc[q] = tot;
+    }
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      x += lane >= (uint32_t)o ? y : 0u;
+    }
+    const uint32_t B = x - tot, E = (uint32_t)__shfl((int)x, 63);
+    const uint32_t nchunk = (E + 63u) >> 6;
+    // entry j0 + lane of the run (wave-converged): its list's words
+    auto locate = [&](uint32_t j0, bool valid) -> const unsigned long long * {
+      const uint32_t j = j0 + lane;
+      uint32_t L = (uint32_t)__popcll(__ballot(B <= j0)) - 1u;  // B is nondecreasing
+      for (;;) {  // a chunk spans few lanes' runs
+        const uint32_t nb = (uint32_t)__shfl((int)B, (int)(L < 63u ? L + 1u : 63u));
+        const bool adv = valid && L < 63u && nb <= j;
+        if (!__any(adv)) break;
+        L += adv ? 1u : 0u;
+      }
+      const uint32_t off = j - (uint32_t)__shfl((int)B, (int)L);
+      const uint32_t e0 = (uint32_t)__shfl((int)inc[0], (int)L), e1 = (uint32_t)__shfl((int)inc[1], (int)L),
+                     e2 = (uint32_t)__shfl((int)inc[2], (int)L);
+      const uint32_t q = (off >= e0 ? 1u : 0u) + (off >= e1 ? 1u : 0u) + (off >= e2 ? 1u : 0u);
+      const uint32_t st = q == 0u ? 0u : q == 1u ? e0 : q == 2u ? e1 : e2;
+      return lists + (((size_t)(L * 4u + q) * nwin + w) * cap + (off - st)) * ew;
+    };
+    for (uint32_t c0 = wv; c0 < nchunk; c0 += 4 * nwv) {  // 4 chunks' loads in flight
+      unsigned long long v[4][4];
+      bool ok[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t c = c0 + (uint32_t)q * nwv;
+        ok[q] = c < nchunk && c * 64u + lane < E;
+        const unsigned long long *e = locate(c * 64u, ok[q]);
+        if (ok[q]) {
+          if (s.narrow) {
+            v[q][0] = e[0];
+            const uint64_t n = e[1];
+            v[q][1] = wide_unpack1(n);
+            v[q][2] = wide_unpack2(n);
+            v[q][3] = e[2];
+          } else {
+            const ulonglong2 a0 = ((const ulonglong2 *)e)[0], a1 = ((const ulonglong2 *)e)[1];
+            v[q][0] = a0.x;
+            v[q][1] = a0.y;
+            v[q][2] = a1.x;
+            v[q][3] = a1.y;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ok[q]) ins(make_ulonglong2(v[q][0], v[q][1]), make_ulonglong2(v[q][2], v[q][3]));
+    }
+  } else
   for (uint32_t l0 = 0; l0 < n_lists; l0 += lists_per_round) {
     const uint32_t l = l0 + threadIdx.x / lpl;
     if (l >= n_lists) continue;
