@@ -87,8 +87,9 @@ typedef struct gpuagg_config {
                                           pointers of this ctx's calls are host pointers          */
 #define GPUAGG_FLAG_NO_WIDE_LISTS 32u  /* 192-bit group-by keys straight into the table with memory-side
                                           atomics, not through per-segment lists (diagnostics) */
-#define GPUAGG_FLAG_WIDE_ENTRIES 512u  /* 32-byte segment-list entries even when the plan's keys have no
-                                          port / DNS fields and 24-byte ones would do (diagnostics) */
+#define GPUAGG_FLAG_NARROW_ENTRIES 512u /* 24-byte segment-list entries instead of 32 when the plan's keys
+                                          have no port / DNS fields: measured C1 -3 %, C4 remote +6 %
+                                          per step (the entries are written as partial sectors)   */
 
 int gpuagg_create(const gpuagg_config *cfg, gpuagg_ctx **out);
 /* Number of gfx950 devices visible to this process (one ctx per device). */

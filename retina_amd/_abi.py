@@ -35,7 +35,7 @@ FLAG_LDS_CUCKOO = 64  # diagnostics: cuckoo LDS IP image even when the radix ima
 FLAG_NO_WIDE_LISTS = 32  # diagnostics: wide group-by keys with memory-side atomics, no segment lists
 FLAG_CPU_BACKEND = 128  # host threads and host memory instead of a device (GPUAGG_FLAG_CPU_BACKEND)
 FLAG_ROW_RADIX = 256  # diagnostics: radix LDS IP images with the row table even when dense ones fit
-FLAG_WIDE_ENTRIES = 512  # diagnostics: 32-byte wide-list entries even when 24-byte narrow ones fit
+FLAG_NARROW_ENTRIES = 512  # 24-byte wide-list entries when the plan's keys have no port / DNS fields
 
 
 class MetricOptions(C.Structure):

@@ -372,7 +372,9 @@ constexpr uint32_t kWideEntryWords = 4, kWideCountShift = 40, kWideHomeShift = 5
 static_assert(kWideHomeShift + kWideSegLog2 == 64, "home field fills the word");
 // Narrow entries (plans with no port option and no DNS family, e.g. C1 / C4 remote): the
 // key's port fields (k1 bits 30-63) and DNS id (k2 bits 0-31) are zero, so k1 and k2 pack
-// into one word d_slot1 << 32 | d_ip -- 24 bytes an entry instead of 32
+// into one word d_slot1 << 32 | d_ip -- 24 bytes an entry instead of 32 (GPUAGG_FLAG_NARROW_ENTRIES:
+// the 24-byte entries are written as partial 32-byte sectors, so they win only while the
+// lists stay small -- C1 -3 % per step, C4 remote +6 %, profiles/round6/exp/r6z6_*, r6fin2_d_*)
 constexpr uint32_t kWideNarrowWords = 3;
 GA_HD uint64_t wide_pack12(uint64_t k1, uint64_t k2) { return ((k1 >> 9) << 32) | (k2 >> 32); }
 GA_HD uint64_t wide_unpack1(uint64_t n) { return (n >> 32) << 9; }

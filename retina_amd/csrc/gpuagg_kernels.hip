@@ -76,7 +76,8 @@ struct DevSparse {
   uint32_t *door;
   uint32_t door_log2;  // 0: no doorkeeper
   // wide keys whose port and DNS fields are zero for every group of the plan (no port
-  // option, no DNS family): list entries drop the zero words (wide_entry_words)
+  // option, no DNS family), with GPUAGG_FLAG_NARROW_ENTRIES: list entries drop the zero
+  // words (list_entry_words)
   uint32_t narrow;
 };
 

@@ -2325,8 +2325,9 @@ int gpuagg_reconcile(gpuagg_ctx *c, const gpuagg_metric_options *opts, size_t n)
       compact &= (groups[g].family == FAM_DNS_REQ || groups[g].family == FAM_DNS_RESP) &&
                  !(groups[g].src_opts & (OPT_IP | OPT_PORT));
   c->sv.compact = compact ? 1u : 0u;
-  // wide keys with no port / DNS fields: 24-byte list entries (kWideNarrowWords)
-  c->sv.narrow = (!compact && !p.need_ports && !p.need_dns && !(c->cfg.flags & GPUAGG_FLAG_WIDE_ENTRIES)) ? 1u : 0u;
+  // wide keys with no port / DNS fields may take 24-byte list entries (kWideNarrowWords) on
+  // request: fewer bytes, but written as partial sectors
+  c->sv.narrow = (!compact && !p.need_ports && !p.need_dns && (c->cfg.flags & GPUAGG_FLAG_NARROW_ENTRIES)) ? 1u : 0u;
   if (c->sparse_slots) {  // probe / fold segments: compact 2^13 slots; wide 2^12 (or the table)
     const uint32_t lg = (uint32_t)__builtin_ctzll(c->sparse_slots);
     c->sv.seg_log2 = compact ? std::min<uint32_t>(lg, kSparseSegLog2)

@@ -188,10 +188,10 @@ def test_hot_key_cache_exact(gpu_device, gen):
                                   sparse_capacity_log2=23,
                                   flags=_abi.FLAG_NO_HOT_KEYS | _abi.FLAG_NO_WIDE_LISTS))
     assert a == c, diff_series(a, c)
-    # C1_REMOTE has no port / DNS labels: its lists take 24-byte entries; the 32-byte form
-    # agrees
+    # C1_REMOTE has no port / DNS labels: the 24-byte list entries (FLAG_NARROW_ENTRIES)
+    # agree with the default 32-byte ones
     d = values_only(engine_series(recs, pods, W.C1_REMOTE, True, gpu_device, host_fed=False, chunks=2,
-                                  sparse_capacity_log2=23, flags=_abi.FLAG_WIDE_ENTRIES))
+                                  sparse_capacity_log2=23, flags=_abi.FLAG_NARROW_ENTRIES))
     assert a == d, diff_series(a, d)
     r = RefCPU(W.C1_REMOTE, pods.endpoints, True, recs.dns)
     r.process(recs)
