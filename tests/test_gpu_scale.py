@@ -215,6 +215,43 @@ def _table_entries(g, device):
     return keys, vals
 
 
+@pytest.mark.parametrize("flags", [0, 512], ids=["32-byte-entries", "24-byte-entries"])
+def test_one_new_key_many_lanes(gpu_device, flags):
+    """A handful of flows, no LDS hot-key cache: every update is a list entry, so the
+    wide fold's balanced lanes meet long runs of the same new key at once.  Each key must
+    take exactly one table slot (the probe waits while a lane publishes it, instead of
+    claiming the next slot), nothing may be dropped, and the series equal the C port."""
+    import torch
+    from retina_amd import _abi
+    pods = W.make_pods(10_000, seed=12)
+    recs = W.gen_records(2_000_000, pods, seed=121, flows=4, flow_zipf=None, n_dst=4)
+    g = make_engine(pods, W.C1_REMOTE, True, gpu_device, sparse_capacity_log2=20,
+                    flags=_abi.FLAG_NO_HOT_KEYS | flags)
+    try:
+        from .helpers import to_device
+        from retina_amd import GpuAgg
+        ts = to_device(recs, gpu_device)
+        half = len(recs) // 2
+        for a, b in ((0, half), (half, len(recs))):
+            g.submit_device(GpuAgg.device_columns(*[x[a:] for x in ts]), b - a)
+        g.sync()
+        assert g.stats()["sparse_dropped"] == 0
+        st = g.state()
+        cap = int(st.sparse_len)
+        out = torch.empty((cap, 5), dtype=torch.int64, device=torch.device("cuda", gpu_device))
+        n = g.sparse_export(out.data_ptr(), cap)
+        keys = out[:n, :3]
+        assert torch.unique(keys, dim=0).shape[0] == n  # one slot per key
+        got = values_only(g.snapshot())
+    finally:
+        g.close()
+    r = RefCPU(W.C1_REMOTE, pods.endpoints, True, recs.dns)
+    r.process(recs)
+    want = r.series()
+    r.close()
+    assert got == want, diff_series(got, want)
+
+
 def test_full_c4_remote_linearity(gpu_device):
     """C4 through the remote context at the full bench size: 100M Zipf(1.2) flow records,
     every update a 192-bit group-by key (~6.7M distinct).  The per-segment lists + LDS
